@@ -1,0 +1,216 @@
+/*
+ * pgx.h -- C-ABI of the MI355X-native batched Panda environment (libpgx.so).
+ *
+ * One handle owns the structure-of-arrays state of N lockstep environments on
+ * one GPU.  Every call is asynchronous on the caller's HIP stream (passed as
+ * void*, NULL = default stream) and takes plain device pointers into
+ * caller-owned buffers (torch tensors on the Python side).  No call allocates,
+ * frees or synchronises on the step path, so a step can be captured in a
+ * hipGraph.
+ *
+ * Reference interfaces each entry point replaces (paths relative to
+ * RaikoPipe/panda-gym):
+ *   pgx_create          PandaReachEnv/PandaPushEnv/PandaPickAndPlaceEnv.__init__
+ *                       panda_gym/envs/panda_tasks.py:37-88, RobotTaskEnv.__init__
+ *                       panda_gym/envs/core.py:264-284, gym registration
+ *                       panda_gym/__init__.py:23-91 (max_episode_steps)
+ *   pgx_reset           RobotTaskEnv.reset core.py:298-308 -> Panda.reset
+ *                       panda.py:290-298, Reach.reset reach.py:63-78,
+ *                       Push.reset push.py:158-176, PickAndPlace.reset
+ *                       pick_and_place.py:252-272
+ *   pgx_step            RobotTaskEnv.step core.py:352-368 -> Panda.set_action
+ *                       panda.py:120-172 (IK: pybullet.py:465-493), PyBullet.step
+ *                       pybullet.py:68-71 (20 x stepSimulation), _get_obs
+ *                       core.py:286-296, Task.is_success / compute_reward
+ *                       reach.py:80-89, + gymnasium TimeLimit and SB3 VecEnv
+ *                       auto-reset (terminal_observation)
+ *   pgx_compute_reward  Task.compute_reward bound as env.compute_reward
+ *                       (core.py:282; reach.py:84-89, push.py:182-187,
+ *                       pick_and_place.py:278-283) over a batch (HER relabel)
+ *   pgx_get_state /     PyBullet.get_joint_angles / get_joint_velocities /
+ *   pgx_set_state       set_joint_angles pybullet.py:313-348,416-435 and
+ *                       RobotTaskEnv.save_state/restore_state core.py:310-336
+ *                       (device snapshots are plain buffer copies)
+ *
+ * Error convention: every call returns PGX_OK (0) or a negative PGX_E_* code;
+ * pgx_last_error() returns a thread-local message for the last failure.
+ */
+#ifndef PGX_H
+#define PGX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PGX_MAX_LINKS 16
+#define PGX_MAX_DOFS 9
+#define PGX_MAX_ROWS 27
+
+#define PGX_OK 0
+#define PGX_E_INVALID -1
+#define PGX_E_HIP -2
+#define PGX_E_UNSUPPORTED -3
+#define PGX_E_NOMEM -4
+
+#define PGX_JOINT_REVOLUTE 0
+#define PGX_JOINT_PRISMATIC 1
+#define PGX_JOINT_FIXED 4
+
+#define PGX_TASK_REACH 0
+#define PGX_TASK_PUSH 1
+#define PGX_TASK_PICK_AND_PLACE 2
+
+#define PGX_CONTROL_EE 0
+#define PGX_CONTROL_JOINTS 1
+
+#define PGX_REWARD_SPARSE 0
+#define PGX_REWARD_DENSE 1
+
+/* solver row kinds (pgx_model.row_kind) */
+#define PGX_ROW_MOTOR 0
+#define PGX_ROW_LIMIT_LOWER 1
+#define PGX_ROW_LIMIT_UPPER 2
+
+/* Multibody description in Bullet link order (built from the URDF by
+ * panda-gym_amd/model.py).  All frames are URDF frames except that link
+ * state is reported at the inertial origin (COM), like getLinkState()[0]. */
+typedef struct pgx_model {
+    int32_t n_links;                       /* links excluding the fixed base */
+    int32_t n_dofs;
+    int32_t ee_link;                       /* Panda.ee_link = 11 (panda.py:68) */
+    int32_t n_rows;                        /* solver rows in Bullet order */
+    int32_t parent[PGX_MAX_LINKS];         /* -1 = base */
+    int32_t jtype[PGX_MAX_LINKS];
+    int32_t dof_of_link[PGX_MAX_LINKS];    /* -1 for fixed joints */
+    int32_t link_of_dof[PGX_MAX_DOFS];
+    int32_t has_limit[PGX_MAX_DOFS];
+    int32_t row_kind[PGX_MAX_ROWS];
+    int32_t row_dof[PGX_MAX_ROWS];
+    int32_t pad0;
+    double jpos[PGX_MAX_LINKS][3];         /* joint origin in parent URDF frame */
+    double jrot[PGX_MAX_LINKS][9];         /* row-major */
+    double axis[PGX_MAX_LINKS][3];         /* joint axis in joint frame */
+    double com[PGX_MAX_LINKS][3];          /* inertial origin in URDF link frame */
+    double mass[PGX_MAX_LINKS];
+    double inertia[PGX_MAX_LINKS][3];      /* principal inertia (Bullet AABB rule) */
+    double lower[PGX_MAX_DOFS];
+    double upper[PGX_MAX_DOFS];
+} pgx_model;
+
+/* Physics / solver constants (pybullet defaults as used by the reference). */
+typedef struct pgx_sim_params {
+    double dt;                    /* 1/500 (pybullet.py:50) */
+    double gravity[3];            /* (0,0,-9.81) (pybullet.py:54) */
+    double lin_damping;           /* btMultiBody default 0.04 */
+    double ang_damping;           /* btMultiBody default 0.04 */
+    double max_coord_vel;         /* btMultiBody::m_maxCoordinateVelocity 100 */
+    double residual_threshold;    /* solver least-squares residual 1e-7 */
+    double erp;                   /* joint-limit violation ERP 0.2 */
+    double limit_max_impulse;     /* btMultiBodyConstraint default 100 */
+    double motor_kp;              /* POSITION_CONTROL default positionGain 0.1 */
+    double motor_kd;              /* POSITION_CONTROL default velocityGain 1.0 */
+    double ik_residual;           /* calculateInverseKinematics residual 1e-4 */
+    double ik_damping;            /* per-joint DLS damping 0.5 */
+    double ik_max_angle;          /* BussIK MaxAngleDLS = pi/4 */
+    int32_t n_substeps;           /* 20 (pybullet.py:25) */
+    int32_t num_iterations;       /* numSolverIterations 50 */
+    int32_t ik_max_iters;         /* maxNumIterations 20 */
+    int32_t flags;                /* PGX_FLAG_* hypotheses (oracle only) */
+} pgx_sim_params;
+
+/* oracle-only modelling switches (documented in DESIGN.md) */
+#define PGX_FLAG_CONSTRAINT_PASS_BIAS 1   /* re-apply velocity bias in the constraint pass */
+#define PGX_FLAG_IK_COM 2                 /* IK targets the link COM instead of the joint pivot */
+#define PGX_FLAG_NO_RESIDUAL_EXIT 4       /* run all solver iterations */
+
+typedef struct pgx_config {
+    int32_t task;                 /* PGX_TASK_* */
+    int32_t control;              /* PGX_CONTROL_* */
+    int32_t reward;               /* PGX_REWARD_* */
+    int32_t n_envs;
+    int32_t max_episode_steps;    /* TimeLimit; 0 = never truncate */
+    int32_t block_gripper;        /* Reach/Push: 1 */
+    int32_t pad0, pad1;
+    uint64_t seed;                /* device Philox key for auto-reset draws */
+    uint64_t env_id_offset;       /* global id of env 0 (multi-GPU sharding) */
+    double base_pos[3];           /* robot base (-0.6,0,0) (panda_tasks.py:85) */
+    double distance_threshold;    /* 0.05 (reach.py:15) */
+    double goal_low[3];
+    double goal_high[3];
+    double joint_forces[PGX_MAX_DOFS]; /* panda.py:63 */
+    double neutral_q[PGX_MAX_DOFS];    /* panda.py:67 */
+    double ee_step;               /* 0.05 (panda.py:235) */
+    double joint_step;            /* 0.05 (panda.py:74) */
+    const pgx_model* model;       /* host pointers, copied at create */
+    const pgx_sim_params* params;
+} pgx_config;
+
+typedef struct pgx_env* pgx_handle;
+
+/* Output buffers of one batched step (device pointers; any may be NULL to skip).
+ * obs [N,obs_dim] f32, achieved/desired [N,3] f32, reward [N] f32,
+ * success/terminated/truncated [N] u8, terminal_obs [N,obs_dim] f32 (obs of the
+ * finished episode, written only for envs that were auto-reset),
+ * terminal_ag [N,3] f32. */
+typedef struct pgx_step_out {
+    float* obs;
+    float* achieved_goal;
+    float* desired_goal;
+    float* reward;
+    uint8_t* success;
+    uint8_t* terminated;
+    uint8_t* truncated;
+    float* terminal_obs;
+    float* terminal_achieved_goal;
+} pgx_step_out;
+
+/* Device-resident state views (SoA, env-minor: x[k*N + env]). */
+typedef struct pgx_state_view {
+    float* q;           /* [n_dofs][N] */
+    float* qd;          /* [n_dofs][N] */
+    double* goal;       /* [3][N] */
+    float* object;      /* [13][N] pos3, quat4 (x,y,z,w), linvel3, angvel3 */
+    int32_t* elapsed;   /* [N] steps in the current episode */
+    uint32_t* episode;  /* [N] episodes finished (RNG counter) */
+} pgx_state_view;
+
+const char* pgx_version(void);
+const char* pgx_last_error(void);
+int pgx_obs_dim(const pgx_config* cfg);
+int pgx_action_dim(const pgx_config* cfg);
+
+int pgx_create(const pgx_config* cfg, int device, pgx_handle* out);
+void pgx_destroy(pgx_handle h);
+int pgx_get_state(pgx_handle h, pgx_state_view* out);
+
+/* Reset envs whose mask byte is non-zero (mask NULL = all).  inject_goal
+ * [N,3] f64 (host-computed PCG64 draws for seeded resets) and inject_object
+ * [N,3] f64 override the device draws where given.  Writes the reset obs. */
+int pgx_reset(pgx_handle h, const uint8_t* env_mask, const double* inject_goal,
+              const double* inject_object, pgx_step_out* out, void* stream);
+
+/* One lockstep env step for all N envs: action [N,A] f32 (device). */
+int pgx_step(pgx_handle h, const float* action, pgx_step_out* out, void* stream);
+
+/* Fill action [N,A] with U[-1,1) from the device Philox stream (benchmark
+ * random policy; counter = (global env id, step)). */
+int pgx_sample_actions(pgx_handle h, float* action, uint64_t step, void* stream);
+
+/* Batched reward for relabelled goals: ag, dg [B,3] f32 device, out [B] f32.
+ * Follows utils.distance (round to 1e-6) in float32 like the reference does
+ * for float32 inputs. */
+int pgx_compute_reward(const float* achieved_goal, const float* desired_goal, int64_t batch,
+                       int32_t reward_type, double distance_threshold, float* out, void* stream);
+
+/* Single-kernel copies of the whole SoA state (snapshot = save_state). */
+int pgx_state_bytes(pgx_handle h, int64_t* nbytes);
+int pgx_save_state(pgx_handle h, void* dst_device, void* stream);
+int pgx_restore_state(pgx_handle h, const void* src_device, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PGX_H */

@@ -1,0 +1,183 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes wrapper of the fp64 CPU oracle (oracle/_build/libpgx_oracle.so).
+
+Importable only from tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg.  The product path (panda-gym_amd) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from typing import Optional, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libpgx_oracle.so")
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+        _lib.pgxo_ik.restype = C.c_int
+        _lib.pgxo_distance_f32_f64.restype = C.c_double
+        _lib.pgxo_distance_f32_f32.restype = C.c_float
+        _lib.pgxo_vec_step.restype = C.c_int
+        _lib.pgxo_vec_reset.restype = C.c_int
+    return _lib
+
+
+class PgxoMotor(C.Structure):
+    _fields_ = [("target_q", C.c_double), ("target_qd", C.c_double), ("kp", C.c_double), ("kd", C.c_double),
+                ("max_impulse", C.c_double)]
+
+
+class PgxoStats(C.Structure):
+    _fields_ = [("solver_iterations", C.c_int32), ("ik_iterations", C.c_int32), ("ik_residual", C.c_double)]
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _d(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _base(base):
+    return (C.c_double * 3)(*base)
+
+
+def fk(model, q, base=(0.0, 0.0, 0.0)) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    n = model.n_links
+    com = np.zeros((n, 3))
+    rot = np.zeros((n, 9))
+    org = np.zeros((n, 3))
+    lib().pgxo_fk(C.byref(model), _base(base), _p(_d(q)), _p(com), _p(rot), _p(org))
+    return com, rot.reshape(n, 3, 3), org
+
+
+def link_velocity(model, q, qd, link, base=(0.0, 0.0, 0.0)):
+    lin, ang = np.zeros(3), np.zeros(3)
+    lib().pgxo_link_velocity(C.byref(model), _base(base), _p(_d(q)), _p(_d(qd)), link, _p(lin), _p(ang))
+    return lin, ang
+
+
+def mass_matrix(model, q, base=(0.0, 0.0, 0.0)):
+    nd = model.n_dofs
+    M = np.zeros((nd, nd))
+    lib().pgxo_mass_matrix(C.byref(model), _base(base), _p(_d(q)), _p(M))
+    return M
+
+
+def bias(model, params, q, qd, with_gravity=True, base=(0.0, 0.0, 0.0)):
+    b = np.zeros(model.n_dofs)
+    lib().pgxo_bias(C.byref(model), C.byref(params), _base(base), _p(_d(q)), _p(_d(qd)), int(with_gravity), _p(b))
+    return b
+
+
+def ik(model, params, q_start, link, target_pos, target_orn, base=(0.0, 0.0, 0.0)):
+    out = np.zeros(model.n_dofs)
+    st = PgxoStats()
+    lib().pgxo_ik(C.byref(model), C.byref(params), _base(base), _p(_d(q_start)), link, _p(_d(target_pos)),
+                  _p(_d(target_orn)), _p(out), C.byref(st))
+    return out, st
+
+
+def make_motors(n, entries):
+    arr = (PgxoMotor * n)()
+    for d, e in entries.items():
+        arr[d].target_q, arr[d].target_qd, arr[d].kp, arr[d].kd, arr[d].max_impulse = e
+    return arr
+
+
+def substep(model, params, q, qd, motors, base=(0.0, 0.0, 0.0)):
+    q = _d(q).copy()
+    qd = _d(qd).copy()
+    st = PgxoStats()
+    lib().pgxo_substep(C.byref(model), C.byref(params), _base(base), _p(q), _p(qd), motors, C.byref(st))
+    return q, qd, st
+
+
+def distance_f32_f64(ag, g) -> float:
+    a = np.ascontiguousarray(ag, dtype=np.float32)
+    b = _d(g)
+    return lib().pgxo_distance_f32_f64(_p(a), _p(b))
+
+
+def compute_reward_f32(ag, dg, reward_type, thr=0.05):
+    ag = np.ascontiguousarray(ag, dtype=np.float32).reshape(-1, 3)
+    dg = np.ascontiguousarray(dg, dtype=np.float32).reshape(-1, 3)
+    out = np.zeros(len(ag), dtype=np.float32)
+    lib().pgxo_compute_reward_f32(_p(ag), _p(dg), C.c_int64(len(ag)), reward_type, C.c_double(thr), _p(out))
+    return out
+
+
+def philox(ctr, key):
+    c = (C.c_uint32 * 4)(*ctr)
+    k = (C.c_uint32 * 2)(*key)
+    o = (C.c_uint32 * 4)()
+    lib().pgxo_philox(c, k, o)
+    return list(o)
+
+
+class OracleVecEnv:
+    """Host-side fp64 mirror of one libpgx handle (AoS state), same vec-env semantics."""
+
+    def __init__(self, cfg, n: int):
+        self.cfg = cfg
+        self.n = n
+        self.nd = cfg.model.contents.n_dofs
+        from panda_gym_amd.abi import EnvSpec  # noqa: F401  (layout helpers only)
+        self.od = 6 + (0 if cfg.block_gripper else 1) + (0 if cfg.task == 0 else 12)
+        self.ad = (3 if cfg.control == 0 else 7) + (0 if cfg.block_gripper else 1)
+        self.q = np.zeros((n, self.nd))
+        self.qd = np.zeros((n, self.nd))
+        self.goal = np.zeros((n, 3))
+        self.obj = np.zeros((n, 13))
+        self.elapsed = np.zeros(n, dtype=np.int32)
+        self.episode = np.zeros(n, dtype=np.uint32)
+
+    def _bufs(self):
+        n, od = self.n, self.od
+        return dict(obs=np.zeros((n, od), np.float32), ag=np.zeros((n, 3), np.float32),
+                    dg=np.zeros((n, 3), np.float32))
+
+    def reset(self, mask: Optional[np.ndarray] = None, inject_goal: Optional[np.ndarray] = None):
+        b = self._bufs()
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        g = None if inject_goal is None else _d(inject_goal)
+        rc = lib().pgxo_vec_reset(C.byref(self.cfg), C.c_int64(self.n), None if m is None else _p(m),
+                                  None if g is None else _p(g), None, _p(self.q), _p(self.qd), _p(self.goal),
+                                  _p(self.obj), _p(self.elapsed), _p(self.episode), _p(b["obs"]), _p(b["ag"]),
+                                  _p(b["dg"]))
+        assert rc == 0, rc
+        return b
+
+    def step(self, action: np.ndarray):
+        a = np.ascontiguousarray(action, dtype=np.float32)
+        b = self._bufs()
+        n = self.n
+        b.update(reward=np.zeros(n, np.float32), success=np.zeros(n, np.uint8), terminated=np.zeros(n, np.uint8),
+                 truncated=np.zeros(n, np.uint8), terminal_obs=np.zeros((n, self.od), np.float32))
+        rc = lib().pgxo_vec_step(C.byref(self.cfg), C.c_int64(n), _p(self.q), _p(self.qd), _p(self.goal),
+                                 _p(self.obj), _p(self.elapsed), _p(self.episode), _p(a), _p(b["obs"]), _p(b["ag"]),
+                                 _p(b["dg"]), _p(b["reward"]), _p(b["success"]), _p(b["terminated"]),
+                                 _p(b["truncated"]), _p(b["terminal_obs"]))
+        assert rc == 0, rc
+        return b
+
+    def sample_actions(self, step: int) -> np.ndarray:
+        a = np.zeros((self.n, self.ad), np.float32)
+        lib().pgxo_sample_actions(C.byref(self.cfg), C.c_int64(self.n), C.c_uint64(step), _p(a))
+        return a

@@ -1,0 +1,70 @@
+/*
+ * pgx_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * fp64 CPU restatement of the reference's per-step hot path, used as the
+ * checker for the HIP kernels (tests/, __graft_entry__.smoke(), bench.py's
+ * cpu_baseline leg).  Never linked into libpgx.so.  See oracle/pgx_oracle.c
+ * for the per-function reference citations and DESIGN.md for how it is pinned.
+ */
+#ifndef PGX_ORACLE_H
+#define PGX_ORACLE_H
+
+#include <stdint.h>
+#include "../include/pgx.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pgxo_motor {
+    double target_q;
+    double target_qd;
+    double kp;
+    double kd;
+    double max_impulse;   /* 0 = motor disabled */
+} pgxo_motor;
+
+/* diagnostics of the last substep (optional) */
+typedef struct pgxo_stats {
+    int32_t solver_iterations;
+    int32_t ik_iterations;
+    double ik_residual;
+} pgxo_stats;
+
+void pgxo_fk(const pgx_model* m, const double base[3], const double* q, double* com_pos,
+             double* rot, double* origin);
+void pgxo_link_velocity(const pgx_model* m, const double base[3], const double* q, const double* qd,
+                        int link, double lin[3], double ang[3]);
+void pgxo_mass_matrix(const pgx_model* m, const double base[3], const double* q, double* M);
+void pgxo_bias(const pgx_model* m, const pgx_sim_params* p, const double base[3], const double* q,
+               const double* qd, int with_gravity, double* b);
+int pgxo_ik(const pgx_model* m, const pgx_sim_params* p, const double base[3], const double* q_start,
+            int link, const double target_pos[3], const double target_orn[4], double* q_out,
+            pgxo_stats* st);
+void pgxo_substep(const pgx_model* m, const pgx_sim_params* p, const double base[3], double* q,
+                  double* qd, const pgxo_motor* motors, pgxo_stats* st);
+
+/* reward / success, reference utils.distance + Reach.is_success / compute_reward */
+double pgxo_distance_f32_f64(const float ag[3], const double g[3]);
+float pgxo_distance_f32_f32(const float ag[3], const float g[3]);
+void pgxo_compute_reward_f32(const float* ag, const float* dg, int64_t n, int reward_type,
+                             double thr, float* out);
+
+/* Philox4x32-10 (device RNG restated for parity of auto-reset draws) */
+void pgxo_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+
+/* Batched env step with the kernel's vec-env semantics (TimeLimit + auto-reset).
+ * State arrays are AoS per env here: q[N*nd], qd[N*nd], goal[N*3], obj[N*13]. */
+int pgxo_vec_step(const pgx_config* cfg, int64_t n, double* q, double* qd, double* goal,
+                  double* obj, int32_t* elapsed, uint32_t* episode, const float* action,
+                  float* obs, float* ag, float* dg, float* reward, uint8_t* success,
+                  uint8_t* terminated, uint8_t* truncated, float* terminal_obs);
+int pgxo_vec_reset(const pgx_config* cfg, int64_t n, const uint8_t* mask, const double* inject_goal,
+                   const double* inject_obj, double* q, double* qd, double* goal, double* obj,
+                   int32_t* elapsed, uint32_t* episode, float* obs, float* ag, float* dg);
+void pgxo_sample_actions(const pgx_config* cfg, int64_t n, uint64_t step, float* action);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

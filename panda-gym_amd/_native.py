@@ -1,0 +1,63 @@
+"""Loader for libpgx.so, the HIP/gfx950 implementation of the env step (C-ABI in include/pgx.h).
+
+The product path has no CPU fallback: if the shared library is missing or does
+not export the full ABI, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from .abi import PgxConfig, PgxStepOut, PgxStateView
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpgx.so")
+
+EXPORTS = [
+    "pgx_version", "pgx_last_error", "pgx_obs_dim", "pgx_action_dim", "pgx_create", "pgx_destroy",
+    "pgx_get_state", "pgx_reset", "pgx_step", "pgx_sample_actions", "pgx_compute_reward",
+    "pgx_state_bytes", "pgx_save_state", "pgx_restore_state",
+]
+
+
+class PgxError(RuntimeError):
+    """A libpgx call returned a negative status (message from pgx_last_error)."""
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load libpgx.so once; raise loudly if it is absent (build with __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise PgxError(f"libpgx.so not found at {path}: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = C.CDLL(path)
+    for name in EXPORTS:
+        if not hasattr(lib, name):
+            raise PgxError(f"libpgx.so does not export {name}")
+    lib.pgx_version.restype = C.c_char_p
+    lib.pgx_last_error.restype = C.c_char_p
+    lib.pgx_obs_dim.argtypes = [C.POINTER(PgxConfig)]
+    lib.pgx_action_dim.argtypes = [C.POINTER(PgxConfig)]
+    lib.pgx_create.argtypes = [C.POINTER(PgxConfig), C.c_int, C.POINTER(C.c_void_p)]
+    lib.pgx_destroy.argtypes = [C.c_void_p]
+    lib.pgx_destroy.restype = None
+    lib.pgx_get_state.argtypes = [C.c_void_p, C.POINTER(PgxStateView)]
+    lib.pgx_reset.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(PgxStepOut), C.c_void_p]
+    lib.pgx_step.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(PgxStepOut), C.c_void_p]
+    lib.pgx_sample_actions.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+    lib.pgx_compute_reward.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_double, C.c_void_p,
+                                       C.c_void_p]
+    lib.pgx_state_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
+    lib.pgx_save_state.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.pgx_restore_state.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().pgx_last_error().decode(errors="replace")
+        raise PgxError(f"{what} failed ({rc}): {msg}")

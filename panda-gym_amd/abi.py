@@ -1,0 +1,199 @@
+"""ctypes mirror of include/pgx.h and builders for its structs.
+
+Only plain C structs cross the boundary (no torch types): the same structs are
+handed to libpgx.so (the HIP product) and, in tests, to the oracle library.
+Default constants are the ones the reference uses; each carries its citation.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from .model import Model, MAX_LINKS, MAX_DOFS, load_model
+
+MAX_ROWS = 27
+
+TASK_REACH, TASK_PUSH, TASK_PICK_AND_PLACE = 0, 1, 2
+CONTROL_EE, CONTROL_JOINTS = 0, 1
+REWARD_SPARSE, REWARD_DENSE = 0, 1
+
+FLAG_CONSTRAINT_PASS_BIAS = 1
+FLAG_IK_COM = 2
+FLAG_NO_RESIDUAL_EXIT = 4
+
+PGX_OK = 0
+
+
+class PgxModel(C.Structure):
+    _fields_ = [
+        ("n_links", C.c_int32), ("n_dofs", C.c_int32), ("ee_link", C.c_int32), ("n_rows", C.c_int32),
+        ("parent", C.c_int32 * MAX_LINKS), ("jtype", C.c_int32 * MAX_LINKS),
+        ("dof_of_link", C.c_int32 * MAX_LINKS), ("link_of_dof", C.c_int32 * MAX_DOFS),
+        ("has_limit", C.c_int32 * MAX_DOFS), ("row_kind", C.c_int32 * MAX_ROWS),
+        ("row_dof", C.c_int32 * MAX_ROWS), ("pad0", C.c_int32),
+        ("jpos", (C.c_double * 3) * MAX_LINKS), ("jrot", (C.c_double * 9) * MAX_LINKS),
+        ("axis", (C.c_double * 3) * MAX_LINKS), ("com", (C.c_double * 3) * MAX_LINKS),
+        ("mass", C.c_double * MAX_LINKS), ("inertia", (C.c_double * 3) * MAX_LINKS),
+        ("lower", C.c_double * MAX_DOFS), ("upper", C.c_double * MAX_DOFS),
+    ]
+
+
+class PgxSimParams(C.Structure):
+    _fields_ = [
+        ("dt", C.c_double), ("gravity", C.c_double * 3), ("lin_damping", C.c_double),
+        ("ang_damping", C.c_double), ("max_coord_vel", C.c_double), ("residual_threshold", C.c_double),
+        ("erp", C.c_double), ("limit_max_impulse", C.c_double), ("motor_kp", C.c_double),
+        ("motor_kd", C.c_double), ("ik_residual", C.c_double), ("ik_damping", C.c_double),
+        ("ik_max_angle", C.c_double), ("n_substeps", C.c_int32), ("num_iterations", C.c_int32),
+        ("ik_max_iters", C.c_int32), ("flags", C.c_int32),
+    ]
+
+
+class PgxConfig(C.Structure):
+    _fields_ = [
+        ("task", C.c_int32), ("control", C.c_int32), ("reward", C.c_int32), ("n_envs", C.c_int32),
+        ("max_episode_steps", C.c_int32), ("block_gripper", C.c_int32), ("pad0", C.c_int32),
+        ("pad1", C.c_int32), ("seed", C.c_uint64), ("env_id_offset", C.c_uint64),
+        ("base_pos", C.c_double * 3), ("distance_threshold", C.c_double),
+        ("goal_low", C.c_double * 3), ("goal_high", C.c_double * 3),
+        ("joint_forces", C.c_double * MAX_DOFS), ("neutral_q", C.c_double * MAX_DOFS),
+        ("ee_step", C.c_double), ("joint_step", C.c_double),
+        ("model", C.POINTER(PgxModel)), ("params", C.POINTER(PgxSimParams)),
+    ]
+
+
+class PgxStepOut(C.Structure):
+    _fields_ = [
+        ("obs", C.c_void_p), ("achieved_goal", C.c_void_p), ("desired_goal", C.c_void_p),
+        ("reward", C.c_void_p), ("success", C.c_void_p), ("terminated", C.c_void_p),
+        ("truncated", C.c_void_p), ("terminal_obs", C.c_void_p), ("terminal_achieved_goal", C.c_void_p),
+    ]
+
+
+class PgxStateView(C.Structure):
+    _fields_ = [
+        ("q", C.c_void_p), ("qd", C.c_void_p), ("goal", C.c_void_p), ("object", C.c_void_p),
+        ("elapsed", C.c_void_p), ("episode", C.c_void_p),
+    ]
+
+
+def make_model(model: Model, ee_link: int = 11) -> PgxModel:
+    m = PgxModel()
+    m.n_links, m.n_dofs, m.ee_link = model.n_links, model.n_dofs, ee_link
+    assert model.n_links <= MAX_LINKS and model.n_dofs <= MAX_DOFS
+    kinds, dofs = model.row_table()
+    m.n_rows = len(kinds)
+    for i in range(model.n_links):
+        m.parent[i] = model.parent[i]
+        m.jtype[i] = model.jtype[i]
+        m.dof_of_link[i] = model.dof_of_link[i]
+        for c in range(3):
+            m.jpos[i][c] = model.jpos[i][c]
+            m.axis[i][c] = model.axis[i][c]
+            m.com[i][c] = model.com[i][c]
+            m.inertia[i][c] = model.inertia[i][c]
+        for c in range(9):
+            m.jrot[i][c] = model.jrot[i][c]
+        m.mass[i] = model.mass[i]
+    for d in range(model.n_dofs):
+        m.link_of_dof[d] = model.link_of_dof[d]
+        m.has_limit[d] = model.has_limit[d]
+        m.lower[d] = model.lower[d]
+        m.upper[d] = model.upper[d]
+    for r, (k, d) in enumerate(zip(kinds, dofs)):
+        m.row_kind[r], m.row_dof[r] = int(k), int(d)
+    return m
+
+
+def default_sim_params(n_substeps: int = 20, flags: int = 0) -> PgxSimParams:
+    """pybullet defaults as configured by the reference's PyBullet facade."""
+    p = PgxSimParams()
+    p.dt = 1.0 / 500                         # panda_gym/pybullet.py:50
+    p.gravity[0], p.gravity[1], p.gravity[2] = 0.0, 0.0, -9.81   # pybullet.py:54
+    p.lin_damping = 0.04                     # btMultiBody m_linearDamping
+    p.ang_damping = 0.04                     # btMultiBody m_angularDamping
+    p.max_coord_vel = 100.0                  # btMultiBody m_maxCoordinateVelocity
+    p.residual_threshold = 1e-7              # pybullet solverResidualThreshold
+    p.erp = 0.2                              # btContactSolverInfo m_erp
+    p.limit_max_impulse = 100.0              # btMultiBodyConstraint m_maxAppliedImpulse
+    p.motor_kp = 0.1                         # setJointMotorControlArray positionGains default
+    p.motor_kd = 1.0                         # setJointMotorControlArray velocityGains default
+    p.ik_residual = 1e-4                     # calculateInverseKinematics residualThreshold
+    p.ik_damping = 0.5                       # per-joint DLS damping default
+    p.ik_max_angle = math.pi / 4             # BussIK Jacobian::MaxAngleDLS
+    p.n_substeps = n_substeps                # pybullet.py:25
+    p.num_iterations = 50                    # pybullet numSolverIterations
+    p.ik_max_iters = 20                      # calculateInverseKinematics maxNumIterations
+    p.flags = flags
+    return p
+
+
+NEUTRAL_Q = [0.0, -0.3, 0.0, -2.2, 0.0, 2.0, math.pi / 4, 0.0, 0.0]        # panda.py:67
+JOINT_FORCES = [87.0, 87.0, 87.0, 87.0, 12.0, 120.0, 120.0, 170.0, 170.0]  # panda.py:63
+
+
+@dataclass
+class EnvSpec:
+    """Task/robot configuration of one registered env id (panda_gym/__init__.py:23-91)."""
+
+    task: int = TASK_REACH
+    control: int = CONTROL_EE
+    reward: int = REWARD_SPARSE
+    max_episode_steps: int = 50
+    block_gripper: bool = True
+    base_pos: Sequence[float] = (-0.6, 0.0, 0.0)       # panda_tasks.py:49,66,85
+    distance_threshold: float = 0.05                   # reach.py:15
+    goal_range: float = 0.3                            # reach.py:16
+
+    def goal_bounds(self):
+        if self.task == TASK_REACH:   # reach.py:24-25
+            g = self.goal_range
+            return [-g / 2, -g / 2, 0.0], [g / 2, g / 2, g]
+        if self.task == TASK_PUSH:    # push.py:111-112 (+ z offset object_size/2 added at sample)
+            return [-0.15, -0.15, 0.0], [0.15, 0.15, 0.0]
+        return [-0.15, -0.15, 0.0], [0.15, 0.15, 0.2]  # pick_and_place.py:211-212
+
+    @property
+    def obs_dim(self) -> int:
+        return 6 + (0 if self.block_gripper else 1) + (0 if self.task == TASK_REACH else 12)
+
+    @property
+    def action_dim(self) -> int:
+        return (3 if self.control == CONTROL_EE else 7) + (0 if self.block_gripper else 1)
+
+
+def make_config(spec: EnvSpec, n_envs: int, model: PgxModel, params: PgxSimParams, seed: int = 0,
+                env_id_offset: int = 0) -> PgxConfig:
+    c = PgxConfig()
+    c.task, c.control, c.reward = spec.task, spec.control, spec.reward
+    c.n_envs = n_envs
+    c.max_episode_steps = spec.max_episode_steps
+    c.block_gripper = 1 if spec.block_gripper else 0
+    c.seed = seed & 0xFFFFFFFFFFFFFFFF
+    c.env_id_offset = env_id_offset
+    for i in range(3):
+        c.base_pos[i] = spec.base_pos[i]
+    c.distance_threshold = spec.distance_threshold
+    lo, hi = spec.goal_bounds()
+    for i in range(3):
+        c.goal_low[i], c.goal_high[i] = lo[i], hi[i]
+    for d in range(MAX_DOFS):
+        c.joint_forces[d] = JOINT_FORCES[d]
+        c.neutral_q[d] = NEUTRAL_Q[d]
+    c.ee_step = 0.05        # panda.py:235
+    c.joint_step = 0.05     # panda.py:74 max_change_position
+    c.model = C.pointer(model)
+    c.params = C.pointer(params)
+    return c
+
+
+def ptr(a: Optional[np.ndarray]):
+    """Raw pointer of a host numpy array (or None)."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(C.c_void_p)

@@ -1,0 +1,338 @@
+/*
+ * pgx_api.cpp -- C-ABI of libpgx.so (declared in include/pgx.h).
+ *
+ * Host side of the drop-in boundary: validates the robot model against the
+ * topology the kernels are compiled for, folds the fixed links rigidly
+ * attached to panda_link7 into one composite body (exact for inertia; their
+ * COM offsets are kept for Bullet's per-link damping), owns one device
+ * allocation holding the SoA state of all N envs, and launches the kernels on
+ * the caller's stream.  Nothing here allocates or synchronises on the step path.
+ */
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/pgx.h"
+#include "pgx_dev.h"
+#include "pgx_rows.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) return fail(PGX_E_HIP, "%s: %s", what, hipGetErrorString(e));
+    return PGX_OK;
+}
+
+/* 3x3 helpers in double for model preprocessing */
+void m3mul(const double* A, const double* B, double* C) {
+    double t[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) t[i * 3 + j] = A[i * 3] * B[j] + A[i * 3 + 1] * B[3 + j] + A[i * 3 + 2] * B[6 + j];
+    std::memcpy(C, t, sizeof t);
+}
+void m3v(const double* A, const double* v, double* o) {
+    double t[3];
+    for (int i = 0; i < 3; i++) t[i] = A[i * 3] * v[0] + A[i * 3 + 1] * v[1] + A[i * 3 + 2] * v[2];
+    std::memcpy(o, t, sizeof t);
+}
+
+}  // namespace
+
+struct pgx_env {
+    int device;
+    PgxDevModel dm;
+    PgxDevEnv de;
+    PgxDevState ds;
+    void* blob;
+    size_t blob_bytes;
+};
+
+extern "C" {
+
+const char* pgx_version(void) { return "pgx 0.1.0 (gfx950)"; }
+const char* pgx_last_error(void) { return g_err.c_str(); }
+
+int pgx_obs_dim(const pgx_config* c) {
+    if (!c) return PGX_E_INVALID;
+    return 6 + (c->block_gripper ? 0 : 1) + (c->task == PGX_TASK_REACH ? 0 : 12);
+}
+int pgx_action_dim(const pgx_config* c) {
+    if (!c) return PGX_E_INVALID;
+    return (c->control == PGX_CONTROL_EE ? 3 : 7) + (c->block_gripper ? 0 : 1);
+}
+
+/* Fold the model into the kernel's constant tables. */
+static int build_dev_model(const pgx_config* cfg, PgxDevModel* dm) {
+    const pgx_model* m = cfg->model;
+    const pgx_sim_params* p = cfg->params;
+    std::memset(dm, 0, sizeof *dm);
+    if (m->n_dofs != PGX_NJ) return fail(PGX_E_UNSUPPORTED, "kernel is built for 7 arm dofs, model has %d", m->n_dofs);
+    for (int j = 0; j < PGX_NJ; j++) {
+        if (m->parent[j] != j - 1 || m->jtype[j] != PGX_JOINT_REVOLUTE || m->dof_of_link[j] != j)
+            return fail(PGX_E_UNSUPPORTED, "link %d is not the %d-th revolute joint of a serial chain", j, j);
+        if (m->axis[j][0] != 0.0 || m->axis[j][1] != 0.0 || m->axis[j][2] != 1.0)
+            return fail(PGX_E_UNSUPPORTED, "joint %d axis is not URDF z", j);
+        if (!m->has_limit[j]) return fail(PGX_E_UNSUPPORTED, "joint %d has no limit constraint", j);
+    }
+    if (m->n_rows != PGX_N_ROWS) return fail(PGX_E_UNSUPPORTED, "model has %d solver rows, kernel %d", m->n_rows, PGX_N_ROWS);
+    for (int r = 0; r < PGX_N_ROWS; r++)
+        if (((m->row_kind[r] << 4) | m->row_dof[r]) != kPgxRowCode[r])
+            return fail(PGX_E_UNSUPPORTED, "solver row %d differs from the compiled row order", r);
+    if (m->ee_link < PGX_NJ || m->ee_link >= m->n_links) return fail(PGX_E_INVALID, "ee_link %d", m->ee_link);
+
+    /* transforms of every fixed link relative to panda_link7's URDF frame */
+    double R[PGX_MAX_LINKS][9], O[PGX_MAX_LINKS][3];
+    const int last = PGX_NJ - 1;
+    const double I9[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    std::memcpy(R[last], I9, sizeof I9);
+    std::memset(O[last], 0, sizeof O[last]);
+    for (int i = PGX_NJ; i < m->n_links; i++) {
+        int par = m->parent[i];
+        if (m->jtype[i] != PGX_JOINT_FIXED || par < last || par >= i)
+            return fail(PGX_E_UNSUPPORTED, "link %d is not a fixed descendant of link %d", i, last);
+        m3mul(R[par], m->jrot[i], R[i]);
+        m3v(R[par], m->jpos[i], O[i]);
+        for (int c = 0; c < 3; c++) O[i][c] += O[par][c];
+    }
+    /* composite of the link-7 group: mass, COM, inertia about COM, sum of own inertias */
+    double mt = 0, cm[3] = {0, 0, 0};
+    double comp[PGX_MAX_LINKS][3];
+    for (int i = last; i < m->n_links; i++) {
+        m3v(R[i], m->com[i], comp[i]);
+        for (int c = 0; c < 3; c++) comp[i][c] += O[i][c];
+        mt += m->mass[i];
+        for (int c = 0; c < 3; c++) cm[c] += m->mass[i] * comp[i][c];
+    }
+    if (mt <= 0) return fail(PGX_E_INVALID, "link-7 group has no mass");
+    for (int c = 0; c < 3; c++) cm[c] /= mt;
+    double Ic[9] = {0}, Io[9] = {0};
+    int nd = 0;
+    for (int i = last; i < m->n_links; i++) {
+        double mi = m->mass[i];
+        if (mi == 0.0) continue;
+        double Iw[9];
+        for (int a = 0; a < 3; a++)
+            for (int b = 0; b < 3; b++)
+                Iw[a * 3 + b] = R[i][a * 3] * m->inertia[i][0] * R[i][b * 3] +
+                                R[i][a * 3 + 1] * m->inertia[i][1] * R[i][b * 3 + 1] +
+                                R[i][a * 3 + 2] * m->inertia[i][2] * R[i][b * 3 + 2];
+        double r[3] = {comp[i][0] - cm[0], comp[i][1] - cm[1], comp[i][2] - cm[2]};
+        double rr = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+        for (int a = 0; a < 3; a++)
+            for (int b = 0; b < 3; b++) {
+                Io[a * 3 + b] += Iw[a * 3 + b];
+                Ic[a * 3 + b] += Iw[a * 3 + b] + mi * ((a == b ? rr : 0.0) - r[a] * r[b]);
+            }
+        if (nd >= PGX_MAX_DAMP) return fail(PGX_E_UNSUPPORTED, "too many massive bodies on link 7");
+        for (int c = 0; c < 3; c++) dm->dpos[nd][c] = (float)comp[i][c];
+        dm->dmass[nd] = (float)mi;
+        nd++;
+    }
+    dm->ndamp = nd;
+    auto pack = [](const double* S, float* o) {
+        o[0] = (float)S[0]; o[1] = (float)S[4]; o[2] = (float)S[8];
+        o[3] = (float)S[1]; o[4] = (float)S[2]; o[5] = (float)S[5];
+    };
+    pack(Ic, dm->i6c);
+    pack(Io, dm->i6own);
+    for (int j = 0; j < PGX_NJ; j++) {
+        for (int c = 0; c < 3; c++) dm->jp[j][c] = (float)m->jpos[j][c];
+        for (int c = 0; c < 9; c++) dm->jr[j][c] = (float)m->jrot[j][c];
+        if (j < last) {
+            for (int c = 0; c < 3; c++) dm->com[j][c] = (float)m->com[j][c];
+            for (int c = 0; c < 3; c++) dm->inertia[j][c] = (float)m->inertia[j][c];
+            dm->mass[j] = (float)m->mass[j];
+        }
+        dm->lower[j] = (float)m->lower[j];
+        dm->upper[j] = (float)m->upper[j];
+        dm->max_impulse[j] = (float)(cfg->joint_forces[j] * p->dt);
+        dm->neutral_q[j] = (float)cfg->neutral_q[j];
+    }
+    for (int c = 0; c < 3; c++) dm->com[last][c] = (float)cm[c];
+    dm->mass[last] = (float)mt;
+    const int ee = m->ee_link;
+    for (int c = 0; c < 3; c++) {
+        dm->ee_pivot[c] = (float)O[ee][c];
+        dm->ee_com[c] = (float)comp[ee][c];
+        dm->base[c] = (float)cfg->base_pos[c];
+        dm->gravity[c] = (float)p->gravity[c];
+    }
+    for (int c = 0; c < 9; c++) dm->ee_rot[c] = (float)R[ee][c];
+    dm->dt = (float)p->dt;
+    dm->inv_dt = (float)(1.0 / p->dt);
+    dm->lin_damp = (float)p->lin_damping;
+    dm->ang_damp = (float)p->ang_damping;
+    dm->max_vel = (float)p->max_coord_vel;
+    dm->residual_thr = (float)p->residual_threshold;
+    dm->erp = (float)p->erp;
+    dm->limit_max_imp = (float)p->limit_max_impulse;
+    dm->kp = (float)p->motor_kp;
+    dm->kd = (float)p->motor_kd;
+    dm->ik_residual = (float)p->ik_residual;
+    dm->ik_damping = (float)p->ik_damping;
+    dm->ik_max_angle = (float)p->ik_max_angle;
+    dm->n_substeps = p->n_substeps;
+    dm->num_iterations = p->num_iterations;
+    dm->ik_max_iters = p->ik_max_iters;
+    dm->ee_step = (float)cfg->ee_step;
+    dm->joint_step = (float)cfg->joint_step;
+    if (p->flags != 0) return fail(PGX_E_UNSUPPORTED, "modelling flags are oracle-only");
+    return PGX_OK;
+}
+
+int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
+    if (!cfg || !out || !cfg->model || !cfg->params) return fail(PGX_E_INVALID, "null argument");
+    *out = nullptr;
+    if (cfg->n_envs <= 0) return fail(PGX_E_INVALID, "n_envs must be > 0 (got %d)", cfg->n_envs);
+    if (cfg->task != PGX_TASK_REACH)
+        return fail(PGX_E_UNSUPPORTED, "task %d: only PGX_TASK_REACH is implemented by this build", cfg->task);
+    if (cfg->control != PGX_CONTROL_EE && cfg->control != PGX_CONTROL_JOINTS)
+        return fail(PGX_E_INVALID, "control %d", cfg->control);
+    if (cfg->reward != PGX_REWARD_SPARSE && cfg->reward != PGX_REWARD_DENSE)
+        return fail(PGX_E_INVALID, "reward %d", cfg->reward);
+    pgx_env* h = new pgx_env();
+    h->device = device;
+    int rc = build_dev_model(cfg, &h->dm);
+    if (rc) { delete h; return rc; }
+    PgxDevEnv& e = h->de;
+    e.task = cfg->task;
+    e.control = cfg->control;
+    e.reward = cfg->reward;
+    e.n_envs = cfg->n_envs;
+    e.max_episode_steps = cfg->max_episode_steps;
+    e.block_gripper = cfg->block_gripper;
+    e.obs_dim = pgx_obs_dim(cfg);
+    e.action_dim = pgx_action_dim(cfg);
+    e.seed = cfg->seed;
+    e.env_id_offset = cfg->env_id_offset;
+    e.distance_threshold = cfg->distance_threshold;
+    for (int c = 0; c < 3; c++) { e.goal_low[c] = cfg->goal_low[c]; e.goal_high[c] = cfg->goal_high[c]; }
+
+    rc = hip_check(hipSetDevice(device), "hipSetDevice");
+    if (rc) { delete h; return rc; }
+    const size_t N = (size_t)cfg->n_envs;
+    auto align = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    size_t off_goal = 0, off_q = align(off_goal + 3 * N * 8), off_qd = align(off_q + PGX_NJ * N * 4),
+           off_obj = align(off_qd + PGX_NJ * N * 4), off_el = align(off_obj + 13 * N * 4),
+           off_ep = align(off_el + N * 4), total = align(off_ep + N * 4);
+    rc = hip_check(hipMalloc(&h->blob, total), "hipMalloc(state)");
+    if (rc) { delete h; return rc; }
+    h->blob_bytes = total;
+    char* b = (char*)h->blob;
+    h->ds.goal = (double*)(b + off_goal);
+    h->ds.q = (float*)(b + off_q);
+    h->ds.qd = (float*)(b + off_qd);
+    h->ds.object = (float*)(b + off_obj);
+    h->ds.elapsed = (int32_t*)(b + off_el);
+    h->ds.episode = (uint32_t*)(b + off_ep);
+    rc = hip_check(hipMemset(h->blob, 0, total), "hipMemset(state)");
+    if (!rc) {
+        PgxDevOut none;
+        std::memset(&none, 0, sizeof none);
+        rc = hip_check((hipError_t)pgx_launch_reset(h->dm, h->de, h->ds, nullptr, nullptr, none, nullptr), "reset launch");
+        /* episodes count resets; the construction reset (core.py:270) is not counted */
+        if (!rc) rc = hip_check(hipMemset(h->ds.episode, 0, N * 4), "hipMemset(episode)");
+        if (!rc) rc = hip_check(hipDeviceSynchronize(), "create sync");
+    }
+    if (rc) { (void)hipFree(h->blob); delete h; return rc; }
+    *out = h;
+    return PGX_OK;
+}
+
+void pgx_destroy(pgx_handle h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    (void)hipFree(h->blob);
+    delete h;
+}
+
+int pgx_get_state(pgx_handle h, pgx_state_view* out) {
+    if (!h || !out) return fail(PGX_E_INVALID, "null argument");
+    out->q = h->ds.q;
+    out->qd = h->ds.qd;
+    out->goal = h->ds.goal;
+    out->object = h->ds.object;
+    out->elapsed = h->ds.elapsed;
+    out->episode = h->ds.episode;
+    return PGX_OK;
+}
+
+static PgxDevOut to_dev_out(const pgx_step_out* o) {
+    PgxDevOut d;
+    std::memset(&d, 0, sizeof d);
+    if (!o) return d;
+    d.obs = o->obs;
+    d.ag = o->achieved_goal;
+    d.dg = o->desired_goal;
+    d.reward = o->reward;
+    d.success = o->success;
+    d.terminated = o->terminated;
+    d.truncated = o->truncated;
+    d.terminal_obs = o->terminal_obs;
+    d.terminal_ag = o->terminal_achieved_goal;
+    return d;
+}
+
+int pgx_reset(pgx_handle h, const uint8_t* env_mask, const double* inject_goal, const double* inject_object,
+              pgx_step_out* out, void* stream) {
+    if (!h) return fail(PGX_E_INVALID, "null handle");
+    if (inject_object) return fail(PGX_E_UNSUPPORTED, "object injection needs an object task");
+    return hip_check((hipError_t)pgx_launch_reset(h->dm, h->de, h->ds, env_mask, inject_goal, to_dev_out(out), stream),
+                     "reset launch");
+}
+
+int pgx_step(pgx_handle h, const float* action, pgx_step_out* out, void* stream) {
+    if (!h || !action) return fail(PGX_E_INVALID, "null argument");
+    return hip_check((hipError_t)pgx_launch_step(h->dm, h->de, h->ds, action, to_dev_out(out), stream), "step launch");
+}
+
+int pgx_sample_actions(pgx_handle h, float* action, uint64_t step, void* stream) {
+    if (!h || !action) return fail(PGX_E_INVALID, "null argument");
+    return hip_check((hipError_t)pgx_launch_sample_actions(h->de, action, step, stream), "sample launch");
+}
+
+int pgx_compute_reward(const float* ag, const float* dg, int64_t batch, int32_t reward_type, double thr, float* out,
+                       void* stream) {
+    if (batch < 0 || (batch > 0 && (!ag || !dg || !out))) return fail(PGX_E_INVALID, "bad arguments");
+    if (reward_type != PGX_REWARD_SPARSE && reward_type != PGX_REWARD_DENSE)
+        return fail(PGX_E_INVALID, "reward_type %d", reward_type);
+    return hip_check((hipError_t)pgx_launch_compute_reward(ag, dg, batch, reward_type, thr, out, stream),
+                     "compute_reward launch");
+}
+
+int pgx_state_bytes(pgx_handle h, int64_t* nbytes) {
+    if (!h || !nbytes) return fail(PGX_E_INVALID, "null argument");
+    *nbytes = (int64_t)h->blob_bytes;
+    return PGX_OK;
+}
+
+int pgx_save_state(pgx_handle h, void* dst, void* stream) {
+    if (!h || !dst) return fail(PGX_E_INVALID, "null argument");
+    return hip_check(hipMemcpyAsync(dst, h->blob, h->blob_bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream),
+                     "save_state copy");
+}
+
+int pgx_restore_state(pgx_handle h, const void* src, void* stream) {
+    if (!h || !src) return fail(PGX_E_INVALID, "null argument");
+    return hip_check(hipMemcpyAsync(h->blob, src, h->blob_bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream),
+                     "restore_state copy");
+}
+
+}  // extern "C"

@@ -1,0 +1,79 @@
+/*
+ * pgx_dev.h -- device-side constant tables and launch interface of libpgx.
+ *
+ * The env robot (franka_panda_custom_0, panda.py:54) is a 7-revolute-joint
+ * chain whose joint axes are all URDF z, followed by six links rigidly fixed
+ * to panda_link7 (link8, hand, ee, fingers, grasptarget: Bullet links 7-12).
+ * The kernel hard-codes that topology (checked on the host at pgx_create) and
+ * takes every numeric constant from PgxDevModel, passed by value as a kernel
+ * argument so that it is read through scalar loads into SGPRs.
+ */
+#pragma once
+#include <stdint.h>
+
+#define PGX_NJ 7          /* arm joints */
+#define PGX_MAX_DAMP 4    /* bodies of the link-7 group with mass (linear damping) */
+
+struct PgxDevModel {
+    float jp[PGX_NJ][3];      /* joint origin in parent URDF frame */
+    float jr[PGX_NJ][9];      /* joint origin rotation (row-major) */
+    float com[PGX_NJ][3];     /* COM in URDF link frame; [6] = composite COM of the link-7 group */
+    float mass[PGX_NJ];       /* [6] = composite mass */
+    float inertia[PGX_NJ - 1][3]; /* principal inertia of links 1..6 (COM frame == URDF frame) */
+    float i6c[6];             /* composite inertia of the link-7 group about its COM (xx,yy,zz,xy,xz,yz) */
+    float i6own[6];           /* sum of the group bodies' own inertias (angular damping) */
+    float dpos[PGX_MAX_DAMP][3]; /* COMs of group bodies with mass (link-7 frame) */
+    float dmass[PGX_MAX_DAMP];
+    int32_t ndamp;
+    float ee_pivot[3];        /* EE link URDF origin in link-7 frame (IK point) */
+    float ee_rot[9];          /* EE link rotation relative to link 7 */
+    float ee_com[3];          /* EE link COM in link-7 frame (getLinkState()[0]) */
+    float lower[PGX_NJ], upper[PGX_NJ];
+    float max_impulse[PGX_NJ];  /* joint_forces * dt */
+    float dt, inv_dt;
+    float gravity[3];
+    float lin_damp, ang_damp, max_vel, residual_thr, erp, limit_max_imp, kp, kd;
+    float ik_residual, ik_damping, ik_max_angle;
+    int32_t n_substeps, num_iterations, ik_max_iters;
+    float base[3];
+    float ee_step, joint_step;
+    float neutral_q[PGX_NJ];
+};
+
+struct PgxDevEnv {
+    int32_t task, control, reward, n_envs;
+    int32_t max_episode_steps, block_gripper, obs_dim, action_dim;
+    uint64_t seed, env_id_offset;
+    double distance_threshold;
+    double goal_low[3], goal_high[3];
+};
+
+struct PgxDevState {
+    float* q;          /* [7][N] */
+    float* qd;         /* [7][N] */
+    double* goal;      /* [3][N] */
+    float* object;     /* [13][N] */
+    int32_t* elapsed;  /* [N] */
+    uint32_t* episode; /* [N] */
+};
+
+struct PgxDevOut {
+    float* obs;
+    float* ag;
+    float* dg;
+    float* reward;
+    uint8_t* success;
+    uint8_t* terminated;
+    uint8_t* truncated;
+    float* terminal_obs;
+    float* terminal_ag;
+};
+
+/* launchers (pgx_kernels.hip); return hipError_t as int */
+int pgx_launch_step(const PgxDevModel& m, const PgxDevEnv& e, const PgxDevState& s, const float* action,
+                    const PgxDevOut& o, void* stream);
+int pgx_launch_reset(const PgxDevModel& m, const PgxDevEnv& e, const PgxDevState& s, const uint8_t* mask,
+                     const double* inject_goal, const PgxDevOut& o, void* stream);
+int pgx_launch_sample_actions(const PgxDevEnv& e, float* action, uint64_t step, void* stream);
+int pgx_launch_compute_reward(const float* ag, const float* dg, int64_t n, int32_t reward_type, double thr,
+                              float* out, void* stream);

@@ -1,0 +1,392 @@
+"""Vectorised Panda environments on MI355X: the reference's env surface over libpgx.
+
+Mirrors the reference's interfaces for the hot path:
+  * ``register_envs`` / ``make`` -- env ids and kwargs of panda_gym/__init__.py:23-91
+    (``PandaReach{,Joints}{,Dense}-v3``, max_episode_steps);
+  * ``PandaEnv`` -- one env with the ``RobotTaskEnv`` surface (core.py:255-414):
+    ``reset(seed, options)``, ``step(action)`` -> (obs dict, float reward,
+    terminated, truncated, info{"is_success","is_truncated"}), ``compute_reward``,
+    ``save_state/restore_state/remove_state``, gymnasium TimeLimit truncation;
+  * ``PandaVecEnv`` -- N lockstep envs on one GPU with SB3's VecEnv protocol
+    (``reset``, ``step_async/step_wait``, ``env_method("compute_reward", ...)``,
+    ``get_attr/set_attr``, auto-reset with ``terminal_observation`` and
+    ``TimeLimit.truncated`` infos) plus a device-resident ``step_tensors`` path.
+
+State lives in one device allocation owned by libpgx; observations come back
+as torch tensors on the env's device.  There is no CPU physics fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import replace
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import abi
+from ._native import PgxError, check, load
+from .model import load_model
+
+try:
+    import torch
+except ImportError:  # pragma: no cover - torch is part of the image
+    torch = None
+
+
+# ----------------------------------------------------------------- spaces
+class Box:
+    """Minimal gymnasium.spaces.Box stand-in (gymnasium is not installed here)."""
+
+    def __init__(self, low: float, high: float, shape: Tuple[int, ...], dtype=np.float32):
+        self.low = np.full(shape, low, dtype=dtype)
+        self.high = np.full(shape, high, dtype=dtype)
+        self.shape = tuple(shape)
+        self.dtype = np.dtype(dtype)
+        self._rng = np.random.default_rng()
+
+    def seed(self, seed: Optional[int] = None) -> None:
+        self._rng = np.random.default_rng(seed)
+
+    def sample(self) -> np.ndarray:
+        return self._rng.uniform(self.low, self.high).astype(self.dtype)
+
+    def contains(self, x) -> bool:
+        x = np.asarray(x)
+        return x.shape == self.shape and bool(np.all(x >= self.low) and np.all(x <= self.high))
+
+
+class DictSpace(dict):
+    """Minimal gymnasium.spaces.Dict stand-in."""
+
+    @property
+    def spaces(self) -> Dict[str, Box]:
+        return dict(self)
+
+
+# --------------------------------------------------------------- registry
+_REGISTRY: Dict[str, abi.EnvSpec] = {}
+
+
+def register_envs(max_ep_steps: int = 50) -> None:
+    """panda_gym.register_envs (panda_gym/__init__.py:23-91) for the tasks this build runs."""
+    for reward in (abi.REWARD_SPARSE, abi.REWARD_DENSE):
+        for control in (abi.CONTROL_EE, abi.CONTROL_JOINTS):
+            rs = "Dense" if reward == abi.REWARD_DENSE else ""
+            cs = "Joints" if control == abi.CONTROL_JOINTS else ""
+            _REGISTRY[f"PandaReach{cs}{rs}-v3"] = abi.EnvSpec(task=abi.TASK_REACH, control=control, reward=reward,
+                                                             max_episode_steps=max_ep_steps, block_gripper=True)
+
+
+def registered_ids() -> List[str]:
+    return sorted(_REGISTRY)
+
+
+def spec(env_id: str) -> abi.EnvSpec:
+    if not _REGISTRY:
+        register_envs(50)
+    if env_id not in _REGISTRY:
+        raise KeyError(f"{env_id} is not registered (call register_envs); known: {registered_ids()}")
+    return _REGISTRY[env_id]
+
+
+def seeded_goal(env_spec: abi.EnvSpec, seed: Optional[int]) -> Optional[np.ndarray]:
+    """Goal draw of RobotTaskEnv.reset(seed) (core.py:302 reseeds PCG64 every reset; reach.py:75-78)."""
+    if seed is None:
+        return None
+    rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed)))
+    lo, hi = env_spec.goal_bounds()
+    return rng.uniform(np.array(lo), np.array(hi))
+
+
+# ------------------------------------------------------------ vec env
+class PandaVecEnv:
+    """N independent Panda envs stepped in lockstep by one HIP kernel launch."""
+
+    def __init__(self, env_id: str = "PandaReach-v3", num_envs: int = 4096, device: Any = "cuda:0", seed: int = 0,
+                 env_id_offset: int = 0, max_episode_steps: Optional[int] = None, auto_reset: bool = True,
+                 n_substeps: int = 20, model_name: str = "panda_custom0"):
+        if torch is None:
+            raise PgxError("PandaVecEnv needs torch for device buffers")
+        self.lib = load()
+        self.env_id = env_id
+        base_spec = spec(env_id)
+        if max_episode_steps is not None:
+            base_spec = replace(base_spec, max_episode_steps=max_episode_steps)
+        self.spec = base_spec
+        self.num_envs = int(num_envs)
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise PgxError("PandaVecEnv runs on a HIP device only (no CPU physics fallback)")
+        self._model = abi.make_model(load_model(model_name), ee_link=11)
+        self._params = abi.default_sim_params(n_substeps=n_substeps)
+        cfg_spec = replace(self.spec, max_episode_steps=self.spec.max_episode_steps if auto_reset else 0)
+        self._cfg = abi.make_config(cfg_spec, self.num_envs, self._model, self._params, seed=seed,
+                                    env_id_offset=env_id_offset)
+        self.obs_dim = self.lib.pgx_obs_dim(C.byref(self._cfg))
+        self.action_dim = self.lib.pgx_action_dim(C.byref(self._cfg))
+        h = C.c_void_p()
+        torch.cuda.set_device(self.device)
+        check(self.lib.pgx_create(C.byref(self._cfg), self.device.index or 0, C.byref(h)), "pgx_create")
+        self._h = h
+        self.seed_value = seed
+        n, od = self.num_envs, self.obs_dim
+        kw = dict(device=self.device)
+        self.obs = torch.zeros((n, od), dtype=torch.float32, **kw)
+        self.achieved_goal = torch.zeros((n, 3), dtype=torch.float32, **kw)
+        self.desired_goal = torch.zeros((n, 3), dtype=torch.float32, **kw)
+        self.reward = torch.zeros(n, dtype=torch.float32, **kw)
+        self.success = torch.zeros(n, dtype=torch.uint8, **kw)
+        self.terminated = torch.zeros(n, dtype=torch.uint8, **kw)
+        self.truncated = torch.zeros(n, dtype=torch.uint8, **kw)
+        self.terminal_obs = torch.zeros((n, od), dtype=torch.float32, **kw)
+        self.terminal_ag = torch.zeros((n, 3), dtype=torch.float32, **kw)
+        self._actions = torch.zeros((n, self.action_dim), dtype=torch.float32, **kw)
+        self._out = abi.PgxStepOut(self.obs.data_ptr(), self.achieved_goal.data_ptr(), self.desired_goal.data_ptr(),
+                                   self.reward.data_ptr(), self.success.data_ptr(), self.terminated.data_ptr(),
+                                   self.truncated.data_ptr(), self.terminal_obs.data_ptr(), self.terminal_ag.data_ptr())
+        self.observation_space = DictSpace(observation=Box(-10.0, 10.0, (od,)), desired_goal=Box(-10.0, 10.0, (3,)),
+                                           achieved_goal=Box(-10.0, 10.0, (3,)))
+        self.action_space = Box(-1.0, 1.0, (self.action_dim,))
+        self.distance_threshold = self.spec.distance_threshold
+        self.reward_type = "dense" if self.spec.reward == abi.REWARD_DENSE else "sparse"
+        self._snapshots: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
+        self._next_snap = 0
+        self._pending: Optional[torch.Tensor] = None
+        self._step_index = 0
+
+    # ---------------------------------------------------------------- core
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            torch.cuda.synchronize(self.device)
+            self.lib.pgx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def state(self) -> Dict[str, torch.Tensor]:
+        """Device views of the SoA state (q, qd [7,N] f32; goal [3,N] f64; elapsed, episode [N])."""
+        v = abi.PgxStateView()
+        check(self.lib.pgx_get_state(self._h, C.byref(v)), "pgx_get_state")
+        n = self.num_envs
+        return {
+            "q": _view(v.q, (7, n), torch.float32, self.device),
+            "qd": _view(v.qd, (7, n), torch.float32, self.device),
+            "goal": _view(v.goal, (3, n), torch.float64, self.device),
+            "elapsed": _view(v.elapsed, (n,), torch.int32, self.device),
+            "episode": _view(v.episode, (n,), torch.int32, self.device),
+        }
+
+    def _obs_dict(self) -> Dict[str, torch.Tensor]:
+        return {"observation": self.obs, "achieved_goal": self.achieved_goal, "desired_goal": self.desired_goal}
+
+    def reset_tensors(self, seed: Optional[int] = None, mask: Optional[torch.Tensor] = None,
+                      goals: Optional[np.ndarray] = None) -> Dict[str, torch.Tensor]:
+        """Reset (masked) envs on device; ``seed`` reproduces the reference's PCG64 goal draws
+        for env i with seed+i (SB3 VecEnv seeding), injected into the kernel."""
+        inj = None
+        if goals is not None:
+            inj = torch.as_tensor(np.asarray(goals, dtype=np.float64).reshape(self.num_envs, 3), device=self.device)
+        elif seed is not None:
+            g = np.stack([seeded_goal(self.spec, seed + i) for i in range(self.num_envs)])
+            inj = torch.as_tensor(g, device=self.device)
+        m = None
+        if mask is not None:
+            m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        check(self.lib.pgx_reset(self._h, None if m is None else C.c_void_p(m.data_ptr()),
+                                 None if inj is None else C.c_void_p(inj.data_ptr()), None, C.byref(self._out),
+                                 self._stream()), "pgx_reset")
+        self._keep = (m, inj)  # keep the buffers alive until the stream consumes them
+        return self._obs_dict()
+
+    def step_tensors(self, actions: torch.Tensor):
+        """Device-resident step: actions [N,A] f32 on device -> (obs dict, reward, terminated, truncated, success).
+
+        Returned tensors are the env's persistent buffers (overwritten by the next step)."""
+        a = actions
+        if a.dtype != torch.float32 or a.device != self.device or not a.is_contiguous():
+            a = a.to(device=self.device, dtype=torch.float32).contiguous()
+        if tuple(a.shape) != (self.num_envs, self.action_dim):
+            raise ValueError(f"actions must be [{self.num_envs}, {self.action_dim}], got {tuple(a.shape)}")
+        check(self.lib.pgx_step(self._h, C.c_void_p(a.data_ptr()), C.byref(self._out), self._stream()), "pgx_step")
+        self._step_index += 1
+        return self._obs_dict(), self.reward, self.terminated, self.truncated, self.success
+
+    def sample_actions(self, step: Optional[int] = None) -> torch.Tensor:
+        """Random policy U[-1,1) from the device Philox stream (benchmark workload)."""
+        s = self._step_index if step is None else step
+        check(self.lib.pgx_sample_actions(self._h, C.c_void_p(self._actions.data_ptr()), C.c_uint64(s),
+                                          self._stream()), "pgx_sample_actions")
+        return self._actions
+
+    # ------------------------------------------------------- SB3 VecEnv API
+    def reset(self, seed: Optional[int] = None, options: Optional[dict] = None):
+        self.reset_tensors(seed=seed)
+        return self._numpy_obs()
+
+    def seed(self, seed: Optional[int] = None) -> List[Optional[int]]:
+        self._pending_seed = seed
+        return [None if seed is None else seed + i for i in range(self.num_envs)]
+
+    def step_async(self, actions) -> None:
+        self._pending = torch.as_tensor(np.asarray(actions, dtype=np.float32) if not torch.is_tensor(actions)
+                                        else actions)
+
+    def step_wait(self):
+        obs, rew, term, trunc, succ = self.step_tensors(self._pending)
+        self._pending = None
+        dones = (term | trunc).bool()
+        o = self._numpy_obs()
+        r = rew.cpu().numpy()
+        d = dones.cpu().numpy()
+        tr = trunc.bool().cpu().numpy()
+        te = term.bool().cpu().numpy()
+        sc = succ.bool().cpu().numpy()
+        infos: List[Dict[str, Any]] = [{"is_success": bool(sc[i]), "is_truncated": False} for i in range(self.num_envs)]
+        idx = np.nonzero(d)[0]
+        if len(idx):
+            tobs = self.terminal_obs.cpu().numpy()
+            tag = self.terminal_ag.cpu().numpy()
+            for i in idx:
+                infos[i]["terminal_observation"] = {"observation": tobs[i].copy(), "achieved_goal": tag[i].copy(),
+                                                    "desired_goal": o["desired_goal"][i].copy()}
+                infos[i]["TimeLimit.truncated"] = bool(tr[i] and not te[i])
+        return o, r, d, infos
+
+    def step(self, actions):
+        self.step_async(actions)
+        return self.step_wait()
+
+    def _numpy_obs(self) -> Dict[str, np.ndarray]:
+        return {k: v.cpu().numpy().copy() for k, v in self._obs_dict().items()}
+
+    def compute_reward(self, achieved_goal, desired_goal, info=None):
+        """Task.compute_reward over a batch (HER relabel path), on device.
+
+        Float32 inputs follow the reference's float32 numpy arithmetic bit for bit."""
+        is_np = not torch.is_tensor(achieved_goal)
+        ag = torch.as_tensor(np.asarray(achieved_goal, dtype=np.float32) if is_np else achieved_goal)
+        dg = torch.as_tensor(np.asarray(desired_goal, dtype=np.float32) if is_np else desired_goal)
+        shape = ag.shape[:-1]
+        ag = ag.to(self.device, torch.float32).reshape(-1, 3).contiguous()
+        dg = dg.to(self.device, torch.float32).reshape(-1, 3).contiguous()
+        out = torch.empty(ag.shape[0], dtype=torch.float32, device=self.device)
+        rt = abi.REWARD_DENSE if self.reward_type == "dense" else abi.REWARD_SPARSE
+        check(self.lib.pgx_compute_reward(C.c_void_p(ag.data_ptr()), C.c_void_p(dg.data_ptr()),
+                                          C.c_int64(ag.shape[0]), rt, C.c_double(self.distance_threshold),
+                                          C.c_void_p(out.data_ptr()), self._stream()), "pgx_compute_reward")
+        out = out.reshape(shape)
+        return out.cpu().numpy() if is_np else out
+
+    def env_method(self, method_name: str, *args, indices=None, **kwargs):
+        if method_name == "compute_reward":
+            return [self.compute_reward(*args, **kwargs)]
+        return [getattr(self, method_name)(*args, **kwargs)]
+
+    def get_attr(self, attr_name: str, indices=None):
+        val = getattr(self, attr_name)
+        n = self.num_envs if indices is None else len(list(indices))
+        return [val] * n
+
+    def set_attr(self, attr_name: str, value, indices=None) -> None:
+        setattr(self, attr_name, value)
+
+    # ----------------------------------------------------- save / restore
+    def save_state(self) -> int:
+        """Device snapshot of the whole SoA state (RobotTaskEnv.save_state, core.py:310-321)."""
+        nb = C.c_int64()
+        check(self.lib.pgx_state_bytes(self._h, C.byref(nb)), "pgx_state_bytes")
+        buf = torch.empty(nb.value, dtype=torch.uint8, device=self.device)
+        check(self.lib.pgx_save_state(self._h, C.c_void_p(buf.data_ptr()), self._stream()), "pgx_save_state")
+        sid = self._next_snap
+        self._next_snap += 1
+        self._snapshots[sid] = buf
+        return sid
+
+    def restore_state(self, state_id: int) -> None:
+        if state_id not in self._snapshots:
+            raise PgxError(f"Could not restore state {state_id}: no such saved state")
+        buf = self._snapshots[state_id]
+        check(self.lib.pgx_restore_state(self._h, C.c_void_p(buf.data_ptr()), self._stream()), "pgx_restore_state")
+
+    def remove_state(self, state_id: int) -> None:
+        if state_id not in self._snapshots:
+            raise PgxError(f"Could not remove state {state_id}: no such saved state")
+        del self._snapshots[state_id]
+
+
+def _view(addr: int, shape, dtype, device):
+    """Wrap a libpgx-owned device buffer as a torch tensor (no copy)."""
+    typestr = {torch.float32: "<f4", torch.float64: "<f8", torch.int32: "<i4"}[dtype]
+
+    class _Iface:  # torch has no public from-pointer constructor; use __cuda_array_interface__
+        __cuda_array_interface__ = {"shape": tuple(shape), "typestr": typestr, "data": (int(addr), False),
+                                    "version": 2, "strides": None}
+
+    return torch.as_tensor(_Iface(), device=device)
+
+
+# --------------------------------------------------------- single env
+class PandaEnv:
+    """One env with the RobotTaskEnv + TimeLimit surface (gym.make("PandaReach-v3") in the reference)."""
+
+    metadata = {"render_modes": []}
+
+    def __init__(self, env_id: str = "PandaReach-v3", device: Any = "cuda:0", max_episode_steps: Optional[int] = None,
+                 seed: int = 0):
+        self._vec = PandaVecEnv(env_id, num_envs=1, device=device, seed=seed, auto_reset=False,
+                                max_episode_steps=max_episode_steps)
+        self.spec = self._vec.spec
+        self.observation_space = self._vec.observation_space
+        self.action_space = self._vec.action_space
+        self._elapsed = 0
+        self._saved_elapsed: Dict[int, int] = {}
+
+    def reset(self, seed: Optional[int] = None, options: Optional[dict] = None):
+        g = seeded_goal(self.spec, seed)
+        self._vec.reset_tensors(goals=None if g is None else g[None, :])
+        self._elapsed = 0
+        obs = self._vec._numpy_obs()
+        obs = {k: v[0] for k, v in obs.items()}
+        return obs, {"is_success": bool(self._vec.success[0].item())}
+
+    def step(self, action):
+        a = torch.as_tensor(np.asarray(action, dtype=np.float32).reshape(1, -1), device=self._vec.device)
+        obs, rew, term, trunc, succ = self._vec.step_tensors(a)
+        self._elapsed += 1
+        o = {k: v[0].cpu().numpy().copy() for k, v in obs.items()}
+        truncated = self.spec.max_episode_steps > 0 and self._elapsed >= self.spec.max_episode_steps
+        info = {"is_success": bool(succ[0].item()), "is_truncated": False}
+        return o, float(rew[0].item()), bool(term[0].item()), bool(truncated), info
+
+    def compute_reward(self, achieved_goal, desired_goal, info=None):
+        return self._vec.compute_reward(achieved_goal, desired_goal, info)
+
+    def save_state(self) -> int:
+        sid = self._vec.save_state()
+        self._saved_elapsed[sid] = self._elapsed
+        return sid
+
+    def restore_state(self, state_id: int) -> None:
+        self._vec.restore_state(state_id)
+        self._elapsed = self._saved_elapsed[state_id]
+
+    def remove_state(self, state_id: int) -> None:
+        self._vec.remove_state(state_id)
+        self._saved_elapsed.pop(state_id, None)
+
+    def close(self) -> None:
+        self._vec.close()
+
+
+def make(env_id: str, **kwargs) -> PandaEnv:
+    """gym.make equivalent for the registered ids (single env with TimeLimit)."""
+    spec(env_id)
+    return PandaEnv(env_id, **kwargs)
