@@ -1,0 +1,172 @@
+"""Benchmark: aggregate env-steps/s of PandaReach at 4096 envs per GPU (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 4096]
+
+One step = one batched env step of all envs on the GPU: device Philox random
+actions (pgx_sample_actions) + the fused IK/physics/obs/reward/auto-reset
+kernel (pgx_step).  Inputs and state stay resident in HBM.  For N > 1 the
+driver launches one process per GPU (torch.distributed.run); envs are sharded
+by global id (rank r owns ids [r*E, (r+1)*E)), nothing is exchanged on the step
+path, and the timed region is bracketed by barriers with the max over ranks.
+
+Rank 0 prints one JSON line with the roofline of the step kernel (algorithmic
+bytes from SURVEY.md §8d over the HIP-event kernel time) and a CPU baseline
+(the fp64 oracle = CPU restatement, not PyBullet, timed on this host).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
+VALU_PEAK_TFLOPS = 157.3         # FP32 vector peak (spec)
+ALG_BYTES_PER_ENV_STEP = 199.0   # read 84 + write 115 B per Reach env-step
+PROFILE_JSON = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--env-id", default="PandaReach-v3")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel-launches", type=int, default=200, help="launches for the kernel-time measurement")
+    return ap.parse_args()
+
+
+def cpu_baseline(venv, seconds: float):
+    """fp64 oracle on the host cores (threads; ctypes releases the GIL) over a bounded sample."""
+    import concurrent.futures as cf
+
+    from oracle import oracle as O
+
+    n = venv.num_envs
+    threads = max(1, min(16, os.cpu_count() or 1))
+    shards = np.array_split(np.arange(n), threads)
+    envs = []
+    for sh in shards:
+        cfg = type(venv._cfg).from_buffer_copy(venv._cfg)
+        cfg.n_envs = len(sh)
+        cfg.env_id_offset = int(sh[0])
+        e = O.OracleVecEnv(cfg, len(sh))
+        e.reset()
+        envs.append(e)
+    steps = 0
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as ex:
+        while time.perf_counter() - t0 < seconds and steps < 200:
+            list(ex.map(lambda e: e.step(e.sample_actions(steps)), envs))
+            steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"fp64 C oracle (CPU restatement, not PyBullet): {n} PandaReach envs x {steps} steps "
+                      f"= {n * steps} env-steps in {dt:.1f} s on {threads} host threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import panda_gym_amd as pg
+    from panda_gym_amd.shard import gather_stats, max_over_ranks, shard_offset
+
+    E = args.envs
+    venv = pg.PandaVecEnv(args.env_id, num_envs=E, device=dev, seed=args.seed,
+                          env_id_offset=shard_offset(rank, E))
+    venv.reset_tensors()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        venv.step_tensors(venv.sample_actions())
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        venv.step_tensors(venv.sample_actions())
+    torch.cuda.synchronize(dev)
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, dist, dev)
+    # episode statistics all-gather (outside the timed region; 16 B per rank over xGMI)
+    stats = gather_stats([float(venv.truncated.sum()), float(venv.success.sum()), float(venv.reward.sum()),
+                          float(args.steps)], dist, dev).sum(0)
+    total = world * E * args.steps
+    value = total / elapsed
+
+    # kernel time of pgx_step alone (HIP events on the launch stream = torch's current stream)
+    acts = venv.sample_actions().clone()
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    ev0.record(stream)
+    for _ in range(args.kernel_launches):
+        venv.step_tensors(acts)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    kernel_ms = ev0.elapsed_time(ev1) / args.kernel_launches
+
+    if rank == 0:
+        alg_bytes = ALG_BYTES_PER_ENV_STEP * E
+        achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+        traffic = None
+        valu = None
+        if os.path.exists(PROFILE_JSON):
+            with open(PROFILE_JSON) as f:
+                prof = json.load(f)
+            if prof.get("num_envs") == E:
+                traffic = prof.get("hbm_bytes_per_launch")
+                ins = prof.get("valu_lane_ops_per_launch")
+                if ins:
+                    valu = {"bound": "valu", "achieved": ins / (kernel_ms * 1e-3) / 1e12 * 2.0,
+                            "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s-equiv (2 x VALU lane-ops)",
+                            "source": os.path.relpath(PROFILE_JSON, ROOT)}
+                    valu["frac"] = valu["achieved"] / VALU_PEAK_TFLOPS
+        line = {
+            "metric": "aggregate env-steps/s, PandaReach 4096 envs @1 GPU; 1/2/4/8-GPU scaling",
+            "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: device Philox random policy U[-1,1)^3, 50-step episodes with in-kernel auto-reset",
+            "config": {"workload": f"{args.env_id} (ee control, sparse reward), {E} envs per GPU, "
+                                   f"no contacts (BASELINE configs[1])",
+                       "envs_per_gpu": E, "global_envs": world * E, "parallelism": f"env-sharded x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "step_kernel<0>", "kernel_ms": kernel_ms,
+                         "alg_bytes_per_launch": alg_bytes},
+            "roofline_valu": valu,
+            "episode_stats": {"success_last_step": float(stats[0]), "reward_sum_last_step": float(stats[1])},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(venv, args.cpu_baseline_seconds)
+        print(json.dumps(line), flush=True)
+    venv.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

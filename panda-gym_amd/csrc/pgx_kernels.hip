@@ -553,6 +553,12 @@ __device__ float distance_f32_f32(const float* a, const float* b) {
     float y = rintf(d * 1e6f);
     return y / 1e6f;
 }
+/* numpy Generator.uniform: low + (high - low) * u, unfused */
+__device__ double uniform_draw(double low, double high, double u) {
+    double r = high - low;
+    double t = r * u;
+    return low + t;
+}
 #pragma clang fp contract(on)
 
 __device__ __forceinline__ void write_obs(const PgxDevEnv& e, float* dst, V3 pos, V3 vel) {
@@ -568,7 +574,7 @@ __device__ __forceinline__ void reset_env(const PgxDevModel& m, const PgxDevEnv&
     uint64_t env = e.env_id_offset + (uint64_t)i;
 #pragma unroll
     for (int c = 0; c < 3; c++)
-        goal[c] = inject ? inject[c] : e.goal_low[c] + (e.goal_high[c] - e.goal_low[c]) * reset_uniform(e, env, episode, c);
+        goal[c] = inject ? inject[c] : uniform_draw(e.goal_low[c], e.goal_high[c], reset_uniform(e, env, episode, c));
     episode += 1;
 }
 

@@ -1,0 +1,247 @@
+"""GPU parity: libpgx (HIP, fp32) against the fp64 oracle on the same seeded inputs.
+
+Tolerances: observations/achieved goals within 1e-4 (BASELINE.json north star,
+fp32 vs the fp64 restatement); integer/byte outputs (truncation, episode
+counters, Philox draws, HER rewards on identical inputs) bit-exact; is_success
+and sparse rewards bit-exact except where the distance lies within 1e-5 of the
+threshold (the fp32 achieved goal legitimately differs from the fp64 one there).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+OBS_TOL = 1e-4
+EDGE = 1e-5
+
+
+@pytest.fixture(scope="module")
+def pg():
+    import panda_gym_amd as pg
+
+    pg.load_native()
+    return pg
+
+
+def _state_to_oracle(venv, ref):
+    st = venv.state()
+    ref.q[:] = st["q"].double().cpu().numpy().T
+    ref.qd[:] = st["qd"].double().cpu().numpy().T
+    ref.goal[:] = st["goal"].cpu().numpy().T
+    ref.elapsed[:] = st["elapsed"].cpu().numpy()
+    ref.episode[:] = st["episode"].cpu().numpy().view(np.uint32)
+
+
+def _check_step(out_gpu, out_ref, goal):
+    obs, ag, dg, rew, succ = out_gpu
+    assert np.all(np.isfinite(obs))
+    err = np.abs(obs - out_ref["obs"]).max()
+    assert err <= OBS_TOL, f"obs error {err}"
+    assert np.abs(ag - out_ref["ag"]).max() <= OBS_TOL
+    assert np.array_equal(dg, out_ref["dg"])
+    d = np.linalg.norm(out_ref["ag"].astype(np.float64) - goal, axis=-1)
+    safe = np.abs(d - 0.05) > EDGE
+    assert np.array_equal(succ[safe].astype(bool), out_ref["success"][safe].astype(bool))
+    return err
+
+
+def _gpu_out(venv):
+    o = venv._obs_dict()
+    return (o["observation"].cpu().numpy(), o["achieved_goal"].cpu().numpy(), o["desired_goal"].cpu().numpy(),
+            venv.reward.cpu().numpy(), venv.success.cpu().numpy())
+
+
+@pytest.mark.parametrize("env_id", ["PandaReach-v3", "PandaReachDense-v3", "PandaReachJoints-v3"])
+def test_one_step_parity(pg, oracle, env_id):
+    n = 512
+    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=3)
+    venv.reset_tensors()
+    ref = oracle.OracleVecEnv(venv._cfg, n)
+    for k in range(3):  # a few steps so the start states are not all neutral
+        venv.step_tensors(venv.sample_actions(100 + k))
+    _state_to_oracle(venv, ref)
+    goal = ref.goal.copy()
+    acts = venv.sample_actions(7).clone()
+    venv.step_tensors(acts)
+    out = ref.step(acts.cpu().numpy())
+    _check_step(_gpu_out(venv), out, goal)
+    dense = env_id.find("Dense") >= 0
+    r_gpu = venv.reward.cpu().numpy()
+    if dense:
+        assert np.abs(r_gpu - out["reward"]).max() <= OBS_TOL
+    venv.close()
+
+
+def test_episode_trajectory_parity(pg, oracle):
+    """Free-running rollout across an auto-reset.
+
+    Positions (ee position, achieved goal) stay within 1e-4 of the oracle for the whole episode.
+    Velocities get 1e-3: the solver stops when the squared row residual <= 1e-7 (pybullet's
+    solverResidualThreshold), so a velocity is only defined to ~3.2e-4 rad/s and an fp32/fp64
+    difference in the exit iteration shows up as a velocity step of that size."""
+    n = 256
+    venv = pg.PandaVecEnv("PandaReach-v3", num_envs=n, device="cuda:0", seed=11)
+    venv.reset_tensors()
+    ref = oracle.OracleVecEnv(venv._cfg, n)
+    _state_to_oracle(venv, ref)
+    worst_pos, worst_vel = 0.0, 0.0
+    for t in range(60):
+        acts = venv.sample_actions(t).clone()
+        a_ref = ref.sample_actions(t)
+        assert np.array_equal(acts.cpu().numpy(), a_ref), "device Philox actions differ from oracle"
+        venv.step_tensors(acts)
+        goal = ref.goal.copy()
+        out = ref.step(a_ref)
+        g = _gpu_out(venv)
+        tr = venv.truncated.cpu().numpy()
+        assert np.array_equal(tr, out["truncated"]), t
+        if tr.any():
+            # the episode just ended: compare terminal observations; new goals come from Philox
+            te = np.abs(venv.terminal_obs.cpu().numpy() - out["terminal_obs"])
+            assert te[:, :3].max() <= OBS_TOL and te[:, 3:].max() <= 10 * OBS_TOL
+            assert np.array_equal(g[2], out["dg"])
+            assert np.abs(g[0] - out["obs"]).max() <= 1e-6   # reset obs: neutral pose
+            continue
+        e = np.abs(g[0] - out["obs"])
+        worst_pos = max(worst_pos, float(e[:, :3].max()), float(np.abs(g[1] - out["ag"]).max()))
+        worst_vel = max(worst_vel, float(e[:, 3:].max()))
+    assert worst_pos <= OBS_TOL, f"trajectory position error {worst_pos}"
+    assert worst_vel <= 10 * OBS_TOL, f"trajectory velocity error {worst_vel}"
+    venv.close()
+
+
+def test_compute_reward_bit_exact_vs_reference_golden(pg):
+    import os
+
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "reward_golden.npz"))
+    for env_id, key in [("PandaReach-v3", "sparse_f32_f32"), ("PandaReachDense-v3", "dense_f32_f32")]:
+        venv = pg.PandaVecEnv(env_id, num_envs=1, device="cuda:0")
+        r = venv.compute_reward(g["ag32"], g["dg32"], {})
+        assert r.dtype == np.float32
+        assert np.array_equal(r.view(np.uint32), g[key].view(np.uint32)), key
+        venv.close()
+
+
+def test_seeded_reset_goals_match_reference_draws(pg):
+    import os
+
+    gold = np.load(os.path.join(os.path.dirname(__file__), "golden", "reset_golden.npz"))
+    env = pg.make("PandaReach-v3")
+    for s, gl in zip(gold["seeds"], gold["reach_goal"]):
+        obs, info = env.reset(seed=int(s))
+        st = env._vec.state()
+        assert np.array_equal(st["goal"].cpu().numpy()[:, 0], gl)
+        assert np.array_equal(obs["desired_goal"], gl.astype(np.float32))
+    env.close()
+
+
+def test_auto_reset_goals_match_oracle_philox(pg, oracle):
+    n = 128
+    venv = pg.PandaVecEnv("PandaReach-v3", num_envs=n, device="cuda:0", seed=1234, env_id_offset=5000,
+                          max_episode_steps=2)
+    venv.reset_tensors()
+    ref = oracle.OracleVecEnv(venv._cfg, n)
+    ref.reset()
+    assert np.array_equal(venv.state()["goal"].cpu().numpy().T, ref.goal)
+    for t in range(4):
+        a = venv.sample_actions(t).clone()
+        venv.step_tensors(a)
+        ref.step(a.cpu().numpy())
+    st = venv.state()
+    assert np.array_equal(st["goal"].cpu().numpy().T, ref.goal)
+    assert np.array_equal(st["episode"].cpu().numpy().view(np.uint32), ref.episode)
+    assert np.array_equal(st["elapsed"].cpu().numpy(), ref.elapsed)
+    venv.close()
+
+
+def test_seed_determinism(pg):
+    """test/seed_test.py:7-28 (PandaReach-v3, seed 12345, fixed 6-action sequence, twice)."""
+    actions = [np.array([-0.931, 0.979, -0.385]), np.array([-0.562, 0.391, -0.532]),
+               np.array([0.042, 0.254, -0.624]), np.array([0.465, 0.745, 0.284]),
+               np.array([-0.237, 0.995, -0.425]), np.array([0.67, 0.472, 0.972])]
+    finals = []
+    env = pg.make("PandaReach-v3")
+    for _ in range(2):
+        env.reset(seed=12345)
+        for a in actions:
+            obs, _, term, trunc, _ = env.step(a)
+            if term or trunc:
+                obs, _ = env.reset()
+        finals.append(obs)
+    for k in ("observation", "achieved_goal", "desired_goal"):
+        assert np.array_equal(finals[0][k], finals[1][k])
+    env.close()
+
+
+def test_save_and_restore_state(pg):
+    """test/save_and_restore_test.py:9-27: save -> step -> reset -> restore -> step gives equal obs."""
+    env = pg.make("PandaReach-v3")
+    env.reset()
+    sid = env.save_state()
+    action = env.action_space.sample()
+    o1, _, _, _, _ = env.step(action)
+    env.reset()
+    env.restore_state(sid)
+    o2, _, _, _, _ = env.step(action)
+    for k in ("observation", "achieved_goal", "desired_goal"):
+        assert np.array_equal(o1[k], o2[k])
+    env.close()
+
+
+def test_remove_state(pg):
+    """test/save_and_restore_test.py:30-36: restoring a removed state raises."""
+    env = pg.make("PandaReach-v3")
+    env.reset()
+    sid = env.save_state()
+    env.remove_state(sid)
+    with pytest.raises(pg.PgxError):
+        env.restore_state(sid)
+    env.close()
+
+
+def test_single_env_time_limit(pg):
+    env = pg.make("PandaReach-v3", max_episode_steps=5)
+    env.reset(seed=0)
+    truncs = []
+    for _ in range(5):
+        _, r, term, trunc, info = env.step(np.zeros(3, np.float32))
+        truncs.append(trunc)
+        assert term is False and isinstance(r, float) and "is_success" in info
+    assert truncs == [False] * 4 + [True]
+    env.close()
+
+
+def test_sb3_vecenv_protocol(pg):
+    venv = pg.PandaVecEnv("PandaReach-v3", num_envs=8, device="cuda:0", max_episode_steps=3)
+    obs = venv.reset(seed=0)
+    assert obs["observation"].shape == (8, 6)
+    for t in range(3):
+        obs, rew, dones, infos = venv.step(np.zeros((8, 3), np.float32))
+    assert dones.all()
+    assert all(i["TimeLimit.truncated"] for i in infos)
+    assert infos[0]["terminal_observation"]["observation"].shape == (6,)
+    r = venv.env_method("compute_reward", obs["achieved_goal"], obs["desired_goal"], infos)[0]
+    assert r.shape == (8,)
+    venv.close()
+
+
+def test_large_batch_properties(pg):
+    """Full-size batch (65536 envs): finite, bounded, deterministic, reward consistent with success."""
+    n = 65536
+    outs = []
+    for _ in range(2):
+        venv = pg.PandaVecEnv("PandaReach-v3", num_envs=n, device="cuda:0", seed=99)
+        venv.reset_tensors()
+        for t in range(12):
+            venv.step_tensors(venv.sample_actions(t))
+        torch.cuda.synchronize()
+        o = venv.obs.cpu().numpy()
+        outs.append((o, venv.reward.cpu().numpy(), venv.success.cpu().numpy()))
+        venv.close()
+    o, r, s = outs[0]
+    assert np.all(np.isfinite(o)) and np.abs(o).max() < 10.0
+    assert np.array_equal(outs[0][0], outs[1][0])  # bitwise deterministic
+    assert np.array_equal(r == 0.0, s.astype(bool) | (r == 0.0))
+    assert set(np.unique(r)).issubset({-1.0, 0.0})
