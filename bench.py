@@ -158,7 +158,8 @@ def main():
                          "kernel": "step_kernel<0>", "kernel_ms": kernel_ms,
                          "alg_bytes_per_launch": alg_bytes},
             "roofline_valu": valu,
-            "episode_stats": {"success_last_step": float(stats[0]), "reward_sum_last_step": float(stats[1])},
+            "episode_stats_last_step": {"truncated": float(stats[0]), "success": float(stats[1]),
+                                        "reward_sum": float(stats[2])},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(venv, args.cpu_baseline_seconds)

@@ -41,7 +41,12 @@ __device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y 
 __device__ __forceinline__ V3 cross(V3 a, V3 b) {
     return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
-__device__ __forceinline__ float norm(V3 a) { return sqrtf(dot(a, a)); }
+/* Hot-path reciprocal / square root: the hardware v_rcp_f32 / v_sqrt_f32 (1 ulp).  The
+ * library is compiled with correctly rounded '/' and sqrtf, which the reward path needs
+ * for bit-exact parity with numpy; the physics does not. */
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float norm(V3 a) { return fast_sqrt(dot(a, a)); }
 
 /* row-major 3x3 */
 struct M3 {
@@ -144,30 +149,30 @@ __device__ __forceinline__ void mat_to_quat(const M3& M, float* q) {
     const float* m = M.m;
     float tr = m[0] + m[4] + m[8];
     if (tr > 0.0f) {
-        float s = sqrtf(tr + 1.0f);
+        float s = fast_sqrt(tr + 1.0f);
         q[3] = s * 0.5f;
-        s = 0.5f / s;
+        s = 0.5f * fast_rcp(s);
         q[0] = (m[7] - m[5]) * s;
         q[1] = (m[2] - m[6]) * s;
         q[2] = (m[3] - m[1]) * s;
     } else if (!(m[0] < m[4]) && !(m[0] < m[8])) { /* i = 0, j = 1, k = 2 */
-        float s = sqrtf(m[0] - m[4] - m[8] + 1.0f);
+        float s = fast_sqrt(m[0] - m[4] - m[8] + 1.0f);
         q[0] = s * 0.5f;
-        s = 0.5f / s;
+        s = 0.5f * fast_rcp(s);
         q[3] = (m[7] - m[5]) * s;
         q[1] = (m[3] + m[1]) * s;
         q[2] = (m[6] + m[2]) * s;
     } else if (m[0] < m[4] && !(m[4] < m[8])) { /* i = 1, j = 2, k = 0 */
-        float s = sqrtf(m[4] - m[8] - m[0] + 1.0f);
+        float s = fast_sqrt(m[4] - m[8] - m[0] + 1.0f);
         q[1] = s * 0.5f;
-        s = 0.5f / s;
+        s = 0.5f * fast_rcp(s);
         q[3] = (m[2] - m[6]) * s;
         q[2] = (m[7] + m[5]) * s;
         q[0] = (m[1] + m[3]) * s;
     } else { /* i = 2, j = 0, k = 1 */
-        float s = sqrtf(m[8] - m[0] - m[4] + 1.0f);
+        float s = fast_sqrt(m[8] - m[0] - m[4] + 1.0f);
         q[2] = s * 0.5f;
-        s = 0.5f / s;
+        s = 0.5f * fast_rcp(s);
         q[3] = (m[3] - m[1]) * s;
         q[0] = (m[2] + m[6]) * s;
         q[1] = (m[5] + m[7]) * s;
@@ -181,9 +186,8 @@ __device__ __forceinline__ void chol7(float A[NJ][NJ]) {
         float s = A[j][j];
 #pragma unroll
         for (int k = 0; k < j; k++) s -= A[j][k] * A[j][k];
-        float d = sqrtf(fmaxf(s, 1e-30f));
-        float inv = 1.0f / d;
-        A[j][j] = d;
+        float inv = __builtin_amdgcn_rsqf(fmaxf(s, 1e-30f));
+        A[j][j] = inv; /* the factor's diagonal is stored inverted */
 #pragma unroll
         for (int i = j + 1; i < NJ; i++) {
             float t = A[i][j];
@@ -200,14 +204,14 @@ __device__ __forceinline__ void chol7_solve(const float L[NJ][NJ], const float* 
         float s = b[i];
 #pragma unroll
         for (int k = 0; k < i; k++) s -= L[i][k] * y[k];
-        y[i] = s / L[i][i];
+        y[i] = s * L[i][i];
     }
 #pragma unroll
     for (int i = NJ - 1; i >= 0; i--) {
         float s = y[i];
 #pragma unroll
         for (int k = i + 1; k < NJ; k++) s -= L[k][i] * x[k];
-        x[i] = s / L[i][i];
+        x[i] = s * L[i][i];
     }
 }
 
@@ -241,7 +245,7 @@ __device__ __forceinline__ void ik(const PgxDevModel& m, const float* q0, V3 tar
             dq[2] = aw * bz + az * bw + ax * by - ay * bx;
             dq[3] = aw * bw - ax * bx - ay * by - az * bz;
         }
-        float vn = sqrtf(dq[0] * dq[0] + dq[1] * dq[1] + dq[2] * dq[2]);
+        float vn = fast_sqrt(dq[0] * dq[0] + dq[1] * dq[1] + dq[2] * dq[2]);
         float angle = 2.0f * atan2f(vn, dq[3]);
         if (angle > 3.14159265358979f) angle -= 6.28318530717959f;
         V3 axis = vn > 1e-30f ? (1.0f / vn) * v3(dq[0], dq[1], dq[2]) : v3(1.0f, 0.0f, 0.0f);
@@ -266,7 +270,7 @@ __device__ __forceinline__ void ik(const PgxDevModel& m, const float* q0, V3 tar
         float mx = 0.0f;
 #pragma unroll
         for (int j = 0; j < NJ; j++) mx = fmaxf(mx, fabsf(dth[j]));
-        float sc = mx > m.ik_max_angle ? m.ik_max_angle / mx : 1.0f;
+        float sc = mx > m.ik_max_angle ? m.ik_max_angle * fast_rcp(mx) : 1.0f;
 #pragma unroll
         for (int j = 0; j < NJ; j++) qs[j] += dth[j] * sc;
         diff = norm(x - target);
@@ -383,7 +387,7 @@ __device__ __forceinline__ void substep(const PgxDevModel& m, float* q, float* q
             if (j < NJ - 1) {
                 float mj = m.mass[j];
                 float mt = mc + mj;
-                V3 cn = (1.0f / mt) * (mc * cc + mj * c[j]);
+                V3 cn = fast_rcp(mt) * (mc * cc + mj * c[j]);
                 Ic = add(add(Ic, steiner(mc, cc - cn)), add(Iw[j], steiner(mj, c[j] - cn)));
                 mc = mt;
                 cc = cn;
@@ -410,7 +414,7 @@ __device__ __forceinline__ void substep(const PgxDevModel& m, float* q, float* q
         float X[NJ][NJ];
 #pragma unroll
         for (int i = 0; i < NJ; i++) {
-            float inv = 1.0f / Mt[i][i];
+            float inv = Mt[i][i]; /* chol7 stores the inverted diagonal */
 #pragma unroll
             for (int jj = 0; jj <= i; jj++) {
                 float s = (jj == i) ? 1.0f : 0.0f;
@@ -434,11 +438,11 @@ __device__ __forceinline__ void substep(const PgxDevModel& m, float* q, float* q
     /* rows (btMultiBodyJointMotor / btMultiBodyJointLimitConstraint::createConstraintRows):
      * jinv depends only on the dof, bounds are constants, so per row only rhs and
      * the accumulated impulse live in registers. */
-    float jinv[NJ];
+    float den[NJ], jinv[NJ];
 #pragma unroll
     for (int d = 0; d < NJ; d++) {
-        const float den = Mi[d][d];
-        jinv[d] = den > 2.220446e-16f ? 1.0f / den : 0.0f; /* SIMD_EPSILON guard */
+        den[d] = Mi[d][d];
+        jinv[d] = den[d] > 2.220446e-16f ? fast_rcp(den[d]) : 0.0f; /* SIMD_EPSILON guard */
     }
     float rhs[PGX_N_ROWS], lam[PGX_N_ROWS];
 #pragma unroll
@@ -458,36 +462,68 @@ __device__ __forceinline__ void substep(const PgxDevModel& m, float* q, float* q
             rhs[r] = (perr + verr) * jinv[d];
         }
     }
+    /* Exact skip of the joint-limit rows.  With only motor impulses |lambda_k| <= F_k dt
+     * applied, |dv_d| <= B_d = sum_k |Minv_dk| F_k dt.  A not-violated limit row of dof d
+     * can only get a positive impulse once vu_d + dv_d crosses -pen/dt (lower) or
+     * +pen/dt (upper); if that is impossible for every limit row, none ever leaves 0
+     * during the sweep (by induction), every evaluation of them clamps to delta = 0,
+     * and dropping them changes no bit of the result or of the exit iteration. */
+    bool far = true;
+#pragma unroll
+    for (int d = 0; d < NJ; d++) {
+        float B = 0.0f;
+#pragma unroll
+        for (int k = 0; k < NJ; k++) B += fabsf(MINV(d, k)) * m.max_impulse[k];
+        B = B * 1.001f + 1e-6f;
+        const float penl = q[d] - m.lower[d], penu = m.upper[d] - q[d];
+        far = far && penl > 0.0f && penu > 0.0f && (vu[d] - B) > -penl * m.inv_dt && (vu[d] + B) < penu * m.inv_dt;
+    }
     float dv[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; j++) dv[j] = 0.0f;
+    /* resolveSingleConstraintRowGeneric, branch-free: clamp the accumulated impulse,
+     * apply the clamped delta through the unit response M^-1 J^T (a column of M^-1). */
     auto row = [&](const int r, float& resid) {
         const int kind = kPgxRowCode[r] >> 4, d = kPgxRowCode[r] & 15;
         const float lo = kind == 0 ? -m.max_impulse[d] : 0.0f;
         const float hi = kind == 0 ? m.max_impulse[d] : m.limit_max_imp;
-        float delta = rhs[r] - (kind == 2 ? -dv[d] : dv[d]) * jinv[d];
-        float sum = lam[r] + delta;
-        if (sum < lo) { delta = lo - lam[r]; lam[r] = lo; }
-        else if (sum > hi) { delta = hi - lam[r]; lam[r] = hi; }
-        else lam[r] = sum;
-        if (delta != 0.0f) {
-            const float sd = kind == 2 ? -delta : delta;
+        const float vd = kind == 2 ? -dv[d] : dv[d];
+        float delta = rhs[r] - vd * jinv[d];
+        const float nl = fminf(fmaxf(lam[r] + delta, lo), hi);
+        delta = nl - lam[r];
+        lam[r] = nl;
+        const float sd = kind == 2 ? -delta : delta;
 #pragma unroll
-            for (int cc = 0; cc < NJ; cc++) dv[cc] += MINV(cc, d) * sd;
-        }
-        float res = jinv[d] != 0.0f ? delta / jinv[d] : 0.0f;
+        for (int cc = 0; cc < NJ; cc++) dv[cc] += MINV(cc, d) * sd;
+        const float res = delta * den[d];
         resid = fmaxf(resid, res * res);
     };
-    for (int it = 0; it < m.num_iterations; it++) {
-        float resid = 0.0f;
-        if (it & 1) {
+    if (__all(far)) {
+        for (int it = 0; it < m.num_iterations; it++) {
+            float resid = 0.0f;
+            if (it & 1) {
 #pragma unroll
-            for (int r = 0; r < PGX_N_ROWS; r++) row(r, resid);
-        } else {
+                for (int r = 0; r < PGX_N_ROWS; r++)
+                    if ((kPgxRowCode[r] >> 4) == 0) row(r, resid);
+            } else {
 #pragma unroll
-            for (int r = PGX_N_ROWS - 1; r >= 0; r--) row(r, resid);
+                for (int r = PGX_N_ROWS - 1; r >= 0; r--)
+                    if ((kPgxRowCode[r] >> 4) == 0) row(r, resid);
+            }
+            if (resid <= m.residual_thr) break;
         }
-        if (resid <= m.residual_thr) break;
+    } else {
+        for (int it = 0; it < m.num_iterations; it++) {
+            float resid = 0.0f;
+            if (it & 1) {
+#pragma unroll
+                for (int r = 0; r < PGX_N_ROWS; r++) row(r, resid);
+            } else {
+#pragma unroll
+                for (int r = PGX_N_ROWS - 1; r >= 0; r--) row(r, resid);
+            }
+            if (resid <= m.residual_thr) break;
+        }
     }
 #undef MINV
 #pragma unroll
