@@ -18,6 +18,7 @@
 
 #include "../../include/pgx.h"
 #include "pgx_dev.h"
+#include "pgx_model_consts.h"
 #include "pgx_rows.h"
 
 namespace {
@@ -57,7 +58,8 @@ void m3v(const double* A, const double* v, double* o) {
 
 struct pgx_env {
     int device;
-    PgxDevModel dm;
+    PgxDevModel dm;      /* host copy */
+    PgxDevModel* dm_dev; /* device copy at the start of the state blob */
     PgxDevEnv de;
     PgxDevState ds;
     void* blob;
@@ -76,6 +78,35 @@ int pgx_obs_dim(const pgx_config* c) {
 int pgx_action_dim(const pgx_config* c) {
     if (!c) return PGX_E_INVALID;
     return (c->control == PGX_CONTROL_EE ? 3 : 7) + (c->block_gripper ? 0 : 1);
+}
+
+/* The kernel is specialised to the env robot at compile time (pgx_model_consts.h);
+ * refuse a runtime model whose folded tables differ from the compiled ones. */
+static int check_compiled_tables(const PgxDevModel& dm) {
+    auto same = [](const float* a, const float* b, int n, const char* what) -> int {
+        for (int i = 0; i < n; i++)
+            if (std::fabs(a[i] - b[i]) > 1e-6f * std::fmax(1.0f, std::fabs(b[i])))
+                return fail(PGX_E_UNSUPPORTED, "model table %s[%d] = %g differs from the compiled robot (%g)", what,
+                            i, (double)a[i], (double)b[i]);
+        return PGX_OK;
+    };
+    int rc = 0;
+    rc = rc ? rc : same(&dm.jp[0][0], &kJp[0][0], 21, "jp");
+    rc = rc ? rc : same(&dm.jr[0][0], &kJr[0][0], 63, "jr");
+    rc = rc ? rc : same(&dm.com[0][0], &kCom[0][0], 21, "com");
+    rc = rc ? rc : same(dm.mass, kMass, 7, "mass");
+    rc = rc ? rc : same(&dm.inertia[0][0], &kInertia[0][0], 18, "inertia");
+    rc = rc ? rc : same(dm.i6c, kI6c, 6, "i6c");
+    rc = rc ? rc : same(dm.i6own, kI6own, 6, "i6own");
+    if (!rc && dm.ndamp != PGX_NDAMP) rc = fail(PGX_E_UNSUPPORTED, "damped body count %d != %d", dm.ndamp, PGX_NDAMP);
+    rc = rc ? rc : same(&dm.dpos[0][0], &kDpos[0][0], 3 * PGX_NDAMP, "dpos");
+    rc = rc ? rc : same(dm.dmass, kDmass, PGX_NDAMP, "dmass");
+    rc = rc ? rc : same(dm.ee_pivot, kEePivot, 3, "ee_pivot");
+    rc = rc ? rc : same(dm.ee_rot, kEeRot, 9, "ee_rot");
+    rc = rc ? rc : same(dm.ee_com, kEeCom, 3, "ee_com");
+    rc = rc ? rc : same(dm.lower, kLower, 7, "lower");
+    rc = rc ? rc : same(dm.upper, kUpper, 7, "upper");
+    return rc;
 }
 
 /* Fold the model into the kernel's constant tables. */
@@ -194,7 +225,7 @@ static int build_dev_model(const pgx_config* cfg, PgxDevModel* dm) {
     dm->ee_step = (float)cfg->ee_step;
     dm->joint_step = (float)cfg->joint_step;
     if (p->flags != 0) return fail(PGX_E_UNSUPPORTED, "modelling flags are oracle-only");
-    return PGX_OK;
+    return check_compiled_tables(*dm);
 }
 
 int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
@@ -229,7 +260,7 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     if (rc) { delete h; return rc; }
     const size_t N = (size_t)cfg->n_envs;
     auto align = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    size_t off_goal = 0, off_q = align(off_goal + 3 * N * 8), off_qd = align(off_q + PGX_NJ * N * 4),
+    size_t off_goal = align(sizeof(PgxDevModel)), off_q = align(off_goal + 3 * N * 8), off_qd = align(off_q + PGX_NJ * N * 4),
            off_obj = align(off_qd + PGX_NJ * N * 4), off_el = align(off_obj + 13 * N * 4),
            off_ep = align(off_el + N * 4), total = align(off_ep + N * 4);
     rc = hip_check(hipMalloc(&h->blob, total), "hipMalloc(state)");
@@ -242,11 +273,13 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     h->ds.object = (float*)(b + off_obj);
     h->ds.elapsed = (int32_t*)(b + off_el);
     h->ds.episode = (uint32_t*)(b + off_ep);
+    h->dm_dev = (PgxDevModel*)b;
     rc = hip_check(hipMemset(h->blob, 0, total), "hipMemset(state)");
+    if (!rc) rc = hip_check(hipMemcpy(h->dm_dev, &h->dm, sizeof(PgxDevModel), hipMemcpyHostToDevice), "model copy");
     if (!rc) {
         PgxDevOut none;
         std::memset(&none, 0, sizeof none);
-        rc = hip_check((hipError_t)pgx_launch_reset(h->dm, h->de, h->ds, nullptr, nullptr, none, nullptr), "reset launch");
+        rc = hip_check((hipError_t)pgx_launch_reset(h->dm_dev, h->de, h->ds, nullptr, nullptr, none, nullptr), "reset launch");
         /* episodes count resets; the construction reset (core.py:270) is not counted */
         if (!rc) rc = hip_check(hipMemset(h->ds.episode, 0, N * 4), "hipMemset(episode)");
         if (!rc) rc = hip_check(hipDeviceSynchronize(), "create sync");
@@ -294,13 +327,13 @@ int pgx_reset(pgx_handle h, const uint8_t* env_mask, const double* inject_goal, 
               pgx_step_out* out, void* stream) {
     if (!h) return fail(PGX_E_INVALID, "null handle");
     if (inject_object) return fail(PGX_E_UNSUPPORTED, "object injection needs an object task");
-    return hip_check((hipError_t)pgx_launch_reset(h->dm, h->de, h->ds, env_mask, inject_goal, to_dev_out(out), stream),
+    return hip_check((hipError_t)pgx_launch_reset(h->dm_dev, h->de, h->ds, env_mask, inject_goal, to_dev_out(out), stream),
                      "reset launch");
 }
 
 int pgx_step(pgx_handle h, const float* action, pgx_step_out* out, void* stream) {
     if (!h || !action) return fail(PGX_E_INVALID, "null argument");
-    return hip_check((hipError_t)pgx_launch_step(h->dm, h->de, h->ds, action, to_dev_out(out), stream), "step launch");
+    return hip_check((hipError_t)pgx_launch_step(h->dm_dev, h->de, h->ds, action, to_dev_out(out), stream), "step launch");
 }
 
 int pgx_sample_actions(pgx_handle h, float* action, uint64_t step, void* stream) {

@@ -5,8 +5,8 @@
  * chain whose joint axes are all URDF z, followed by six links rigidly fixed
  * to panda_link7 (link8, hand, ee, fingers, grasptarget: Bullet links 7-12).
  * The kernel hard-codes that topology (checked on the host at pgx_create) and
- * takes every numeric constant from PgxDevModel, passed by value as a kernel
- * argument so that it is read through scalar loads into SGPRs.
+ * takes every numeric constant from PgxDevModel, copied once to a device
+ * buffer and read through the constant address space (scalar loads, SGPRs).
  */
 #pragma once
 #include <stdint.h>
@@ -70,9 +70,9 @@ struct PgxDevOut {
 };
 
 /* launchers (pgx_kernels.hip); return hipError_t as int */
-int pgx_launch_step(const PgxDevModel& m, const PgxDevEnv& e, const PgxDevState& s, const float* action,
+int pgx_launch_step(const PgxDevModel* m_device, const PgxDevEnv& e, const PgxDevState& s, const float* action,
                     const PgxDevOut& o, void* stream);
-int pgx_launch_reset(const PgxDevModel& m, const PgxDevEnv& e, const PgxDevState& s, const uint8_t* mask,
+int pgx_launch_reset(const PgxDevModel* m_device, const PgxDevEnv& e, const PgxDevState& s, const uint8_t* mask,
                      const double* inject_goal, const PgxDevOut& o, void* stream);
 int pgx_launch_sample_actions(const PgxDevEnv& e, float* action, uint64_t step, void* stream);
 int pgx_launch_compute_reward(const float* ag, const float* dg, int64_t n, int32_t reward_type, double thr,

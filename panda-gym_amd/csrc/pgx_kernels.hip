@@ -24,11 +24,27 @@
 #include <stdint.h>
 
 #include "pgx_dev.h"
+#include "pgx_model_consts.h"
 #include "pgx_rows.h"
 
 namespace {
 
 constexpr int NJ = PGX_NJ;
+
+/* The robot constants (PgxDevModel, ~1.4 KB) live in a device buffer read
+ * through the constant address space, so every access is a scalar load
+ * (s_load_dwordx16 into SGPRs).  `fresh()` hides the pointer behind an empty
+ * asm at the top of each substep / IK iteration: the compiler then re-issues
+ * the scalar loads where the values are used instead of hoisting ~350
+ * constants out of the loops and spilling them to VGPR lanes (which cost one
+ * v_readlane VALU instruction per use). */
+typedef const __attribute__((address_space(4))) PgxDevModel* MPtr;
+typedef const __attribute__((address_space(4))) PgxDevModel& MRef;
+__device__ __forceinline__ MPtr fresh(uint64_t addr) {
+    asm volatile("; pgx fresh model pointer %0" : "+s"(addr));
+    return (MPtr)addr;
+}
+__device__ __forceinline__ MPtr fresh(MPtr p) { return fresh((uint64_t)p); }
 
 struct V3 {
     float x, y, z;
@@ -56,14 +72,25 @@ __device__ __forceinline__ V3 mul(const M3& A, V3 v) {
     return v3(A.m[0] * v.x + A.m[1] * v.y + A.m[2] * v.z, A.m[3] * v.x + A.m[4] * v.y + A.m[5] * v.z,
               A.m[6] * v.x + A.m[7] * v.y + A.m[8] * v.z);
 }
-__device__ __forceinline__ V3 mulc(const M3& A, const float* v) { return mul(A, v3(v[0], v[1], v[2])); }
+/* x * k where k comes from the compile-time robot tables (pgx_model_consts.h):
+ * after unrolling k is a literal, so 0 / +-1 factors vanish (x + -0.0f folds to x
+ * exactly in IEEE) and only the genuine products remain. */
+__device__ __forceinline__ float kmul(float x, float k) {
+    return k == 0.0f ? -0.0f : (k == 1.0f ? x : (k == -1.0f ? -x : x * k));
+}
+/* A * v and A * B with v, B constant tables */
+__device__ __forceinline__ V3 mulc(const M3& A, const float* v) {
+    return v3(kmul(A.m[0], v[0]) + kmul(A.m[1], v[1]) + kmul(A.m[2], v[2]),
+              kmul(A.m[3], v[0]) + kmul(A.m[4], v[1]) + kmul(A.m[5], v[2]),
+              kmul(A.m[6], v[0]) + kmul(A.m[7], v[1]) + kmul(A.m[8], v[2]));
+}
 __device__ __forceinline__ M3 mulm(const M3& A, const float* B) {
     M3 C;
 #pragma unroll
     for (int i = 0; i < 3; i++)
 #pragma unroll
         for (int j = 0; j < 3; j++)
-            C.m[i * 3 + j] = A.m[i * 3] * B[j] + A.m[i * 3 + 1] * B[3 + j] + A.m[i * 3 + 2] * B[6 + j];
+            C.m[i * 3 + j] = kmul(A.m[i * 3], B[j]) + kmul(A.m[i * 3 + 1], B[3 + j]) + kmul(A.m[i * 3 + 2], B[6 + j]);
     return C;
 }
 __device__ __forceinline__ V3 col(const M3& A, int c) { return v3(A.m[c], A.m[3 + c], A.m[6 + c]); }
@@ -96,7 +123,7 @@ __device__ __forceinline__ S3 rot_sym(const M3& R, const float* s) {
     for (int i = 0; i < 3; i++)
 #pragma unroll
         for (int j = 0; j < 3; j++)
-            T[i * 3 + j] = R.m[i * 3] * Sm[j] + R.m[i * 3 + 1] * Sm[3 + j] + R.m[i * 3 + 2] * Sm[6 + j];
+            T[i * 3 + j] = kmul(R.m[i * 3], Sm[j]) + kmul(R.m[i * 3 + 1], Sm[3 + j]) + kmul(R.m[i * 3 + 2], Sm[6 + j]);
     auto e = [&](int i, int j) { return T[i * 3] * R.m[j * 3] + T[i * 3 + 1] * R.m[j * 3 + 1] + T[i * 3 + 2] * R.m[j * 3 + 2]; };
     S3 o;
     o.xx = e(0, 0); o.yy = e(1, 1); o.zz = e(2, 2); o.xy = e(0, 1); o.xz = e(0, 2); o.yz = e(1, 2);
@@ -120,13 +147,13 @@ struct Chain {
     V3 o[NJ];
 };
 
-__device__ __forceinline__ void fk_chain(const PgxDevModel& m, const float* q, Chain& k) {
+__device__ __forceinline__ void fk_chain(MRef m, const float* q, Chain& k) {
     M3 PR = {{1, 0, 0, 0, 1, 0, 0, 0, 1}};
     V3 PO = v3(m.base[0], m.base[1], m.base[2]);
 #pragma unroll
     for (int j = 0; j < NJ; j++) {
-        M3 R = mulm(PR, m.jr[j]);
-        V3 o = PO + mulc(PR, m.jp[j]);
+        M3 R = mulm(PR, kJr[j]);
+        V3 o = PO + mulc(PR, kJp[j]);
         float s, c;
         sincosf(q[j], &s, &c);
         /* R * Rz(q): rotate the first two columns */
@@ -222,18 +249,20 @@ __device__ __forceinline__ void chol7_solve(const float L[NJ][NJ], const float* 
  * link's joint pivot; dq = (J^T J + 0.5 I)^-1 J^T e clamped to max|dq|<=pi/4.
  * The orientation error angle is taken as 2*atan2(|v|, w) (== 2*acos(w) for a
  * unit quaternion, but well conditioned in fp32 for small angles). */
-__device__ __forceinline__ void ik(const PgxDevModel& m, const float* q0, V3 target, const float* torn,
-                                   float* qout) {
+__device__ __forceinline__ void ik(MPtr mp, const float* q0, V3 target, const float* torn, float* qout) {
     float qs[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; j++) qs[j] = q0[j];
     float diff = 1e30f;
-    for (int it = 0; it < m.ik_max_iters; it++) {
-        if (!(diff > m.ik_residual)) break;
+    const int max_iters = mp->ik_max_iters;
+    const float residual = mp->ik_residual;
+    for (int it = 0; it < max_iters; it++) {
+        if (!(diff > residual)) break;
+        MRef m = *fresh(mp);
         Chain k;
         fk_chain(m, qs, k);
-        V3 x = k.o[6] + mulc(k.R[6], m.ee_pivot);
-        M3 Ree = mulm(k.R[6], m.ee_rot);
+        V3 x = k.o[6] + mulc(k.R[6], kEePivot);
+        M3 Ree = mulm(k.R[6], kEeRot);
         float cq[4], dq[4];
         mat_to_quat(Ree, cq);
         /* dq = torn * conj(cq) */
@@ -286,7 +315,8 @@ __device__ __forceinline__ void ik(const PgxDevModel& m, const float* q0, V3 tar
  *   sweeps, early exit when max squared row residual <= residual_thr
  *   qd = clamp(qd_u + M^-1 J^T lambda); q += dt*qd   (constraint pass, stepPositions)
  * M by composite-rigid-body, b by Newton-Euler with Bullet's link damping. */
-__device__ __forceinline__ void substep(const PgxDevModel& m, float* q, float* qd, const float* tq) {
+__device__ __forceinline__ void substep(MPtr mp, float* q, float* qd, const float* tq) {
+    MRef m = *fresh(mp);
     /* FK fused with the per-link quantities the dynamics need, so the 3x3
      * rotations die immediately (only panda_link7's survives for its group). */
     V3 z[NJ], o[NJ], c[NJ];
@@ -297,8 +327,8 @@ __device__ __forceinline__ void substep(const PgxDevModel& m, float* q, float* q
         V3 PO = v3(m.base[0], m.base[1], m.base[2]);
 #pragma unroll
         for (int j = 0; j < NJ; j++) {
-            M3 R = mulm(PR, m.jr[j]);
-            V3 oj = PO + mulc(PR, m.jp[j]);
+            M3 R = mulm(PR, kJr[j]);
+            V3 oj = PO + mulc(PR, kJp[j]);
             float s, cs;
             sincosf(q[j], &s, &cs);
 #pragma unroll
@@ -309,9 +339,9 @@ __device__ __forceinline__ void substep(const PgxDevModel& m, float* q, float* q
             }
             z[j] = col(R, 2);
             o[j] = oj;
-            c[j] = oj + mulc(R, m.com[j]);
-            if (j < NJ - 1) Iw[j] = rot_diag(R, m.inertia[j]);
-            else { Iw[j] = rot_sym(R, m.i6c); R6 = R; }
+            c[j] = oj + mulc(R, kCom[j]);
+            if (j < NJ - 1) Iw[j] = rot_diag(R, kInertia[j]);
+            else { Iw[j] = rot_sym(R, kI6c); R6 = R; }
             PR = R;
             PO = oj;
         }
@@ -338,21 +368,21 @@ __device__ __forceinline__ void substep(const PgxDevModel& m, float* q, float* q
             V3 a = ao + cross(al, rc) + cross(w, wrc);
             float wn = norm(w);
             V3 Iww = mul(Iw[j], w);
-            F[j] = m.mass[j] * (a - g);
+            F[j] = kMass[j] * (a - g);
             T[j] = mul(Iw[j], al) + cross(w, Iww);
             if (j < NJ - 1) {
-                F[j] = F[j] + (m.mass[j] * (m.lin_damp + m.lin_damp * norm(v))) * v;
+                F[j] = F[j] + (kMass[j] * (m.lin_damp + m.lin_damp * norm(v))) * v;
                 T[j] = T[j] + (m.ang_damp + m.ang_damp * wn) * Iww;
             } else {
                 /* link-7 group: composite inertial terms, per-body damping */
-                S3 Iown = rot_sym(R6, m.i6own);
+                S3 Iown = rot_sym(R6, kI6own);
                 T[j] = T[j] + (m.ang_damp + m.ang_damp * wn) * mul(Iown, w);
 #pragma unroll
-                for (int b = 0; b < PGX_MAX_DAMP; b++) {
-                    if (b < m.ndamp) {
-                        V3 rb = mulc(R6, m.dpos[b]);
+                for (int b = 0; b < PGX_NDAMP; b++) {
+                    {
+                        V3 rb = mulc(R6, kDpos[b]);
                         V3 vb = vo + cross(w, rb);
-                        V3 fd = (m.dmass[b] * (m.lin_damp + m.lin_damp * norm(vb))) * vb;
+                        V3 fd = (kDmass[b] * (m.lin_damp + m.lin_damp * norm(vb))) * vb;
                         F[j] = F[j] + fd;
                         T[j] = T[j] + cross(o[j] + rb - c[j], fd);
                     }
@@ -379,13 +409,13 @@ __device__ __forceinline__ void substep(const PgxDevModel& m, float* q, float* q
     /* composite-rigid-body mass matrix (lower triangle, row >= col) */
     float Mt[NJ][NJ];
     {
-        float mc = m.mass[NJ - 1];
+        float mc = kMass[NJ - 1];
         V3 cc = c[NJ - 1];
         S3 Ic = Iw[NJ - 1];
 #pragma unroll
         for (int j = NJ - 1; j >= 0; j--) {
             if (j < NJ - 1) {
-                float mj = m.mass[j];
+                float mj = kMass[j];
                 float mt = mc + mj;
                 V3 cn = fast_rcp(mt) * (mc * cc + mj * c[j]);
                 Ic = add(add(Ic, steiner(mc, cc - cn)), add(Iw[j], steiner(mj, c[j] - cn)));
@@ -455,7 +485,7 @@ __device__ __forceinline__ void substep(const PgxDevModel& m, float* q, float* q
             float desired = m.kp * pos_term + vu[d] + m.kd * (0.0f - vu[d]);
             rhs[r] = (desired - rel) * jinv[d];
         } else {
-            float pen = kind == 1 ? (q[d] - m.lower[d]) : (m.upper[d] - q[d]);
+            float pen = kind == 1 ? (q[d] - kLower[d]) : (kUpper[d] - q[d]);
             float verr = -rel, perr = 0.0f;
             if (pen > 0.0f) verr -= pen * m.inv_dt;
             else perr = -pen * m.erp * m.inv_dt;
@@ -475,7 +505,7 @@ __device__ __forceinline__ void substep(const PgxDevModel& m, float* q, float* q
 #pragma unroll
         for (int k = 0; k < NJ; k++) B += fabsf(MINV(d, k)) * m.max_impulse[k];
         B = B * 1.001f + 1e-6f;
-        const float penl = q[d] - m.lower[d], penu = m.upper[d] - q[d];
+        const float penl = q[d] - kLower[d], penu = kUpper[d] - q[d];
         far = far && penl > 0.0f && penu > 0.0f && (vu[d] - B) > -penl * m.inv_dt && (vu[d] + B) < penu * m.inv_dt;
     }
     float dv[NJ];
@@ -489,14 +519,16 @@ __device__ __forceinline__ void substep(const PgxDevModel& m, float* q, float* q
         const float hi = kind == 0 ? m.max_impulse[d] : m.limit_max_imp;
         const float vd = kind == 2 ? -dv[d] : dv[d];
         float delta = rhs[r] - vd * jinv[d];
-        const float nl = fminf(fmaxf(lam[r] + delta, lo), hi);
+        /* v_med3 with the bounds straight from SGPRs (lo <= hi always holds) */
+        const float nl = __builtin_amdgcn_fmed3f(lam[r] + delta, lo, hi);
         delta = nl - lam[r];
         lam[r] = nl;
         const float sd = kind == 2 ? -delta : delta;
 #pragma unroll
         for (int cc = 0; cc < NJ; cc++) dv[cc] += MINV(cc, d) * sd;
-        const float res = delta * den[d];
-        resid = fmaxf(resid, res * res);
+        /* track max |row residual|; fl(x^2) is monotone in |x|, so squaring the max
+         * once per sweep equals the max of the squares */
+        resid = fmaxf(resid, fabsf(delta * den[d]));
     };
     if (__all(far)) {
         for (int it = 0; it < m.num_iterations; it++) {
@@ -510,7 +542,7 @@ __device__ __forceinline__ void substep(const PgxDevModel& m, float* q, float* q
                 for (int r = PGX_N_ROWS - 1; r >= 0; r--)
                     if ((kPgxRowCode[r] >> 4) == 0) row(r, resid);
             }
-            if (resid <= m.residual_thr) break;
+            if (resid * resid <= m.residual_thr) break;
         }
     } else {
         for (int it = 0; it < m.num_iterations; it++) {
@@ -522,7 +554,7 @@ __device__ __forceinline__ void substep(const PgxDevModel& m, float* q, float* q
 #pragma unroll
                 for (int r = PGX_N_ROWS - 1; r >= 0; r--) row(r, resid);
             }
-            if (resid <= m.residual_thr) break;
+            if (resid * resid <= m.residual_thr) break;
         }
     }
 #undef MINV
@@ -535,10 +567,10 @@ __device__ __forceinline__ void substep(const PgxDevModel& m, float* q, float* q
 }
 
 /* EE (link 11) COM position and velocity: getLinkState(11)[0] and [6] */
-__device__ __forceinline__ void ee_state(const PgxDevModel& m, const float* q, const float* qd, V3& pos, V3& vel) {
+__device__ __forceinline__ void ee_state(MRef m, const float* q, const float* qd, V3& pos, V3& vel) {
     Chain k;
     fk_chain(m, q, k);
-    pos = k.o[NJ - 1] + mulc(k.R[NJ - 1], m.ee_com);
+    pos = k.o[NJ - 1] + mulc(k.R[NJ - 1], kEeCom);
     V3 vv = v3(0, 0, 0);
 #pragma unroll
     for (int j = 0; j < NJ; j++) vv = vv + qd[j] * cross(col(k.R[j], 2), pos - k.o[j]);
@@ -603,7 +635,7 @@ __device__ __forceinline__ void write_obs(const PgxDevEnv& e, float* dst, V3 pos
     if (!e.block_gripper) dst[6] = 0.0f; /* custom_0 fingers are fixed joints: width 0 */
 }
 
-__device__ __forceinline__ void reset_env(const PgxDevModel& m, const PgxDevEnv& e, int i, uint32_t& episode,
+__device__ __forceinline__ void reset_env(MRef m, const PgxDevEnv& e, int i, uint32_t& episode,
                                           const double* inject, float* q, float* qd, double* goal) {
 #pragma unroll
     for (int j = 0; j < NJ; j++) { q[j] = m.neutral_q[j]; qd[j] = 0.0f; }
@@ -615,11 +647,13 @@ __device__ __forceinline__ void reset_env(const PgxDevModel& m, const PgxDevEnv&
 }
 
 template <int CONTROL>
-__global__ __launch_bounds__(64) void step_kernel(PgxDevModel m, PgxDevEnv e, PgxDevState s, const float* __restrict__ action,
-                                                  PgxDevOut o) {
+__global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict__ mdev, PgxDevEnv e, PgxDevState s,
+                                                  const float* __restrict__ action, PgxDevOut o) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int N = e.n_envs;
     if (i >= N) return;
+    const MPtr mp = fresh((uint64_t)mdev);
+    MRef m = *mp;
     float q[NJ], qd[NJ], tq[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; j++) {
@@ -639,11 +673,11 @@ __global__ __launch_bounds__(64) void step_kernel(PgxDevModel m, PgxDevEnv e, Pg
         V3 pos, vel;
         Chain k;
         fk_chain(m, q, k);
-        pos = k.o[NJ - 1] + mulc(k.R[NJ - 1], m.ee_com);
+        pos = k.o[NJ - 1] + mulc(k.R[NJ - 1], kEeCom);
         V3 tgt = pos + v3(a[0] * m.ee_step, a[1] * m.ee_step, a[2] * m.ee_step);
         tgt.z = fmaxf(0.0f, tgt.z);
         const float torn[4] = {1.0f, 0.0f, 0.0f, 0.0f};
-        ik(m, q, tgt, torn, tq);
+        ik(mp, q, tgt, torn, tq);
         (void)vel;
     } else {
 #pragma unroll
@@ -653,10 +687,11 @@ __global__ __launch_bounds__(64) void step_kernel(PgxDevModel m, PgxDevEnv e, Pg
         }
     }
 
-    for (int st = 0; st < m.n_substeps; st++) substep(m, q, qd, tq);
+    const int n_substeps = m.n_substeps;
+    for (int st = 0; st < n_substeps; st++) substep(mp, q, qd, tq);
 
     V3 pos, vel;
-    ee_state(m, q, qd, pos, vel);
+    ee_state(*fresh(mp), q, qd, pos, vel);
     const int od = e.obs_dim;
     double d = distance_f32_f64(pos, goal);
     bool succ = d < e.distance_threshold;
@@ -695,11 +730,12 @@ __global__ __launch_bounds__(64) void step_kernel(PgxDevModel m, PgxDevEnv e, Pg
     s.episode[i] = episode;
 }
 
-__global__ __launch_bounds__(64) void reset_kernel(PgxDevModel m, PgxDevEnv e, PgxDevState s, const uint8_t* mask,
-                                                   const double* inject_goal, PgxDevOut o) {
+__global__ __launch_bounds__(64) void reset_kernel(const PgxDevModel* __restrict__ mdev, PgxDevEnv e, PgxDevState s,
+                                                   const uint8_t* mask, const double* inject_goal, PgxDevOut o) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int N = e.n_envs;
     if (i >= N) return;
+    MRef m = *fresh((uint64_t)mdev);
     if (mask && !mask[i]) return;
     float q[NJ], qd[NJ];
     double goal[3];
@@ -752,7 +788,7 @@ __global__ __launch_bounds__(256) void compute_reward_kernel(const float* __rest
 
 }  // namespace
 
-int pgx_launch_step(const PgxDevModel& m, const PgxDevEnv& e, const PgxDevState& s, const float* action,
+int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState& s, const float* action,
                     const PgxDevOut& o, void* stream) {
     dim3 block(64), grid((e.n_envs + 63) / 64);
     hipStream_t st = (hipStream_t)stream;
@@ -763,7 +799,7 @@ int pgx_launch_step(const PgxDevModel& m, const PgxDevEnv& e, const PgxDevState&
     return (int)hipGetLastError();
 }
 
-int pgx_launch_reset(const PgxDevModel& m, const PgxDevEnv& e, const PgxDevState& s, const uint8_t* mask,
+int pgx_launch_reset(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState& s, const uint8_t* mask,
                      const double* inject_goal, const PgxDevOut& o, void* stream) {
     dim3 block(64), grid((e.n_envs + 63) / 64);
     hipLaunchKernelGGL(reset_kernel, grid, block, 0, (hipStream_t)stream, m, e, s, mask, inject_goal, o);
