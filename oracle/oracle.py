@@ -43,7 +43,8 @@ class PgxoMotor(C.Structure):
 
 
 class PgxoStats(C.Structure):
-    _fields_ = [("solver_iterations", C.c_int32), ("ik_iterations", C.c_int32), ("ik_residual", C.c_double)]
+    _fields_ = [("solver_iterations", C.c_int32), ("ik_iterations", C.c_int32), ("ik_residual", C.c_double),
+                ("limits_far", C.c_int32), ("pad", C.c_int32)]
 
 
 def _p(a):

@@ -363,6 +363,17 @@ void pgxo_substep(const pgx_model* m, const pgx_sim_params* p, const double base
         rhs[nr] = r_rhs; lo[nr] = r_lo; hi[nr] = r_hi; inv[nr] = jinv; sgn[nr] = s; rdof[nr] = d; lam[nr] = 0.0;
         nr++;
     }
+    if (st) { /* diagnostics only: the HIP kernel's limit-row skip criterion */
+        int far = 1;
+        for (int d = 0; d < nd; d++) {
+            double B = 0;
+            for (int k = 0; k < nd; k++) B += fabs(Minv[d * nd + k]) * (motors[k].max_impulse);
+            B = B * 1.001 + 1e-6;
+            double penl = q[d] - m->lower[d], penu = m->upper[d] - q[d];
+            far = far && penl > 0 && penu > 0 && (vu[d] - B) > -penl / dt && (vu[d] + B) < penu / dt;
+        }
+        st->limits_far = far;
+    }
     double dv[D] = {0};
     int it_used = 0;
     for (int it = 0; it < p->num_iterations; it++) {

@@ -29,6 +29,8 @@ typedef struct pgxo_stats {
     int32_t solver_iterations;
     int32_t ik_iterations;
     double ik_residual;
+    int32_t limits_far;   /* diagnostics: the kernel's exact limit-row skip test holds */
+    int32_t pad;
 } pgxo_stats;
 
 void pgxo_fk(const pgx_model* m, const double base[3], const double* q, double* com_pos,

@@ -10,7 +10,7 @@ import os
 
 from .abi import PgxConfig, PgxStepOut, PgxStateView
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpgx.so")
+LIB_PATH = os.environ.get("PGX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpgx.so")
 
 EXPORTS = [
     "pgx_version", "pgx_last_error", "pgx_obs_dim", "pgx_action_dim", "pgx_create", "pgx_destroy",

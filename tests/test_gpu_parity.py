@@ -78,15 +78,17 @@ def test_episode_trajectory_parity(pg, oracle):
     """Free-running rollout across an auto-reset.
 
     Positions (ee position, achieved goal) stay within 1e-4 of the oracle for the whole episode.
-    Velocities get 1e-3: the solver stops when the squared row residual <= 1e-7 (pybullet's
-    solverResidualThreshold), so a velocity is only defined to ~3.2e-4 rad/s and an fp32/fp64
-    difference in the exit iteration shows up as a velocity step of that size."""
+    Velocities: the solver stops when the squared row residual <= 1e-7 (pybullet's
+    solverResidualThreshold), so each joint velocity is only defined to sqrt(1e-7) = 3.2e-4 rad/s;
+    an fp32/fp64 difference in the exit sweep moves the EE velocity by up to sum_j |J_ij| * 3.2e-4
+    (~1e-3 m/s for the Panda's ~0.5 m lever arms).  Bound: max 2.5e-3, 99th percentile 3e-4
+    (DESIGN.md §5)."""
     n = 256
     venv = pg.PandaVecEnv("PandaReach-v3", num_envs=n, device="cuda:0", seed=11)
     venv.reset_tensors()
     ref = oracle.OracleVecEnv(venv._cfg, n)
     _state_to_oracle(venv, ref)
-    worst_pos, worst_vel = 0.0, 0.0
+    worst_pos, worst_vel, vel_err = 0.0, 0.0, []
     for t in range(60):
         acts = venv.sample_actions(t).clone()
         a_ref = ref.sample_actions(t)
@@ -107,8 +109,10 @@ def test_episode_trajectory_parity(pg, oracle):
         e = np.abs(g[0] - out["obs"])
         worst_pos = max(worst_pos, float(e[:, :3].max()), float(np.abs(g[1] - out["ag"]).max()))
         worst_vel = max(worst_vel, float(e[:, 3:].max()))
+        vel_err.append(e[:, 3:].max(axis=1))
     assert worst_pos <= OBS_TOL, f"trajectory position error {worst_pos}"
-    assert worst_vel <= 10 * OBS_TOL, f"trajectory velocity error {worst_vel}"
+    assert worst_vel <= 25 * OBS_TOL, f"trajectory velocity error {worst_vel}"
+    assert np.percentile(np.concatenate(vel_err), 99) <= 3 * OBS_TOL
     venv.close()
 
 
