@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-launches", type=int, default=200, help="launches for the kernel-time measurement")
+    ap.add_argument("--no-her", action="store_true", help="skip the HER relabel leg (BASELINE configs[3])")
+    ap.add_argument("--her-calls", type=int, default=50)
     return ap.parse_args()
 
 
@@ -72,6 +74,87 @@ def cpu_baseline(venv, seconds: float):
     return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": f"fp64 C oracle (CPU restatement, not PyBullet): {n} PandaReach envs x {steps} steps "
                       f"= {n * steps} env-steps in {dt:.1f} s on {threads} host threads"}
+
+
+# HER relabel leg: 16384 envs x one 50-step episode each in a 64-slot ring
+# (SB3 never validates an episode whose length equals the ring size), PickAndPlace rows
+# (obs 19, action 4), B = 2^20 samples per call, "future", her_ratio 0.8.
+HER_N, HER_C, HER_EP, HER_OD, HER_AD, HER_B = 16384, 64, 50, 19, 4, 1 << 20
+
+
+def her_alg_bytes(B: int, nbv: int, total: int, n_valid: int) -> int:
+    """Algorithmic HBM bytes of one sample() call (DESIGN.md "HER relabelling").
+
+    Per sample: valid index 4; rows obs+next_obs 2*4*od, action 4*ad, ag+next_ag 24, goal 12,
+    done+timeout 2; real rows add reward 4 + next_dg 12, relabelled rows add ep_start/ep_length 8;
+    writes 4*(2*od + ad + 12 + 2) + 12 (indices).  Compaction: ep_length read twice + valid write."""
+    od, ad = HER_OD, HER_AD
+    common = 4 + 8 * od + 4 * ad + 24 + 12 + 2 + 4 * (2 * od + ad + 12 + 2) + 12
+    return B * common + (B - nbv) * 16 + nbv * 8 + 8 * total + 4 * n_valid
+
+
+def her_leg(dev, calls: int, with_cpu: bool):
+    from panda_gym_amd.her import HerReplayBuffer
+
+    N, C, B = HER_N, HER_C, HER_B
+    buf = HerReplayBuffer(N * C, device=dev, n_envs=N, obs_dim=HER_OD, action_dim=HER_AD, seed=0,
+                          reward_type="sparse", goal_selection_strategy="future", n_sampled_goal=4)
+    g = torch.Generator(device=dev).manual_seed(0)
+    r = lambda *s: torch.rand(*s, generator=g, device=dev) * 0.3 - 0.15  # noqa: E731
+    for t in range(HER_EP):  # one full 50-step episode per env (PickAndPlace time limit), ends by time-out
+        done = torch.full((N,), int(t == HER_EP - 1), dtype=torch.uint8, device=dev)
+        buf.add_tensors(r(N, HER_OD), r(N, 3), r(N, 3), r(N, HER_AD), -torch.ones(N, device=dev), r(N, HER_OD),
+                        r(N, 3), r(N, 3), done, done)
+    out = buf.sample_raw(B)           # allocates the batch once, validates the ring
+    for _ in range(3):
+        buf.sample_into(out)
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    e0.record(stream)
+    for _ in range(calls):
+        buf.sample_into(out)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / calls
+    nbv = int(buf.her_ratio * B)
+    n_valid = int(buf._arrays()[2].item())
+    if n_valid != N * HER_EP:
+        raise RuntimeError(f"HER ring holds {n_valid} valid transitions, expected {N * HER_EP}")
+    alg = her_alg_bytes(B, nbv, N * C, n_valid)
+    achieved = alg / (ms * 1e-3) / 1e9
+    res = {"metric": "HER relabels/s (virtual transitions, future, her_ratio 0.8)", "value": nbv / (ms * 1e-3),
+           "unit": "relabels/s", "samples_per_s": B / (ms * 1e-3), "ms_per_call": ms, "calls": calls,
+           "config": {"workload": f"HER ring {N} envs x {HER_EP}-step episodes ({C} slots), obs {HER_OD}, "
+                                  f"action {HER_AD}, B={B} "
+                                  f"(BASELINE configs[3] relabel leg)", "batch": B, "relabels_per_call": nbv},
+           "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "sample call (4 kernels)",
+                        "alg_bytes_per_call": alg}}
+    if with_cpu:
+        from oracle import her as H
+
+        orc = H.HerOracle(N, C, HER_OD, HER_AD, seed=0)
+        # the numpy restatement samples its own ring of the same shape (contents do not change the work)
+        z = np.zeros
+        for t in range(HER_EP):
+            d = np.full(N, int(t == HER_EP - 1), np.uint8)
+            orc.add(z((N, HER_OD), np.float32), z((N, 3), np.float32), z((N, 3), np.float32),
+                    z((N, HER_AD), np.float32), z(N, np.float32), z((N, HER_OD), np.float32),
+                    z((N, 3), np.float32), z((N, 3), np.float32), d, d)
+        bs = 1 << 16
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < 5.0:
+            orc.sample(bs, n)
+            n += 1
+        dt = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": int(buf.her_ratio * bs) * n / dt, "unit": "relabels/s", "cores": 1,
+                               "kind": "port",
+                               "sample": f"numpy restatement of SB3 HerReplayBuffer.sample (oracle/her.py), "
+                                         f"{n} calls of B=2^16 on the same ring shape, 1 thread"}
+    buf.close()
+    return res
 
 
 def main():
@@ -163,6 +246,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(venv, args.cpu_baseline_seconds)
+        if world == 1 and not args.no_her:
+            line["her_relabel"] = her_leg(dev, args.her_calls, not args.no_cpu_baseline)
         print(json.dumps(line), flush=True)
     venv.close()
     if dist is not None:

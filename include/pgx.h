@@ -153,7 +153,8 @@ typedef struct pgx_env* pgx_handle;
  * obs [N,obs_dim] f32, achieved/desired [N,3] f32, reward [N] f32,
  * success/terminated/truncated [N] u8, terminal_obs [N,obs_dim] f32 (obs of the
  * finished episode, written only for envs that were auto-reset),
- * terminal_ag [N,3] f32. */
+ * terminal_ag / terminal_dg [N,3] f32 (achieved / desired goal of the finished
+ * episode: SB3 stores next_obs = infos["terminal_observation"] for them). */
 typedef struct pgx_step_out {
     float* obs;
     float* achieved_goal;
@@ -164,6 +165,7 @@ typedef struct pgx_step_out {
     uint8_t* truncated;
     float* terminal_obs;
     float* terminal_achieved_goal;
+    float* terminal_desired_goal;
 } pgx_step_out;
 
 /* Device-resident state views (SoA, env-minor: x[k*N + env]). */
@@ -208,6 +210,82 @@ int pgx_compute_reward(const float* achieved_goal, const float* desired_goal, in
 int pgx_state_bytes(pgx_handle h, int64_t* nbytes);
 int pgx_save_state(pgx_handle h, void* dst_device, void* stream);
 int pgx_restore_state(pgx_handle h, const void* src_device, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Device HER replay ring: the goal-relabelling replay buffer the reference's
+ * training uses (SB3 HerReplayBuffer / the fork's VecHerReplayBuffer,
+ * training/utils/setup_training.py:176-179; classes/train_config.py:15),
+ * "future" strategy, relabelled rewards from Task.compute_reward
+ * (reach.py:84-89 / pick_and_place.py:278-283) in float32.
+ *
+ * Storage is [capacity][n_envs] slot-major like SB3's (buffer_size, n_envs)
+ * arrays; add() writes one transition per env at the shared ring position and
+ * keeps SB3's episode bookkeeping (ep_start / ep_length, invalidation of an
+ * overwritten episode); sample() draws uniformly over valid transitions
+ * (ep_length > 0), relabels the first int(her_ratio*B) samples with the
+ * next_achieved_goal of a uniformly drawn transition t' in [t, episode end),
+ * and recomputes their rewards.  Draws come from the device Philox stream.
+ * ---------------------------------------------------------------------- */
+typedef struct pgx_replay* pgx_replay_handle;
+
+#define PGX_HER_FUTURE 0   /* t' uniform in [t, episode end) */
+#define PGX_HER_FINAL 1    /* t' = last transition of the episode */
+#define PGX_HER_EPISODE 2  /* t' uniform in [episode start, episode end) */
+
+typedef struct pgx_replay_config {
+    int32_t n_envs;
+    int32_t capacity;             /* transitions per env (SB3 buffer_size) */
+    int32_t obs_dim;
+    int32_t action_dim;
+    int32_t reward_type;          /* PGX_REWARD_* */
+    int32_t strategy;             /* PGX_HER_* goal selection (SB3 GoalSelectionStrategy) */
+    double distance_threshold;    /* 0.05 */
+    double her_ratio;             /* 1 - 1/(n_sampled_goal+1) = 0.8 */
+    uint64_t seed;
+} pgx_replay_config;
+
+/* One transition per env (device pointers): obs/next_obs [N,obs_dim], ag/dg/next_ag/next_dg
+ * [N,3], action [N,A] f32, reward [N] f32, done [N] u8, timeout [N] u8 (TimeLimit.truncated). */
+typedef struct pgx_transition {
+    const float* obs;
+    const float* achieved_goal;
+    const float* desired_goal;
+    const float* action;
+    const float* reward;
+    const float* next_obs;
+    const float* next_achieved_goal;
+    const float* next_desired_goal;
+    const uint8_t* done;
+    const uint8_t* timeout;
+} pgx_transition;
+
+/* Sampled, relabelled batch (device pointers, B rows).  dones = done * (1 - timeout).
+ * slot/env/goal_slot (optional, may be NULL): the drawn indices.  When no episode has
+ * completed yet (SB3 raises), every row gets slot = -1 and zeros. */
+typedef struct pgx_replay_batch {
+    float* obs;
+    float* achieved_goal;
+    float* desired_goal;
+    float* action;
+    float* reward;
+    float* next_obs;
+    float* next_achieved_goal;
+    float* next_desired_goal;
+    float* done;
+    int32_t* slot;
+    int32_t* env;
+    int32_t* goal_slot;           /* -1 for real (not relabelled) samples */
+} pgx_replay_batch;
+
+int pgx_replay_create(const pgx_replay_config* cfg, int device, pgx_replay_handle* out);
+void pgx_replay_destroy(pgx_replay_handle h);
+int pgx_replay_add(pgx_replay_handle h, const pgx_transition* t, void* stream);
+/* Number of transitions added per env so far (host-side counter, no sync). */
+int64_t pgx_replay_size(pgx_replay_handle h);
+int pgx_replay_sample(pgx_replay_handle h, int64_t batch, uint64_t draw, pgx_replay_batch* out, void* stream);
+/* Device views of the bookkeeping arrays [capacity][n_envs] i32 and of the valid-transition
+ * count computed by the last sample() (i32 scalar), for tests / checkpoint / the host guard. */
+int pgx_replay_episode_arrays(pgx_replay_handle h, int32_t** ep_start, int32_t** ep_length, int32_t** n_valid);
 
 #ifdef __cplusplus
 }

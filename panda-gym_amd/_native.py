@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-from .abi import PgxConfig, PgxStepOut, PgxStateView
+from .abi import PgxConfig, PgxReplayBatch, PgxReplayConfig, PgxStateView, PgxStepOut, PgxTransition
 
 LIB_PATH = os.environ.get("PGX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpgx.so")
 
@@ -16,6 +16,8 @@ EXPORTS = [
     "pgx_version", "pgx_last_error", "pgx_obs_dim", "pgx_action_dim", "pgx_create", "pgx_destroy",
     "pgx_get_state", "pgx_reset", "pgx_step", "pgx_sample_actions", "pgx_compute_reward",
     "pgx_state_bytes", "pgx_save_state", "pgx_restore_state",
+    "pgx_replay_create", "pgx_replay_destroy", "pgx_replay_add", "pgx_replay_size", "pgx_replay_sample",
+    "pgx_replay_episode_arrays",
 ]
 
 
@@ -53,6 +55,15 @@ def load(path: str = LIB_PATH):
     lib.pgx_state_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
     lib.pgx_save_state.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     lib.pgx_restore_state.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.pgx_replay_create.argtypes = [C.POINTER(PgxReplayConfig), C.c_int, C.POINTER(C.c_void_p)]
+    lib.pgx_replay_destroy.argtypes = [C.c_void_p]
+    lib.pgx_replay_destroy.restype = None
+    lib.pgx_replay_add.argtypes = [C.c_void_p, C.POINTER(PgxTransition), C.c_void_p]
+    lib.pgx_replay_size.argtypes = [C.c_void_p]
+    lib.pgx_replay_size.restype = C.c_int64
+    lib.pgx_replay_sample.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.POINTER(PgxReplayBatch), C.c_void_p]
+    lib.pgx_replay_episode_arrays.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                              C.POINTER(C.c_void_p)]
     _lib = lib
     return lib
 

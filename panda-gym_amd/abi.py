@@ -25,6 +25,8 @@ FLAG_CONSTRAINT_PASS_BIAS = 1
 FLAG_IK_COM = 2
 FLAG_NO_RESIDUAL_EXIT = 4
 
+HER_FUTURE, HER_FINAL, HER_EPISODE = 0, 1, 2
+
 PGX_OK = 0
 
 
@@ -71,6 +73,7 @@ class PgxStepOut(C.Structure):
         ("obs", C.c_void_p), ("achieved_goal", C.c_void_p), ("desired_goal", C.c_void_p),
         ("reward", C.c_void_p), ("success", C.c_void_p), ("terminated", C.c_void_p),
         ("truncated", C.c_void_p), ("terminal_obs", C.c_void_p), ("terminal_achieved_goal", C.c_void_p),
+        ("terminal_desired_goal", C.c_void_p),
     ]
 
 
@@ -78,6 +81,31 @@ class PgxStateView(C.Structure):
     _fields_ = [
         ("q", C.c_void_p), ("qd", C.c_void_p), ("goal", C.c_void_p), ("object", C.c_void_p),
         ("elapsed", C.c_void_p), ("episode", C.c_void_p),
+    ]
+
+
+class PgxReplayConfig(C.Structure):
+    _fields_ = [
+        ("n_envs", C.c_int32), ("capacity", C.c_int32), ("obs_dim", C.c_int32), ("action_dim", C.c_int32),
+        ("reward_type", C.c_int32), ("strategy", C.c_int32), ("distance_threshold", C.c_double),
+        ("her_ratio", C.c_double), ("seed", C.c_uint64),
+    ]
+
+
+class PgxTransition(C.Structure):
+    _fields_ = [
+        ("obs", C.c_void_p), ("achieved_goal", C.c_void_p), ("desired_goal", C.c_void_p), ("action", C.c_void_p),
+        ("reward", C.c_void_p), ("next_obs", C.c_void_p), ("next_achieved_goal", C.c_void_p),
+        ("next_desired_goal", C.c_void_p), ("done", C.c_void_p), ("timeout", C.c_void_p),
+    ]
+
+
+class PgxReplayBatch(C.Structure):
+    _fields_ = [
+        ("obs", C.c_void_p), ("achieved_goal", C.c_void_p), ("desired_goal", C.c_void_p), ("action", C.c_void_p),
+        ("reward", C.c_void_p), ("next_obs", C.c_void_p), ("next_achieved_goal", C.c_void_p),
+        ("next_desired_goal", C.c_void_p), ("done", C.c_void_p), ("slot", C.c_void_p), ("env", C.c_void_p),
+        ("goal_slot", C.c_void_p),
     ]
 
 

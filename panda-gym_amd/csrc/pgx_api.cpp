@@ -56,6 +56,11 @@ void m3v(const double* A, const double* v, double* o) {
 
 }  // namespace
 
+int pgx_set_error(int code, const char* msg) {
+    g_err = msg;
+    return code;
+}
+
 struct pgx_env {
     int device;
     PgxDevModel dm;      /* host copy */
@@ -320,6 +325,7 @@ static PgxDevOut to_dev_out(const pgx_step_out* o) {
     d.truncated = o->truncated;
     d.terminal_obs = o->terminal_obs;
     d.terminal_ag = o->terminal_achieved_goal;
+    d.terminal_dg = o->terminal_desired_goal;
     return d;
 }
 

@@ -67,6 +67,7 @@ struct PgxDevOut {
     uint8_t* truncated;
     float* terminal_obs;
     float* terminal_ag;
+    float* terminal_dg;
 };
 
 /* launchers (pgx_kernels.hip); return hipError_t as int */

@@ -23,6 +23,7 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "pgx_common.h"
 #include "pgx_dev.h"
 #include "pgx_model_consts.h"
 #include "pgx_rows.h"
@@ -606,19 +607,7 @@ __device__ __forceinline__ void ee_state(MRef m, const float* q, const float* qd
 }
 
 /* -------------------------------------------------------------- RNG */
-__device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
-                                       uint32_t* out) {
-#pragma unroll
-    for (int r = 0; r < 10; r++) {
-        uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-        uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-        uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-    }
-    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
-}
+/* philox(): pgx_common.h */
 constexpr uint32_t TAG_RESET = 0x52455345u;
 constexpr uint32_t TAG_ACTION = 0x41435430u;
 
@@ -639,15 +628,6 @@ __device__ double distance_f32_f64(V3 ag, const double* gl) {
     s = s + d2 * d2;
     double d = sqrt(s);
     return rint(d * 1e6) / 1e6;
-}
-/* utils.distance on float32 batches (HER compute_reward) */
-__device__ float distance_f32_f32(const float* a, const float* b) {
-    float d0 = a[0] - b[0], d1 = a[1] - b[1], d2 = a[2] - b[2];
-    float s = d0 * d0 + d1 * d1;
-    s = s + d2 * d2;
-    float d = sqrtf(s);
-    float y = rintf(d * 1e6f);
-    return y / 1e6f;
 }
 /* numpy Generator.uniform: low + (high - low) * u, unfused */
 __device__ double uniform_draw(double low, double high, double u) {
@@ -737,6 +717,10 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
             o.terminal_ag[3 * (size_t)i] = pos.x; o.terminal_ag[3 * (size_t)i + 1] = pos.y;
             o.terminal_ag[3 * (size_t)i + 2] = pos.z;
         }
+        if (o.terminal_dg) {
+            o.terminal_dg[3 * (size_t)i] = (float)goal[0]; o.terminal_dg[3 * (size_t)i + 1] = (float)goal[1];
+            o.terminal_dg[3 * (size_t)i + 2] = (float)goal[2];
+        }
         reset_env(m, e, i, episode, nullptr, q, qd, goal);
         el = 0;
         ee_state(m, q, qd, pos, vel);
@@ -809,8 +793,7 @@ __global__ __launch_bounds__(256) void compute_reward_kernel(const float* __rest
                                                              int64_t n, int32_t reward_type, float thr,
                                                              float* __restrict__ out) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        float d = distance_f32_f32(ag + 3 * i, dg + 3 * i);
-        out[i] = reward_type == 0 ? -((d > thr) ? 1.0f : 0.0f) : -d;
+        out[i] = reward_f32(distance_f32_f32(ag + 3 * i, dg + 3 * i), reward_type, thr);
     }
 }
 

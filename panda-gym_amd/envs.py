@@ -141,10 +141,12 @@ class PandaVecEnv:
         self.truncated = torch.zeros(n, dtype=torch.uint8, **kw)
         self.terminal_obs = torch.zeros((n, od), dtype=torch.float32, **kw)
         self.terminal_ag = torch.zeros((n, 3), dtype=torch.float32, **kw)
+        self.terminal_dg = torch.zeros((n, 3), dtype=torch.float32, **kw)
         self._actions = torch.zeros((n, self.action_dim), dtype=torch.float32, **kw)
         self._out = abi.PgxStepOut(self.obs.data_ptr(), self.achieved_goal.data_ptr(), self.desired_goal.data_ptr(),
                                    self.reward.data_ptr(), self.success.data_ptr(), self.terminated.data_ptr(),
-                                   self.truncated.data_ptr(), self.terminal_obs.data_ptr(), self.terminal_ag.data_ptr())
+                                   self.truncated.data_ptr(), self.terminal_obs.data_ptr(), self.terminal_ag.data_ptr(),
+                                   self.terminal_dg.data_ptr())
         self.observation_space = DictSpace(observation=Box(-10.0, 10.0, (od,)), desired_goal=Box(-10.0, 10.0, (3,)),
                                            achieved_goal=Box(-10.0, 10.0, (3,)))
         self.action_space = Box(-1.0, 1.0, (self.action_dim,))
@@ -254,9 +256,10 @@ class PandaVecEnv:
         if len(idx):
             tobs = self.terminal_obs.cpu().numpy()
             tag = self.terminal_ag.cpu().numpy()
+            tdg = self.terminal_dg.cpu().numpy()
             for i in idx:
                 infos[i]["terminal_observation"] = {"observation": tobs[i].copy(), "achieved_goal": tag[i].copy(),
-                                                    "desired_goal": o["desired_goal"][i].copy()}
+                                                    "desired_goal": tdg[i].copy()}
                 infos[i]["TimeLimit.truncated"] = bool(tr[i] and not te[i])
         return o, r, d, infos
 

@@ -88,7 +88,10 @@ def test_struct_layout_matches_c(tmp_path):
     fields = {"pgx_model": ["n_rows", "jpos", "jrot", "mass", "lower", "upper"],
               "pgx_sim_params": ["dt", "ik_max_angle", "n_substeps", "flags"],
               "pgx_config": ["seed", "base_pos", "joint_forces", "model", "params"],
-              "pgx_step_out": ["terminal_achieved_goal"], "pgx_state_view": ["episode"]}
+              "pgx_step_out": ["terminal_achieved_goal", "terminal_desired_goal"],
+              "pgx_replay_config": ["reward_type", "distance_threshold", "her_ratio", "seed"],
+              "pgx_transition": ["next_obs", "done", "timeout"],
+              "pgx_replay_batch": ["next_desired_goal", "done", "goal_slot"], "pgx_state_view": ["episode"]}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{ROOT}/include/pgx.h"', "int main(){"]
     for s, fs in fields.items():
         lines.append(f'printf("{s} %zu\\n", sizeof({s}));')
@@ -101,7 +104,9 @@ def test_struct_layout_matches_c(tmp_path):
     out = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], capture_output=True, text=True,
                                                           check=True).stdout.split("\n") if l)
     py = {"pgx_model": abi.PgxModel, "pgx_sim_params": abi.PgxSimParams, "pgx_config": abi.PgxConfig,
-          "pgx_step_out": abi.PgxStepOut, "pgx_state_view": abi.PgxStateView}
+          "pgx_step_out": abi.PgxStepOut, "pgx_state_view": abi.PgxStateView,
+          "pgx_replay_config": abi.PgxReplayConfig, "pgx_transition": abi.PgxTransition,
+          "pgx_replay_batch": abi.PgxReplayBatch}
     for s, cls in py.items():
         assert int(out[s]) == C.sizeof(cls), s
         for f in fields[s]:
