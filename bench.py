@@ -82,15 +82,12 @@ def cpu_baseline(venv, seconds: float):
 HER_N, HER_C, HER_EP, HER_OD, HER_AD, HER_B = 16384, 64, 50, 19, 4, 1 << 20
 
 
-def her_alg_bytes(B: int, nbv: int, total: int, n_valid: int) -> int:
+def her_alg_bytes(B: int, nbv: int, row_dim: int, row_stride: int) -> int:
     """Algorithmic HBM bytes of one sample() call (DESIGN.md "HER relabelling").
 
-    Per sample: valid index 4; rows obs+next_obs 2*4*od, action 4*ad, ag+next_ag 24, goal 12,
-    done+timeout 2; real rows add reward 4 + next_dg 12, relabelled rows add ep_start/ep_length 8;
-    writes 4*(2*od + ad + 12 + 2) + 12 (indices).  Compaction: ep_length read twice + valid write."""
-    od, ad = HER_OD, HER_AD
-    common = 4 + 8 * od + 4 * ad + 24 + 12 + 2 + 4 * (2 * od + ad + 12 + 2) + 12
-    return B * common + (B - nbv) * 16 + nbv * 8 + 8 * total + 4 * n_valid
+    Per draw: valid-list entry 4 B, the transition's row 4*row_dim B, the batch row written
+    4*row_stride B; relabelled draws also read ep_start/ep_length 8 B and the goal 12 B."""
+    return B * (4 + 4 * row_dim + 4 * row_stride) + nbv * (8 + 12)
 
 
 def her_leg(dev, calls: int, with_cpu: bool):
@@ -105,9 +102,13 @@ def her_leg(dev, calls: int, with_cpu: bool):
         done = torch.full((N,), int(t == HER_EP - 1), dtype=torch.uint8, device=dev)
         buf.add_tensors(r(N, HER_OD), r(N, 3), r(N, 3), r(N, HER_AD), -torch.ones(N, device=dev), r(N, HER_OD),
                         r(N, 3), r(N, 3), done, done)
-    out = buf.sample_raw(B)           # allocates the batch once, validates the ring
+    out = buf.alloc_batch(B, with_indices=False)   # what a learner consumes: the rows, no index outputs
+    buf.sample_into(out)
     for _ in range(3):
         buf.sample_into(out)
+    # one add() (ring write + valid-list refresh) timed separately: it is the other half of a step
+    obs_args = [r(N, HER_OD), r(N, 3), r(N, 3), r(N, HER_AD), r(N), r(N, HER_OD), r(N, 3), r(N, 3)]
+    zero = torch.zeros(N, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
@@ -117,19 +118,26 @@ def her_leg(dev, calls: int, with_cpu: bool):
     e1.record(stream)
     torch.cuda.synchronize(dev)
     ms = e0.elapsed_time(e1) / calls
+    torch.cuda.synchronize(dev)
+    e0.record(stream)
+    buf.add_tensors(*obs_args, zero, zero)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    add_ms = e0.elapsed_time(e1)
     nbv = int(buf.her_ratio * B)
     n_valid = int(buf._arrays()[2].item())
     if n_valid != N * HER_EP:
         raise RuntimeError(f"HER ring holds {n_valid} valid transitions, expected {N * HER_EP}")
-    alg = her_alg_bytes(B, nbv, N * C, n_valid)
+    alg = her_alg_bytes(B, nbv, buf.row_dim, buf.row_stride)
     achieved = alg / (ms * 1e-3) / 1e9
     res = {"metric": "HER relabels/s (virtual transitions, future, her_ratio 0.8)", "value": nbv / (ms * 1e-3),
            "unit": "relabels/s", "samples_per_s": B / (ms * 1e-3), "ms_per_call": ms, "calls": calls,
+           "ms_per_add": add_ms,
            "config": {"workload": f"HER ring {N} envs x {HER_EP}-step episodes ({C} slots), obs {HER_OD}, "
                                   f"action {HER_AD}, B={B} "
                                   f"(BASELINE configs[3] relabel leg)", "batch": B, "relabels_per_call": nbv},
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "sample call (4 kernels)",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "sample_kernel",
                         "alg_bytes_per_call": alg}}
     if with_cpu:
         from oracle import her as H

@@ -219,12 +219,20 @@ int pgx_restore_state(pgx_handle h, const void* src_device, void* stream);
  * (reach.py:84-89 / pick_and_place.py:278-283) in float32.
  *
  * Storage is [capacity][n_envs] slot-major like SB3's (buffer_size, n_envs)
- * arrays; add() writes one transition per env at the shared ring position and
- * keeps SB3's episode bookkeeping (ep_start / ep_length, invalidation of an
- * overwritten episode); sample() draws uniformly over valid transitions
- * (ep_length > 0), relabels the first int(her_ratio*B) samples with the
- * next_achieved_goal of a uniformly drawn transition t' in [t, episode end),
- * and recomputes their rewards.  Draws come from the device Philox stream.
+ * arrays, one padded record per transition so a sampled transition is one
+ * contiguous gather; add() writes one transition per env at the shared ring
+ * position, keeps SB3's episode bookkeeping (ep_start / ep_length,
+ * invalidation of an overwritten episode) and refreshes the list of valid
+ * transitions (ep_length > 0); sample() draws uniformly over that list,
+ * relabels the first int(her_ratio*B) draws with the next_achieved_goal of a
+ * transition t' of the same episode (strategy below) and recomputes their
+ * rewards.  Draws come from the device Philox stream.
+ *
+ * Batch row layout (floats), row_dim = 2*obs_dim + action_dim + 14, rows
+ * row_stride = round_up(row_dim, 4) apart:
+ *   obs[obs_dim] | achieved_goal[3] | desired_goal[3] | action[action_dim] |
+ *   reward | next_obs[obs_dim] | next_achieved_goal[3] | next_desired_goal[3] | done
+ * SB3 order: the B - int(her_ratio*B) real rows first, then the relabelled rows.
  * ---------------------------------------------------------------------- */
 typedef struct pgx_replay* pgx_replay_handle;
 
@@ -259,32 +267,28 @@ typedef struct pgx_transition {
     const uint8_t* timeout;
 } pgx_transition;
 
-/* Sampled, relabelled batch (device pointers, B rows).  dones = done * (1 - timeout).
- * slot/env/goal_slot (optional, may be NULL): the drawn indices.  When no episode has
- * completed yet (SB3 raises), every row gets slot = -1 and zeros. */
+/* Sampled, relabelled batch (device pointers).  rows [B, row_stride] f32 in the layout
+ * above; done = done * (1 - timeout).  slot/env/goal_slot [B] i32 (optional, may be NULL):
+ * the drawn indices, goal_slot -1 for real rows.  When no episode has completed yet (SB3
+ * raises), every row is zero and slot = -1. */
 typedef struct pgx_replay_batch {
-    float* obs;
-    float* achieved_goal;
-    float* desired_goal;
-    float* action;
-    float* reward;
-    float* next_obs;
-    float* next_achieved_goal;
-    float* next_desired_goal;
-    float* done;
+    float* rows;
     int32_t* slot;
     int32_t* env;
-    int32_t* goal_slot;           /* -1 for real (not relabelled) samples */
+    int32_t* goal_slot;
 } pgx_replay_batch;
 
+/* row_dim / row_stride of a batch row for this config (floats). */
+int pgx_replay_row_dim(const pgx_replay_config* cfg);
+int pgx_replay_row_stride(const pgx_replay_config* cfg);
 int pgx_replay_create(const pgx_replay_config* cfg, int device, pgx_replay_handle* out);
 void pgx_replay_destroy(pgx_replay_handle h);
 int pgx_replay_add(pgx_replay_handle h, const pgx_transition* t, void* stream);
 /* Number of transitions added per env so far (host-side counter, no sync). */
 int64_t pgx_replay_size(pgx_replay_handle h);
 int pgx_replay_sample(pgx_replay_handle h, int64_t batch, uint64_t draw, pgx_replay_batch* out, void* stream);
-/* Device views of the bookkeeping arrays [capacity][n_envs] i32 and of the valid-transition
- * count computed by the last sample() (i32 scalar), for tests / checkpoint / the host guard. */
+/* Device views of the bookkeeping arrays [capacity][n_envs] i32 and of the number of valid
+ * transitions after the last add() (i32 scalar), for tests / checkpoint / the host guard. */
 int pgx_replay_episode_arrays(pgx_replay_handle h, int32_t** ep_start, int32_t** ep_length, int32_t** n_valid);
 
 #ifdef __cplusplus

@@ -17,7 +17,7 @@ EXPORTS = [
     "pgx_get_state", "pgx_reset", "pgx_step", "pgx_sample_actions", "pgx_compute_reward",
     "pgx_state_bytes", "pgx_save_state", "pgx_restore_state",
     "pgx_replay_create", "pgx_replay_destroy", "pgx_replay_add", "pgx_replay_size", "pgx_replay_sample",
-    "pgx_replay_episode_arrays",
+    "pgx_replay_episode_arrays", "pgx_replay_row_dim", "pgx_replay_row_stride",
 ]
 
 
@@ -56,6 +56,8 @@ def load(path: str = LIB_PATH):
     lib.pgx_save_state.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     lib.pgx_restore_state.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     lib.pgx_replay_create.argtypes = [C.POINTER(PgxReplayConfig), C.c_int, C.POINTER(C.c_void_p)]
+    lib.pgx_replay_row_dim.argtypes = [C.POINTER(PgxReplayConfig)]
+    lib.pgx_replay_row_stride.argtypes = [C.POINTER(PgxReplayConfig)]
     lib.pgx_replay_destroy.argtypes = [C.c_void_p]
     lib.pgx_replay_destroy.restype = None
     lib.pgx_replay_add.argtypes = [C.c_void_p, C.POINTER(PgxTransition), C.c_void_p]

@@ -101,12 +101,18 @@ class PgxTransition(C.Structure):
 
 
 class PgxReplayBatch(C.Structure):
-    _fields_ = [
-        ("obs", C.c_void_p), ("achieved_goal", C.c_void_p), ("desired_goal", C.c_void_p), ("action", C.c_void_p),
-        ("reward", C.c_void_p), ("next_obs", C.c_void_p), ("next_achieved_goal", C.c_void_p),
-        ("next_desired_goal", C.c_void_p), ("done", C.c_void_p), ("slot", C.c_void_p), ("env", C.c_void_p),
-        ("goal_slot", C.c_void_p),
-    ]
+    _fields_ = [("rows", C.c_void_p), ("slot", C.c_void_p), ("env", C.c_void_p), ("goal_slot", C.c_void_p)]
+
+
+def replay_row_fields(obs_dim: int, action_dim: int):
+    """(name, offset, width) of the batch row layout of include/pgx.h, plus row_dim."""
+    f, o = [], 0
+    for name, w in (("obs", obs_dim), ("achieved_goal", 3), ("desired_goal", 3), ("action", action_dim),
+                    ("reward", 1), ("next_obs", obs_dim), ("next_achieved_goal", 3), ("next_desired_goal", 3),
+                    ("done", 1)):
+        f.append((name, o, w))
+        o += w
+    return f, o
 
 
 def make_model(model: Model, ee_link: int = 11) -> PgxModel:

@@ -1,27 +1,36 @@
 /*
- * pgx_her.hip -- device HER replay ring ("future" goal relabelling) for gfx950.
+ * pgx_her.hip -- device HER replay ring (goal relabelling) for gfx950.
  *
  * Restates stable-baselines3's HerReplayBuffer as used by the reference's
- * training (setup_training.py:176-179, replay_buffer_class=HerReplayBuffer /
- * the fork's VecHerReplayBuffer; n_sampled_goal 4 -> her_ratio 0.8):
+ * training (setup_training.py:14,176-179, classes/train_config.py:15;
+ * n_sampled_goal 4 -> her_ratio 0.8):
  *   add():    SB3 HerReplayBuffer.add -- invalidate the old episode being
  *             overwritten at `pos`, ep_start[pos] = current episode start,
- *             store, and on done write the episode length over the episode.
- *   sample(): valid = flatnonzero(ep_length > 0) (slot-major, env-minor),
- *             uniform draw over valid, the first int(her_ratio*B) samples are
- *             virtual: goal = next_achieved_goal[t'] with t' uniform in
- *             [t, episode end) ("future", inclusive), reward =
+ *             store, and on done write the episode length over the episode;
+ *             then refresh valid = flatnonzero(ep_length > 0) (slot-major,
+ *             env-minor), the only state sample() depends on besides the ring.
+ *   sample(): uniform draw over valid; the first int(her_ratio*B) draws are
+ *             virtual: goal = next_achieved_goal[t'] with t' from the episode
+ *             of t ("future": uniform in [t, end)), reward =
  *             compute_reward(next_achieved_goal[t], goal) in float32
- *             (reach.py:84-89 on float32 arrays: utils.distance rounds in f32);
- *             dones = done * (1 - timeout).
+ *             (reach.py:84-89 on float32 arrays); dones = done * (1 - timeout);
+ *             output rows real first, then virtual (SB3 concatenation order).
  * Draws: Philox4x32-10, key = buffer seed, counter = (sample lo, sample hi,
  * draw lo, TAG_HER ^ draw hi); u0 = top 53 bits of words 0-1 picks the
- * transition (floor(u0 * n_valid)), u1 of words 2-3 picks t' (floor(u1 * (len - t))).
+ * transition (floor(u0 * n_valid)), u1 of words 2-3 picks t'.
  *
- * Layout: every per-transition array is [capacity][n_envs][dim] so a slot is
- * one contiguous block (add() writes are coalesced; sample() gathers rows).
- * sample() is an HBM-bound gather: one 16-lane group per sample copies the
- * rows with consecutive lanes on consecutive floats.
+ * Layout (HBM): one record of R floats per (slot, env), R = round_up(row_dim
+ * + 2, 32) -- the batch row (pgx.h) followed by the transition's ep_start and
+ * ep_length -- so a sampled transition is R*4 contiguous bytes (2 x 128 B
+ * lines for PickAndPlace) instead of a dozen scattered field rows.  Dense
+ * ep_start/ep_length [C][N] arrays carry SB3's bookkeeping (compaction reads
+ * 4 B per transition); the record copy of ep_length is refreshed whenever an
+ * episode completes and only read for transitions the dense array marks valid.
+ *
+ * sample(): one wave per 64 draws.  Phase 1: lane i draws sample i (Philox,
+ * valid-list lookup, episode fields, goal, relabelled reward) into LDS.
+ * Phase 2: 16-lane groups copy 4 records at a time with float4 loads/stores,
+ * patching desired goals and reward of the relabelled rows.
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -31,54 +40,101 @@
 
 namespace {
 
+constexpr uint32_t TAG_HER = 0x48455230u;
+constexpr int GROUP = 16;  /* lanes per record copy (float4 each) */
+
 struct RingPtrs {
-    float *obs, *ag, *dg, *action, *reward, *next_obs, *next_ag, *next_dg;
-    uint8_t *done, *timeout;
+    float* rec;                 /* [C][N][R] */
     int32_t *ep_start, *ep_length, *cur_ep_start;
     int32_t *valid, *block_count, *n_valid;
 };
 
+/* field offsets inside a row / record (floats) */
 struct RingDims {
     int32_t n, cap, od, ad;
+    int32_t R, S;               /* record stride, batch row stride */
+    int32_t ag, dg, act, rew, nobs, nag, ndg, done, eps, epl;
 };
 
-constexpr uint32_t TAG_HER = 0x48455230u;
+RingDims make_dims(const pgx_replay_config& c) {
+    RingDims d{};
+    d.n = c.n_envs;
+    d.cap = c.capacity;
+    d.od = c.obs_dim;
+    d.ad = c.action_dim;
+    d.ag = d.od;
+    d.dg = d.ag + 3;
+    d.act = d.dg + 3;
+    d.rew = d.act + d.ad;
+    d.nobs = d.rew + 1;
+    d.nag = d.nobs + d.od;
+    d.ndg = d.nag + 3;
+    d.done = d.ndg + 3;
+    d.eps = d.done + 1;        /* == row_dim */
+    d.epl = d.eps + 1;
+    d.S = (d.eps + 3) & ~3;
+    d.R = (d.epl + 1 + 31) & ~31;
+    return d;
+}
+
+__device__ __forceinline__ float ibits(int32_t v) { return __int_as_float(v); }
+__device__ __forceinline__ int32_t fbits(float v) { return __float_as_int(v); }
 
 /* ------------------------------------------------------------------ add */
-__global__ __launch_bounds__(256) void add_kernel(RingPtrs p, RingDims d, int32_t pos, pgx_transition t) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+/* value of record float f for env e of transition t */
+__device__ __forceinline__ float record_value(const RingDims& d, const pgx_transition& t, int e, int f, float dones,
+                                              int32_t cur, int32_t len) {
+    if (f < d.ag) return t.obs[(size_t)e * d.od + f];
+    if (f < d.dg) return t.achieved_goal[(size_t)e * 3 + (f - d.ag)];
+    if (f < d.act) return t.desired_goal[(size_t)e * 3 + (f - d.dg)];
+    if (f < d.rew) return t.action[(size_t)e * d.ad + (f - d.act)];
+    if (f == d.rew) return t.reward[e];
+    if (f < d.nag) return t.next_obs[(size_t)e * d.od + (f - d.nobs)];
+    if (f < d.ndg) return t.next_achieved_goal[(size_t)e * 3 + (f - d.nag)];
+    if (f < d.done) return t.next_desired_goal[(size_t)e * 3 + (f - d.ndg)];
+    if (f == d.done) return dones;
+    if (f == d.eps) return ibits(cur);
+    if (f == d.epl) return ibits(len);
+    return 0.0f;
+}
+
+__global__ __launch_bounds__(64) void add_kernel(RingPtrs p, RingDims d, int32_t pos, pgx_transition t) {
+    const int g = threadIdx.x % GROUP;
+    const int e = blockIdx.x * (64 / GROUP) + threadIdx.x / GROUP;
     const int N = d.n, C = d.cap;
     if (e >= N) return;
     const size_t se = (size_t)pos * N + e;
+    const int32_t cur = p.cur_ep_start[e];
+    const bool dn = t.done[e] != 0;
+    const bool to = t.timeout ? t.timeout[e] != 0 : false;
+    int32_t end = (pos + 1) % C;
+    if (end < cur) end += C;
+    const int32_t len = dn ? end - cur : 0;
+    /* SB3 stores done and timeout; sample() only ever uses done * (1 - timeout) */
+    const float dones = (float)dn * (1.0f - (float)to);
+    float* rec = p.rec + se * d.R;
+    for (int c = g; 4 * c < d.R; c += GROUP) {
+        float4 v;
+        v.x = record_value(d, t, e, 4 * c + 0, dones, cur, len);
+        v.y = record_value(d, t, e, 4 * c + 1, dones, cur, len);
+        v.z = record_value(d, t, e, 4 * c + 2, dones, cur, len);
+        v.w = record_value(d, t, e, 4 * c + 3, dones, cur, len);
+        *reinterpret_cast<float4*>(rec + 4 * c) = v;
+    }
+    if (g != 0) return;
     /* an old episode is being overwritten: its remaining transitions become invalid */
     const int32_t old_len = p.ep_length[se];
     if (old_len > 0) {
-        const int32_t end = p.ep_start[se] + old_len;
-        for (int32_t k = pos; k < end; k++) p.ep_length[(size_t)(k % C) * N + e] = 0;
+        const int32_t old_end = p.ep_start[se] + old_len;
+        for (int32_t k = pos; k < old_end; k++) p.ep_length[(size_t)(k % C) * N + e] = 0;
     }
-    p.ep_start[se] = p.cur_ep_start[e];
-    for (int k = 0; k < d.od; k++) {
-        p.obs[se * d.od + k] = t.obs[(size_t)e * d.od + k];
-        p.next_obs[se * d.od + k] = t.next_obs[(size_t)e * d.od + k];
-    }
-    for (int k = 0; k < 3; k++) {
-        p.ag[se * 3 + k] = t.achieved_goal[(size_t)e * 3 + k];
-        p.dg[se * 3 + k] = t.desired_goal[(size_t)e * 3 + k];
-        p.next_ag[se * 3 + k] = t.next_achieved_goal[(size_t)e * 3 + k];
-        p.next_dg[se * 3 + k] = t.next_desired_goal[(size_t)e * 3 + k];
-    }
-    for (int k = 0; k < d.ad; k++) p.action[se * d.ad + k] = t.action[(size_t)e * d.ad + k];
-    p.reward[se] = t.reward[e];
-    const uint8_t dn = t.done[e];
-    p.done[se] = dn;
-    p.timeout[se] = t.timeout ? t.timeout[e] : 0;
-    /* the ring was written before ep_length is set below: SB3 stores then computes lengths */
-    if (dn) {
-        const int32_t start = p.cur_ep_start[e];
-        int32_t end = (pos + 1) % C;
-        if (end < start) end += C;
-        const int32_t len = end - start;
-        for (int32_t k = start; k < end; k++) p.ep_length[(size_t)(k % C) * N + e] = len;
+    p.ep_start[se] = cur;
+    if (dn) {  /* SB3 _compute_episode_length: the new episode spans [cur, end) */
+        for (int32_t k = cur; k < end; k++) {
+            const size_t sk = (size_t)(k % C) * N + e;
+            p.ep_length[sk] = len;
+            if (k % C != pos) p.rec[sk * d.R + d.epl] = ibits(len);  /* own record written above */
+        }
         p.cur_ep_start[e] = (pos + 1) % C;
     }
 }
@@ -142,81 +198,92 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scatter_kernel(RingPtrs p, int64_t
 }
 
 /* ---------------------------------------------------------------- sample */
+struct Draw {
+    int64_t rec;    /* record index (slot * N + env), -1: no valid transition */
+    int64_t row;    /* output row */
+    float goal[3];
+    float reward;
+    int32_t her;
+    int32_t pad;
+};
 
-constexpr int GROUP = 16;  /* lanes per sample */
-
-__global__ __launch_bounds__(256) void sample_kernel(RingPtrs p, RingDims d, int64_t B, int64_t nb_virtual,
-                                                     uint64_t seed, uint64_t draw, int32_t reward_type,
-                                                     int32_t strategy, float thr, pgx_replay_batch o) {
-    const int lane = threadIdx.x % GROUP;
-    const int64_t b = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / GROUP;
-    if (b >= B) return;
+__global__ __launch_bounds__(64) void sample_kernel(RingPtrs p, RingDims d, int64_t B, int64_t nb_virtual,
+                                                    uint64_t seed, uint64_t draw, int32_t reward_type,
+                                                    int32_t strategy, float thr, pgx_replay_batch o) {
+    __shared__ Draw dr[64];
+    const int lane = threadIdx.x;
+    const int64_t b0 = (int64_t)blockIdx.x * 64;
     const int N = d.n, C = d.cap;
     const int32_t nv = *p.n_valid;
-    if (nv <= 0) {  /* no finished episode yet: SB3 raises; mark the rows invalid */
-        for (int k = lane; k < d.od; k += GROUP) o.obs[b * d.od + k] = o.next_obs[b * d.od + k] = 0.0f;
-        for (int k = lane; k < d.ad; k += GROUP) o.action[b * d.ad + k] = 0.0f;
-        if (lane < 3)
-            o.achieved_goal[b * 3 + lane] = o.next_achieved_goal[b * 3 + lane] = o.desired_goal[b * 3 + lane] =
-                o.next_desired_goal[b * 3 + lane] = 0.0f;
-        if (lane == 0) {
-            o.reward[b] = o.done[b] = 0.0f;
-            if (o.slot) o.slot[b] = -1;
-            if (o.env) o.env[b] = -1;
-            if (o.goal_slot) o.goal_slot[b] = -1;
+    /* phase 1: lane `lane` draws sample b0 + lane */
+    {
+        const int64_t b = b0 + lane;
+        Draw w{};
+        w.rec = -1;
+        if (b < B) {
+            const bool her = b < nb_virtual;
+            w.row = her ? B - nb_virtual + b : b - nb_virtual;
+            w.her = her;
+            int32_t slot = -1, env = -1, goal_slot = -1;
+            if (nv > 0) {
+                uint32_t r[4];
+                philox((uint32_t)b, (uint32_t)(b >> 32), (uint32_t)draw, TAG_HER ^ (uint32_t)(draw >> 32),
+                       (uint32_t)seed, (uint32_t)(seed >> 32), r);
+                const double u0 = u53(r[0], r[1]), u1 = u53(r[2], r[3]);
+                int64_t j = (int64_t)(u0 * (double)nv);
+                if (j >= nv) j = nv - 1;
+                const int32_t flat = p.valid[j];
+                slot = flat / N;
+                env = flat % N;
+                w.rec = flat;
+                if (her) {
+                    const float* rc = p.rec + (size_t)flat * d.R;
+                    const int32_t start = fbits(rc[d.eps]), len = fbits(rc[d.epl]);
+                    const int32_t cur = ((slot - start) % C + C) % C;
+                    int32_t t_in;
+                    if (strategy == PGX_HER_FINAL) t_in = len - 1;
+                    else if (strategy == PGX_HER_EPISODE) t_in = (int32_t)(u1 * (double)len);
+                    else t_in = cur + (int32_t)(u1 * (double)(len - cur));
+                    goal_slot = (t_in + start) % C;
+                    const float* gr = p.rec + ((size_t)goal_slot * N + env) * d.R + d.nag;
+                    w.goal[0] = gr[0]; w.goal[1] = gr[1]; w.goal[2] = gr[2];
+                    w.reward = reward_f32(distance_f32_f32(rc + d.nag, w.goal), reward_type, thr);
+                }
+            }
+            if (o.slot) o.slot[w.row] = slot;
+            if (o.env) o.env[w.row] = env;
+            if (o.goal_slot) o.goal_slot[w.row] = goal_slot;
         }
-        return;
+        dr[lane] = w;
     }
-    uint32_t r[4];
-    philox((uint32_t)b, (uint32_t)(b >> 32), (uint32_t)draw, TAG_HER ^ (uint32_t)(draw >> 32), (uint32_t)seed,
-           (uint32_t)(seed >> 32), r);
-    const double u0 = u53(r[0], r[1]), u1 = u53(r[2], r[3]);
-    int64_t j = (int64_t)(u0 * (double)nv);
-    if (j >= nv) j = nv - 1;
-    const int32_t flat = p.valid[j];
-    const int32_t slot = flat / N, env = flat % N;
-    const size_t se = (size_t)slot * N + env;
-    const bool her = b < nb_virtual;
-    size_t ge = se;  /* row of the goal */
-    int32_t goal_slot = -1;
-    if (her) {
-        const int32_t start = p.ep_start[se], len = p.ep_length[se];
-        const int32_t cur = ((slot - start) % C + C) % C;
-        int32_t t_in;
-        if (strategy == PGX_HER_FINAL) t_in = len - 1;
-        else if (strategy == PGX_HER_EPISODE) t_in = (int32_t)(u1 * (double)len);
-        else t_in = cur + (int32_t)(u1 * (double)(len - cur));
-        goal_slot = (t_in + start) % C;
-        ge = (size_t)goal_slot * N + env;
-    }
-    const float* goal = her ? p.next_ag + ge * 3 : p.dg + se * 3;
-    const float* ngoal = her ? p.next_ag + ge * 3 : p.next_dg + se * 3;
-    /* SB3 concatenates (real, virtual): draw b < nb_virtual lands after the B - nb_virtual real rows */
-    const int64_t row = her ? B - nb_virtual + b : b - nb_virtual;
-    /* rows: consecutive lanes copy consecutive floats */
-    for (int k = lane; k < d.od; k += GROUP) {
-        o.obs[row * d.od + k] = p.obs[se * d.od + k];
-        o.next_obs[row * d.od + k] = p.next_obs[se * d.od + k];
-    }
-    for (int k = lane; k < d.ad; k += GROUP) o.action[row * d.ad + k] = p.action[se * d.ad + k];
-    if (lane < 3) {
-        o.achieved_goal[row * 3 + lane] = p.ag[se * 3 + lane];
-        o.next_achieved_goal[row * 3 + lane] = p.next_ag[se * 3 + lane];
-        o.desired_goal[row * 3 + lane] = goal[lane];
-        o.next_desired_goal[row * 3 + lane] = ngoal[lane];
-    }
-    if (lane == 0) {
-        float rew;
-        if (her) {
-            rew = reward_f32(distance_f32_f32(p.next_ag + se * 3, goal), reward_type, thr);
-        } else {
-            rew = p.reward[se];
+    __syncthreads();
+    /* phase 2: 16-lane groups copy 4 records per iteration */
+    const int g = lane % GROUP;
+    for (int s = lane / GROUP; s < 64 && b0 + s < B; s += 64 / GROUP) {
+        const Draw& w = dr[s];
+        float* out = o.rows + w.row * d.S;
+        for (int c = g; 4 * c < d.S; c += GROUP) {
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (w.rec >= 0) {
+                v = *reinterpret_cast<const float4*>(p.rec + w.rec * d.R + 4 * c);
+                if (w.her) {
+                    float* vv = reinterpret_cast<float*>(&v);
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const int f = 4 * c + k;
+                        if (f >= d.dg && f < d.dg + 3) vv[k] = w.goal[f - d.dg];
+                        else if (f >= d.ndg && f < d.ndg + 3) vv[k] = w.goal[f - d.ndg];
+                        else if (f == d.rew) vv[k] = w.reward;
+                    }
+                }
+            }
+            /* the record's ep_start/ep_length may share the last float4: not part of a row */
+            float* vv = reinterpret_cast<float*>(&v);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (4 * c + k >= d.eps) vv[k] = 0.0f;
+            *reinterpret_cast<float4*>(out + 4 * c) = v;
         }
-        o.reward[row] = rew;
-        o.done[row] = (float)p.done[se] * (1.0f - (float)p.timeout[se]);
-        if (o.slot) o.slot[row] = slot;
-        if (o.env) o.env[row] = env;
-        if (o.goal_slot) o.goal_slot[row] = goal_slot;
     }
 }
 
@@ -236,6 +303,16 @@ int pgx_set_error(int code, const char* msg);  /* pgx_api.cpp: sets pgx_last_err
 
 extern "C" {
 
+int pgx_replay_row_dim(const pgx_replay_config* cfg) {
+    if (!cfg || cfg->obs_dim <= 0 || cfg->action_dim <= 0) return PGX_E_INVALID;
+    return make_dims(*cfg).eps;
+}
+
+int pgx_replay_row_stride(const pgx_replay_config* cfg) {
+    if (!cfg || cfg->obs_dim <= 0 || cfg->action_dim <= 0) return PGX_E_INVALID;
+    return make_dims(*cfg).S;
+}
+
 int pgx_replay_create(const pgx_replay_config* cfg, int device, pgx_replay_handle* out) {
     if (!cfg || !out || cfg->n_envs <= 0 || cfg->capacity <= 1 || cfg->obs_dim <= 0 || cfg->action_dim <= 0)
         return pgx_set_error(PGX_E_INVALID, "pgx_replay_create: bad config (n_envs, capacity > 1, dims > 0)");
@@ -248,17 +325,17 @@ int pgx_replay_create(const pgx_replay_config* cfg, int device, pgx_replay_handl
     if (cfg->strategy < PGX_HER_FUTURE || cfg->strategy > PGX_HER_EPISODE)
         return pgx_set_error(PGX_E_INVALID, "pgx_replay_create: unknown goal selection strategy");
     *out = nullptr;
-    if (hipSetDevice(device) != hipSuccess) return PGX_E_HIP;
+    if (hipSetDevice(device) != hipSuccess) return pgx_set_error(PGX_E_HIP, "pgx_replay_create: hipSetDevice");
     pgx_replay* h = new pgx_replay();
     h->device = device;
     h->cfg = *cfg;
-    const size_t N = cfg->n_envs, C = cfg->capacity, od = cfg->obs_dim, ad = cfg->action_dim, T = N * C;
+    h->d = make_dims(*cfg);
+    const size_t N = cfg->n_envs, C = cfg->capacity, T = N * C;
     const size_t nblocks = (T + SCAN_BLOCK - 1) / SCAN_BLOCK;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    size_t sizes[] = {T * od * 4, T * 12, T * 12, T * ad * 4, T * 4, T * od * 4, T * 12, T * 12, T, T,
-                      T * 4, T * 4, N * 4, T * 4, nblocks * 4, 4};
-    size_t off[16], total = 0;
-    for (int i = 0; i < 16; i++) { off[i] = total; total = al(total + sizes[i]); }
+    const size_t sizes[] = {T * h->d.R * 4, T * 4, T * 4, N * 4, T * 4, nblocks * 4, 4};
+    size_t off[7], total = 0;
+    for (int i = 0; i < 7; i++) { off[i] = total; total = al(total + sizes[i]); }
     if (hipMalloc(&h->blob, total) != hipSuccess) {
         delete h;
         return pgx_set_error(PGX_E_NOMEM, "pgx_replay_create: hipMalloc failed");
@@ -270,13 +347,13 @@ int pgx_replay_create(const pgx_replay_config* cfg, int device, pgx_replay_handl
     }
     char* b = (char*)h->blob;
     RingPtrs& p = h->p;
-    p.obs = (float*)(b + off[0]); p.ag = (float*)(b + off[1]); p.dg = (float*)(b + off[2]);
-    p.action = (float*)(b + off[3]); p.reward = (float*)(b + off[4]); p.next_obs = (float*)(b + off[5]);
-    p.next_ag = (float*)(b + off[6]); p.next_dg = (float*)(b + off[7]); p.done = (uint8_t*)(b + off[8]);
-    p.timeout = (uint8_t*)(b + off[9]); p.ep_start = (int32_t*)(b + off[10]); p.ep_length = (int32_t*)(b + off[11]);
-    p.cur_ep_start = (int32_t*)(b + off[12]); p.valid = (int32_t*)(b + off[13]);
-    p.block_count = (int32_t*)(b + off[14]); p.n_valid = (int32_t*)(b + off[15]);
-    h->d = RingDims{cfg->n_envs, cfg->capacity, cfg->obs_dim, cfg->action_dim};
+    p.rec = (float*)(b + off[0]);
+    p.ep_start = (int32_t*)(b + off[1]);
+    p.ep_length = (int32_t*)(b + off[2]);
+    p.cur_ep_start = (int32_t*)(b + off[3]);
+    p.valid = (int32_t*)(b + off[4]);
+    p.block_count = (int32_t*)(b + off[5]);
+    p.n_valid = (int32_t*)(b + off[6]);
     h->pos = 0;
     h->added = 0;
     *out = h;
@@ -294,8 +371,15 @@ int pgx_replay_add(pgx_replay_handle h, const pgx_transition* t, void* stream) {
     if (!h || !t || !t->obs || !t->achieved_goal || !t->desired_goal || !t->action || !t->reward || !t->next_obs ||
         !t->next_achieved_goal || !t->next_desired_goal || !t->done)
         return pgx_set_error(PGX_E_INVALID, "pgx_replay_add: null handle or transition pointer");
+    hipStream_t st = (hipStream_t)stream;
     const int N = h->d.n;
-    hipLaunchKernelGGL(add_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, h->p, h->d, h->pos, *t);
+    const int per_block = 64 / GROUP;
+    hipLaunchKernelGGL(add_kernel, dim3((N + per_block - 1) / per_block), dim3(64), 0, st, h->p, h->d, h->pos, *t);
+    const int64_t total = (int64_t)h->d.n * h->d.cap;
+    const int32_t nblocks = (int32_t)((total + SCAN_BLOCK - 1) / SCAN_BLOCK);
+    hipLaunchKernelGGL(count_kernel, dim3(nblocks), dim3(SCAN_BLOCK), 0, st, h->p, total);
+    hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(1024), 0, st, h->p, nblocks);
+    hipLaunchKernelGGL(scatter_kernel, dim3(nblocks), dim3(SCAN_BLOCK), 0, st, h->p, total);
     if (hipGetLastError() != hipSuccess) return pgx_set_error(PGX_E_HIP, "pgx_replay_add: launch failed");
     h->pos = (h->pos + 1) % h->d.cap;
     h->added += 1;
@@ -307,20 +391,13 @@ int64_t pgx_replay_size(pgx_replay_handle h) { return h ? h->added : PGX_E_INVAL
 int pgx_replay_sample(pgx_replay_handle h, int64_t batch, uint64_t draw, pgx_replay_batch* out, void* stream) {
     if (!h || !out || batch <= 0 || batch > (1ll << 26))
         return pgx_set_error(PGX_E_INVALID, "pgx_replay_sample: null handle or batch not in [1, 2^26]");
-    if (!out->obs || !out->achieved_goal || !out->desired_goal || !out->action || !out->reward || !out->next_obs ||
-        !out->next_achieved_goal || !out->next_desired_goal || !out->done)
-        return pgx_set_error(PGX_E_INVALID, "pgx_replay_sample: null output pointer");
+    if (!out->rows) return pgx_set_error(PGX_E_INVALID, "pgx_replay_sample: null rows pointer");
+    if (((uintptr_t)out->rows & 15) != 0) return pgx_set_error(PGX_E_INVALID, "pgx_replay_sample: rows not 16 B aligned");
     if (h->added == 0) return pgx_set_error(PGX_E_INVALID, "pgx_replay_sample: buffer is empty");
-    hipStream_t st = (hipStream_t)stream;
-    const int64_t total = (int64_t)h->d.n * h->d.cap;
-    const int32_t nblocks = (int32_t)((total + SCAN_BLOCK - 1) / SCAN_BLOCK);
-    hipLaunchKernelGGL(count_kernel, dim3(nblocks), dim3(SCAN_BLOCK), 0, st, h->p, total);
-    hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(1024), 0, st, h->p, nblocks);
-    hipLaunchKernelGGL(scatter_kernel, dim3(nblocks), dim3(SCAN_BLOCK), 0, st, h->p, total);
     const int64_t nb_virtual = (int64_t)(h->cfg.her_ratio * (double)batch);
-    const int64_t threads = batch * GROUP;
-    hipLaunchKernelGGL(sample_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, h->p, h->d, batch,
-                       nb_virtual, h->cfg.seed, draw, h->cfg.reward_type, h->cfg.strategy, (float)h->cfg.distance_threshold, *out);
+    hipLaunchKernelGGL(sample_kernel, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0, (hipStream_t)stream, h->p,
+                       h->d, batch, nb_virtual, h->cfg.seed, draw, h->cfg.reward_type, h->cfg.strategy,
+                       (float)h->cfg.distance_threshold, *out);
     return hipGetLastError() == hipSuccess ? PGX_OK : pgx_set_error(PGX_E_HIP, "pgx_replay_sample: launch failed");
 }
 

@@ -95,6 +95,10 @@ class HerReplayBuffer:
         cfg.strategy = STRATEGIES[goal_selection_strategy]
         cfg.distance_threshold, cfg.her_ratio, cfg.seed = self.distance_threshold, self.her_ratio, int(seed)
         self._cfg = cfg
+        self._fields, self.row_dim = abi.replay_row_fields(self.obs_dim, self.action_dim)
+        self.row_stride = self.lib.pgx_replay_row_stride(C.byref(cfg))
+        if self.lib.pgx_replay_row_dim(C.byref(cfg)) != self.row_dim:
+            raise PgxError("libpgx batch row layout differs from abi.replay_row_fields")
         h = C.c_void_p()
         torch.cuda.set_device(self.device)
         check(self.lib.pgx_replay_create(C.byref(cfg), self.device.index or 0, C.byref(h)), "pgx_replay_create")
@@ -197,35 +201,32 @@ class HerReplayBuffer:
                          next_o, next_ag, next_dg, done, timeout)
 
     # --------------------------------------------------------------- sample
+    def alloc_batch(self, batch_size: int, with_indices: bool = True) -> Dict[str, "torch.Tensor"]:
+        """Batch tensors: ``rows`` [B, row_stride] plus per-field views into it (include/pgx.h layout)."""
+        B = int(batch_size)
+        rows = torch.empty((B, self.row_stride), dtype=torch.float32, device=self.device)
+        out = {"rows": rows}
+        for name, off, w in self._fields:
+            out[name] = rows[:, off] if name in ("reward", "done") else rows[:, off:off + w]
+        for k in ("slot", "env", "goal_slot"):
+            out[k] = torch.empty((B,), dtype=torch.int32, device=self.device) if with_indices else None
+        return out
+
     def sample_raw(self, batch_size: int, draw: Optional[int] = None) -> Dict[str, "torch.Tensor"]:
-        """One relabelled batch as a flat dict of device tensors (plus the drawn slot/env/goal_slot)."""
-        B, od, ad = int(batch_size), self.obs_dim, self.action_dim
-        kw = dict(device=self.device)
-        out = {"obs": torch.empty((B, od), dtype=torch.float32, **kw),
-               "achieved_goal": torch.empty((B, 3), dtype=torch.float32, **kw),
-               "desired_goal": torch.empty((B, 3), dtype=torch.float32, **kw),
-               "action": torch.empty((B, ad), dtype=torch.float32, **kw),
-               "reward": torch.empty((B,), dtype=torch.float32, **kw),
-               "next_obs": torch.empty((B, od), dtype=torch.float32, **kw),
-               "next_achieved_goal": torch.empty((B, 3), dtype=torch.float32, **kw),
-               "next_desired_goal": torch.empty((B, 3), dtype=torch.float32, **kw),
-               "done": torch.empty((B,), dtype=torch.float32, **kw),
-               "slot": torch.empty((B,), dtype=torch.int32, **kw),
-               "env": torch.empty((B,), dtype=torch.int32, **kw),
-               "goal_slot": torch.empty((B,), dtype=torch.int32, **kw)}
+        """One relabelled batch: field views (obs, achieved_goal, ..., done) plus the drawn slot/env/goal_slot."""
+        out = self.alloc_batch(batch_size)
         self.sample_into(out, draw)
         return out
 
     def sample_into(self, out: Dict[str, "torch.Tensor"], draw: Optional[int] = None) -> None:
-        """Fill preallocated batch tensors (no allocation; the benchmark's timed call)."""
-        B = out["reward"].shape[0]
+        """Fill a batch from alloc_batch() (no allocation; the benchmark's timed call)."""
+        rows = out["rows"]
         d = self._draw if draw is None else int(draw)
         self._draw = d + 1
-        names = ["obs", "achieved_goal", "desired_goal", "action", "reward", "next_obs", "next_achieved_goal",
-                 "next_desired_goal", "done", "slot", "env", "goal_slot"]
-        b = abi.PgxReplayBatch(*[(out[k].data_ptr() if out.get(k) is not None else None) for k in names])
-        check(self.lib.pgx_replay_sample(self._h, C.c_int64(B), C.c_uint64(d), C.byref(b), self._stream()),
-              "pgx_replay_sample")
+        ptr = lambda k: out[k].data_ptr() if out.get(k) is not None else None  # noqa: E731
+        b = abi.PgxReplayBatch(rows.data_ptr(), ptr("slot"), ptr("env"), ptr("goal_slot"))
+        check(self.lib.pgx_replay_sample(self._h, C.c_int64(rows.shape[0]), C.c_uint64(d), C.byref(b),
+                                         self._stream()), "pgx_replay_sample")
         if not self._seen_valid:
             # SB3 raises before the first episode has ended; check once (one sync) until it has
             if int(self._arrays()[2].item()) == 0:

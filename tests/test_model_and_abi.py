@@ -91,7 +91,7 @@ def test_struct_layout_matches_c(tmp_path):
               "pgx_step_out": ["terminal_achieved_goal", "terminal_desired_goal"],
               "pgx_replay_config": ["reward_type", "distance_threshold", "her_ratio", "seed"],
               "pgx_transition": ["next_obs", "done", "timeout"],
-              "pgx_replay_batch": ["next_desired_goal", "done", "goal_slot"], "pgx_state_view": ["episode"]}
+              "pgx_replay_batch": ["rows", "env", "goal_slot"], "pgx_state_view": ["episode"]}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{ROOT}/include/pgx.h"', "int main(){"]
     for s, fs in fields.items():
         lines.append(f'printf("{s} %zu\\n", sizeof({s}));')
