@@ -47,6 +47,8 @@ extern "C" {
 #define PGX_MAX_LINKS 16
 #define PGX_MAX_DOFS 9
 #define PGX_MAX_ROWS 27
+#define PGX_MAX_CAPSULES 16
+#define PGX_CONTACT_SLOTS 12       /* 3 contact groups x 4 points (Bullet manifold size) */
 
 #define PGX_OK 0
 #define PGX_E_INVALID -1
@@ -97,7 +99,20 @@ typedef struct pgx_model {
     double inertia[PGX_MAX_LINKS][3];      /* principal inertia (Bullet AABB rule) */
     double lower[PGX_MAX_DOFS];
     double upper[PGX_MAX_DOFS];
+    /* Collision geometry for contacts: the URDF's <collision> cylinders with their
+     * end spheres fused into capsules (segment a-b in the URDF frame of link
+     * cap_link, radius), lone spheres as zero-length capsules. */
+    int32_t n_capsules;
+    int32_t pad1;
+    int32_t cap_link[PGX_MAX_CAPSULES];
+    int32_t cap_flags[PGX_MAX_CAPSULES];   /* PGX_CAP_* */
+    double cap_a[PGX_MAX_CAPSULES][3];
+    double cap_b[PGX_MAX_CAPSULES][3];
+    double cap_radius[PGX_MAX_CAPSULES];
 } pgx_model;
+
+#define PGX_CAP_VS_TABLE 1                 /* capsule end spheres collide with table / plane */
+#define PGX_CAP_VS_OBJECT 2                /* capsule collides with the object (cube) */
 
 /* Physics / solver constants (pybullet defaults as used by the reference). */
 typedef struct pgx_sim_params {
@@ -118,6 +133,10 @@ typedef struct pgx_sim_params {
     int32_t num_iterations;       /* numSolverIterations 50 */
     int32_t ik_max_iters;         /* maxNumIterations 20 */
     int32_t flags;                /* PGX_FLAG_* hypotheses (oracle only) */
+    double contact_distance;      /* contact processing threshold 0.02 (gContactBreakingThreshold) */
+    double contact_erp;           /* ERP of multibody contact rows (m_erp 0.2) */
+    double friction;              /* combined lateral friction 0.5 * 0.5 (btManifoldResult) */
+    double warmstart;             /* m_warmstartingFactor 0.85 (normal impulses) */
 } pgx_sim_params;
 
 /* oracle-only modelling switches (documented in DESIGN.md) */
@@ -145,6 +164,20 @@ typedef struct pgx_config {
     double joint_step;            /* 0.05 (panda.py:74) */
     const pgx_model* model;       /* host pointers, copied at create */
     const pgx_sim_params* params;
+    /* scene (Task._create_scene, push.py:31-47; pybullet.py:759-817) */
+    int32_t contacts;             /* 1: robot/table/object contacts (the reference's scene) */
+    int32_t pad2;
+    double goal_offset[3];        /* goal = offset + uniform(goal_low, goal_high): (0,0,0.02) Push/PnP */
+    double goal_z_zero_prob;      /* PickAndPlace: noise z = 0 with probability 0.3 */
+    double obj_low[3];            /* object = obj_offset + uniform(obj_low, obj_high) */
+    double obj_high[3];
+    double obj_offset[3];
+    double object_half;           /* cube half extent 0.02 */
+    double object_mass;           /* 1.0 */
+    double object_inertia;        /* principal inertia (Bullet compound-AABB rule) */
+    double table_center[3];       /* (-0.3, 0, -0.2) */
+    double table_half[3];         /* (0.55, 0.35, 0.2) */
+    double plane_z;               /* top of the plane box: -0.4 */
 } pgx_config;
 
 typedef struct pgx_env* pgx_handle;
@@ -174,6 +207,7 @@ typedef struct pgx_state_view {
     float* qd;          /* [n_dofs][N] */
     double* goal;       /* [3][N] */
     float* object;      /* [13][N] pos3, quat4 (x,y,z,w), linvel3, angvel3 */
+    float* contacts;    /* [2*PGX_CONTACT_SLOTS][N] warm-start cache: (id, normal impulse) per slot */
     int32_t* elapsed;   /* [N] steps in the current episode */
     uint32_t* episode;  /* [N] episodes finished (RNG counter) */
 } pgx_state_view;

@@ -298,22 +298,209 @@ static void chol_solve(int n, const double* Lm, const double* b, double* x) {
 
 static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
-/* One stepSimulation() of a fixed-base multibody with joint motors and joint
- * limits, no contacts (PyBullet.step pybullet.py:68-71 calls this 20x):
- *  1. unconstrained: qd += dt*qdd(q,qd), clamp |qd| <= maxCoordinateVelocity
- *     (btMultiBodyDynamicsWorld::solveExternalForces -> ABA + applyDeltaVeeMultiDof)
- *  2. constraint rows (btMultiBodyJointMotor / btMultiBodyJointLimitConstraint ::
- *     createConstraintRows) solved by projected Gauss-Seidel
- *     (btMultiBodyConstraintSolver::resolveSingleConstraintRowGeneric), rows in the
- *     world's sorted order, reversed on even iterations, stop when the max squared
- *     row residual <= residual_threshold or after num_iterations
- *  3. qd += M^-1 J^T lambda (constraint pass), q += dt*qd (stepPositionsMultiDof). */
-void pgxo_substep(const pgx_model* m, const pgx_sim_params* p, const double base[3], double* q, double* qd,
-                  const pgxo_motor* motors, pgxo_stats* st) {
+/* ======================================================= world: object + contacts
+ * The scene of Reach/Push/PickAndPlace (Task._create_scene, push.py:31-47;
+ * PyBullet.create_table / create_plane pybullet.py:759-817): a static table box
+ * (top z = 0), a static plane box (top z = -0.4) and, for Push/PickAndPlace, a
+ * free 4 cm cube (a zero-link btMultiBody with a floating base).
+ *
+ * Contacts restated from Bullet 3.2.x (btMultiBodyDynamicsWorld +
+ * btMultiBodyConstraintSolver) -- unpinned: no known answer exists:
+ *  - detection at the start of the step, points with separation < contact_distance
+ *    (0.02, speculative), at most 4 per contact group (btPersistentManifold size),
+ *    the 4 deepest (ties: lower feature id); features with a fixed identity (cube
+ *    vertex, capsule end, capsule sample sphere) carry the normal impulse to the next
+ *    step (warm start x 0.85) like a manifold point does;
+ *  - cube vs table / plane: cube vertices against the top face of the box under them;
+ *    robot capsules (model.capsules) vs table / plane: the end spheres; robot capsules
+ *    vs cube: spheres sampled along the capsule axis at <= r/2 spacing vs the box;
+ *  - rows per point: normal (impulse >= 0; rhs from ERP 0.2 when penetrating, from
+ *    -distance/dt when separated), two friction rows along btPlaneSpace1(normal) with
+ *    |impulse| <= mu * normal impulse (mu = 0.5 * 0.5); solved after the joint rows in
+ *    every sweep (normal rows, then friction rows; a friction row is skipped while its
+ *    normal impulse is 0), same residual exit;
+ *  - body A is the robot (or the cube against the table), B the table (or the cube):
+ *    the normal points from B to A, A's Jacobian is taken at the point on A, B's at
+ *    the point on B.
+ * Cube dynamics: btMultiBody floating base -- gravity, damping m v (k + k|v|),
+ * I w (k + k|w|), the base bias term m (w x v) (computeAccelerations...MultiDof:
+ * "zeroAccSpatFrc[0].addLinear(m_baseMass * omega.cross(vel))"), gyroscopic w x I w
+ * (zero for a cube); orientation by the exponential map (stepPositionsMultiDof). */
+#define OBJ_N 37              /* pos3 quat4 (x,y,z,w) linvel3 angvel3 + 12 x (id, impulse) */
+static void quat_mul(const double* a, const double* b, double* o);
+#define NC_MAX PGX_CONTACT_SLOTS
+
+typedef struct {
+    int grp, id, link;
+    double n[3], pa[3], pb[3], dist;
+} contact_t;
+
+typedef struct {
+    int contacts, has_object;
+    double half, mass, inertia;
+    double tc[3], th[3], plane_z;
+} world_t;
+
+static void quat_to_mat(const double* q, double* R) {
+    double x = q[0], y = q[1], z = q[2], w = q[3];
+    R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - z * w);     R[2] = 2 * (x * z + y * w);
+    R[3] = 2 * (x * y + z * w);     R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - x * w);
+    R[6] = 2 * (x * z - y * w);     R[7] = 2 * (y * z + x * w);     R[8] = 1 - 2 * (x * x + y * y);
+}
+
+/* top of the static box under (x, y): the table top inside its footprint, else the plane */
+static double ground_z(const world_t* W, const double* P) {
+    if (fabs(P[0] - W->tc[0]) <= W->th[0] && fabs(P[1] - W->tc[1]) <= W->th[1]) return W->tc[2] + W->th[2];
+    return W->plane_z;
+}
+
+/* keep the 4 deepest candidates (stable for equal depth: earlier = lower id wins) */
+static void keep4(contact_t* sel, int* n, const contact_t* c) {
+    int pos;
+    if (*n < 4) pos = (*n)++;
+    else if (c->dist < sel[3].dist) pos = 3;
+    else return;
+    while (pos > 0 && c->dist < sel[pos - 1].dist) { sel[pos] = sel[pos - 1]; pos--; }
+    sel[pos] = *c;
+}
+static void sort_by_id(contact_t* s, int n) {
+    for (int i = 1; i < n; i++)
+        for (int j = i; j > 0 && s[j].id < s[j - 1].id; j--) { contact_t t = s[j]; s[j] = s[j - 1]; s[j - 1] = t; }
+}
+
+/* number of sample spheres along a capsule (spacing <= r/2) */
+static int capsule_samples(const double* a, const double* b, double r) {
+    double d[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+    double len = v3_norm(d);
+    if (len <= 0.0) return 1;
+    return (int)ceil(len / (0.5 * r) - 1e-9) + 1;
+}
+
+/* contact detection; returns the number of contacts (grouped, each group sorted by id) */
+static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W, const kin_t* k, const double* obj,
+                  contact_t* out) {
+    const double tau = p->contact_distance;
+    contact_t g0[4], g1[4], g2[4];
+    int n0 = 0, n1 = 0, n2 = 0;
+    double Rc[9];
+    if (W->has_object) {
+        quat_to_mat(obj + 3, Rc);
+        const double h = W->half;
+        for (int v = 0; v < 8; v++) {
+            double lc[3] = {(v & 1) ? h : -h, (v & 2) ? h : -h, (v & 4) ? h : -h}, P[3];
+            m3_v(Rc, lc, P);
+            for (int i = 0; i < 3; i++) P[i] += obj[i];
+            double zt = ground_z(W, P);
+            double d = P[2] - zt;
+            if (d < tau) {
+                contact_t c = {0, v, -1, {0, 0, 1}, {P[0], P[1], P[2]}, {P[0], P[1], zt}, d};
+                keep4(g0, &n0, &c);
+            }
+        }
+    }
+    for (int ci = 0; ci < m->n_capsules; ci++) {
+        int li = m->cap_link[ci];
+        double A[3], B[3];
+        m3_v(k->R[li], m->cap_a[ci], A);
+        m3_v(k->R[li], m->cap_b[ci], B);
+        for (int i = 0; i < 3; i++) { A[i] += k->o[li][i]; B[i] += k->o[li][i]; }
+        const double r = m->cap_radius[ci];
+        int same = m->cap_a[ci][0] == m->cap_b[ci][0] && m->cap_a[ci][1] == m->cap_b[ci][1] &&
+                   m->cap_a[ci][2] == m->cap_b[ci][2];
+        if (W->contacts && (m->cap_flags[ci] & PGX_CAP_VS_TABLE)) {
+            for (int e = 0; e < (same ? 1 : 2); e++) {
+                const double* P = e ? B : A;
+                double zt = ground_z(W, P);
+                double d = P[2] - r - zt;
+                if (d < tau) {
+                    contact_t c = {1, 2 * ci + e, li, {0, 0, 1}, {P[0], P[1], P[2] - r}, {P[0], P[1], zt}, d};
+                    keep4(g1, &n1, &c);
+                }
+            }
+        }
+        if (W->has_object && (m->cap_flags[ci] & PGX_CAP_VS_OBJECT)) {
+            const double h = W->half;
+            int ns = capsule_samples(m->cap_a[ci], m->cap_b[ci], r);
+            for (int s = 0; s < ns; s++) {
+                double t = ns > 1 ? (double)s / (double)(ns - 1) : 0.0, C[3], rel[3], cl[3];
+                for (int i = 0; i < 3; i++) { C[i] = A[i] + t * (B[i] - A[i]); rel[i] = C[i] - obj[i]; }
+                /* box frame: R^T (C - p) */
+                for (int i = 0; i < 3; i++) cl[i] = Rc[i] * rel[0] + Rc[3 + i] * rel[1] + Rc[6 + i] * rel[2];
+                double qb[3], diff[3], nl[3], depth;
+                for (int i = 0; i < 3; i++) { qb[i] = clampd(cl[i], -h, h); diff[i] = cl[i] - qb[i]; }
+                double dist = v3_norm(diff);
+                if (dist > 1e-12) {
+                    for (int i = 0; i < 3; i++) nl[i] = diff[i] / dist;
+                    depth = dist - r;
+                } else { /* sphere centre inside the box: push out through the nearest face */
+                    int ax = 0;
+                    double best = h - fabs(cl[0]);
+                    for (int i = 1; i < 3; i++)
+                        if (h - fabs(cl[i]) < best) { best = h - fabs(cl[i]); ax = i; }
+                    double sg = cl[ax] < 0 ? -1.0 : 1.0;
+                    nl[0] = nl[1] = nl[2] = 0.0;
+                    nl[ax] = sg;
+                    qb[ax] = sg * h;
+                    depth = -best - r;
+                }
+                if (depth < tau) {
+                    contact_t c;
+                    c.grp = 2; c.id = ci * 16 + s; c.link = li; c.dist = depth;
+                    m3_v(Rc, nl, c.n);
+                    m3_v(Rc, qb, c.pb);
+                    for (int i = 0; i < 3; i++) { c.pb[i] += obj[i]; c.pa[i] = C[i] - r * c.n[i]; }
+                    keep4(g2, &n2, &c);
+                }
+            }
+        }
+    }
+    sort_by_id(g0, n0); sort_by_id(g1, n1); sort_by_id(g2, n2);
+    int n = 0;
+    for (int i = 0; i < n0; i++) out[n++] = g0[i];
+    for (int i = 0; i < n1; i++) out[n++] = g1[i];
+    for (int i = 0; i < n2; i++) out[n++] = g2[i];
+    return n;
+}
+
+/* btPlaneSpace1 */
+static void plane_space(const double* n, double* p, double* q) {
+    if (fabs(n[2]) > 0.7071067811865476) {
+        double a = n[1] * n[1] + n[2] * n[2], k = 1.0 / sqrt(a);
+        p[0] = 0; p[1] = -n[2] * k; p[2] = n[1] * k;
+        q[0] = a * k; q[1] = -n[0] * p[2]; q[2] = n[0] * p[1];
+    } else {
+        double a = n[0] * n[0] + n[1] * n[1], k = 1.0 / sqrt(a);
+        p[0] = -n[1] * k; p[1] = n[0] * k; p[2] = 0;
+        q[0] = -n[2] * p[1]; q[1] = n[2] * p[0]; q[2] = a * k;
+    }
+}
+
+typedef struct {
+    double Jr[D], Rr[D];   /* robot Jacobian row and M^-1 J^T */
+    double Jc[6], Rc[6];   /* object (linvel, angvel) row and its response */
+    double jinv, rhs, lam, lo, hi;
+} crow_t;
+
+/* One stepSimulation() (PyBullet.step pybullet.py:68-71 calls this 20x):
+ *  1. contacts at the current poses (world only)
+ *  2. unconstrained: qd += dt*qdd(q,qd), clamp |qd| <= maxCoordinateVelocity
+ *     (btMultiBodyDynamicsWorld::solveExternalForces -> ABA + applyDeltaVeeMultiDof);
+ *     object: v += dt (g - (k + k|v|) v - w x v), w += dt (-(k + k|w|) w)
+ *  3. constraint rows (btMultiBodyJointMotor / btMultiBodyJointLimitConstraint ::
+ *     createConstraintRows, contact rows above) solved by projected Gauss-Seidel
+ *     (btMultiBodyConstraintSolver::resolveSingleConstraintRowGeneric): joint rows in
+ *     the world's sorted order, reversed on even iterations, then normal rows, then
+ *     friction rows; stop when the max squared row residual <= residual_threshold
+ *  4. qd += M^-1 J^T lambda (constraint pass), q += dt*qd (stepPositionsMultiDof);
+ *     object: p += dt v, orientation by the exponential map of w dt. */
+static void substep_impl(const pgx_model* m, const pgx_sim_params* p, const double base[3], double* q, double* qd,
+                         const pgxo_motor* motors, pgxo_stats* st, const world_t* W, double* obj) {
     int nd = m->n_dofs;
     double dt = p->dt;
     kin_t k;
     fk(m, base, q, &k);
+    contact_t con[NC_MAX];
+    int ncon = W ? detect(m, p, W, &k, obj, con) : 0;
     double M[D * D], Lm[D * D], b[D], qdd[D], Minv[D * D];
     mass_matrix(m, &k, M);
     bias(m, p, &k, qd, 1, 1, b);
@@ -330,8 +517,20 @@ void pgxo_substep(const pgx_model* m, const pgx_sim_params* p, const double base
     }
     double vu[D];
     for (int d = 0; d < nd; d++) vu[d] = clampd(qd[d] + dt * qdd[d], -p->max_coord_vel, p->max_coord_vel);
+    double vcu[3] = {0, 0, 0}, wcu[3] = {0, 0, 0};
+    const int has_obj = W && W->has_object;
+    if (has_obj) {
+        const double* v = obj + 7;
+        const double* w = obj + 10;
+        double vn = v3_norm(v), wn = v3_norm(w), wxv[3];
+        v3_cross(w, v, wxv);
+        for (int i = 0; i < 3; i++) {
+            vcu[i] = v[i] + dt * (p->gravity[i] - (p->lin_damping + p->lin_damping * vn) * v[i] - wxv[i]);
+            wcu[i] = w[i] + dt * (-(p->ang_damping + p->ang_damping * wn) * w[i]);
+        }
+    }
 
-    /* --- constraint rows */
+    /* --- joint rows */
     int nr = 0;
     double rhs[PGX_MAX_ROWS], lo[PGX_MAX_ROWS], hi[PGX_MAX_ROWS], inv[PGX_MAX_ROWS], sgn[PGX_MAX_ROWS],
         lam[PGX_MAX_ROWS];
@@ -367,14 +566,70 @@ void pgxo_substep(const pgx_model* m, const pgx_sim_params* p, const double base
         int far = 1;
         for (int d = 0; d < nd; d++) {
             double B = 0;
-            for (int k = 0; k < nd; k++) B += fabs(Minv[d * nd + k]) * (motors[k].max_impulse);
+            for (int kk = 0; kk < nd; kk++) B += fabs(Minv[d * nd + kk]) * (motors[kk].max_impulse);
             B = B * 1.001 + 1e-6;
             double penl = q[d] - m->lower[d], penu = m->upper[d] - q[d];
             far = far && penl > 0 && penu > 0 && (vu[d] - B) > -penl / dt && (vu[d] + B) < penu / dt;
         }
         st->limits_far = far;
+        st->n_contacts = ncon;
     }
-    double dv[D] = {0};
+    double dv[D] = {0}, dvc[6] = {0, 0, 0, 0, 0, 0};
+
+    /* --- contact rows: [3 * k] normal, [3 * k + 1 + j] friction j */
+    crow_t cr[3 * NC_MAX];
+    for (int c = 0; c < ncon; c++) {
+        const contact_t* ct = &con[c];
+        double dirs[3][3];
+        memcpy(dirs[0], ct->n, sizeof dirs[0]);
+        plane_space(ct->n, dirs[1], dirs[2]);
+        double Jv[3 * D], Jw[3 * D];
+        if (ct->grp != 0) jacobian(m, &k, ct->link, ct->pa, Jv, Jw);
+        for (int j = 0; j < 3; j++) {
+            crow_t* R = &cr[3 * c + j];
+            const double* u = dirs[j];
+            memset(R, 0, sizeof *R);
+            if (ct->grp != 0)
+                for (int d = 0; d < nd; d++) R->Jr[d] = Jv[d] * u[0] + Jv[nd + d] * u[1] + Jv[2 * nd + d] * u[2];
+            if (ct->grp == 0 || ct->grp == 2) {
+                const double* pt = ct->grp == 0 ? ct->pa : ct->pb;
+                double rr[3] = {pt[0] - obj[0], pt[1] - obj[1], pt[2] - obj[2]}, rxu[3];
+                v3_cross(rr, u, rxu);
+                double sg = ct->grp == 0 ? 1.0 : -1.0;
+                for (int i = 0; i < 3; i++) { R->Jc[i] = sg * u[i]; R->Jc[3 + i] = sg * rxu[i]; }
+            }
+            for (int a = 0; a < nd; a++) {
+                double s = 0;
+                for (int d = 0; d < nd; d++) s += Minv[a * nd + d] * R->Jr[d];
+                R->Rr[a] = s;
+            }
+            for (int i = 0; i < 3; i++) { R->Rc[i] = R->Jc[i] / W->mass; R->Rc[3 + i] = R->Jc[3 + i] / W->inertia; }
+            double den = 0, rel = 0;
+            for (int d = 0; d < nd; d++) { den += R->Jr[d] * R->Rr[d]; rel += R->Jr[d] * vu[d]; }
+            for (int i = 0; i < 6; i++) den += R->Jc[i] * R->Rc[i];
+            for (int i = 0; i < 3; i++) rel += R->Jc[i] * vcu[i] + R->Jc[3 + i] * wcu[i];
+            R->jinv = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
+            if (j == 0) {
+                double pen = ct->dist, perr = 0.0, verr = -rel;
+                if (pen > 0) verr -= pen / dt;
+                else perr = -pen * p->contact_erp / dt;
+                R->rhs = (perr + verr) * R->jinv;
+                R->lo = 0.0;
+                R->hi = 1e10;
+                /* warm start from the same feature's impulse of the previous step */
+                const double* cache = obj + 13 + 8 * ct->grp;
+                for (int s = 0; s < 4; s++)
+                    if ((int)cache[2 * s] == ct->id) R->lam = p->warmstart * cache[2 * s + 1];
+                if (R->lam != 0.0) {
+                    for (int d = 0; d < nd; d++) dv[d] += R->Rr[d] * R->lam;
+                    for (int i = 0; i < 6; i++) dvc[i] += R->Rc[i] * R->lam;
+                }
+            } else {
+                R->rhs = -rel * R->jinv;
+            }
+        }
+    }
+
     int it_used = 0;
     for (int it = 0; it < p->num_iterations; it++) {
         double resid = 0.0;
@@ -389,6 +644,31 @@ void pgxo_substep(const pgx_model* m, const pgx_sim_params* p, const double base
             for (int c = 0; c < nd; c++) dv[c] += Minv[c * nd + d] * sgn[r] * delta;
             double res = inv[r] != 0.0 ? delta / inv[r] : 0.0;
             if (res * res > resid) resid = res * res;
+        }
+        for (int pass = 0; pass < 2; pass++) {
+            for (int c = 0; c < ncon; c++) {
+                for (int j = (pass ? 1 : 0); j < (pass ? 3 : 1); j++) {
+                    crow_t* R = &cr[3 * c + j];
+                    if (pass) { /* friction: bounds from the normal impulse, skipped while it is 0 */
+                        double ln = cr[3 * c].lam;
+                        if (!(ln > 0.0)) continue;
+                        R->lo = -p->friction * ln;
+                        R->hi = p->friction * ln;
+                    }
+                    double jdv = 0;
+                    for (int d = 0; d < nd; d++) jdv += R->Jr[d] * dv[d];
+                    for (int i = 0; i < 6; i++) jdv += R->Jc[i] * dvc[i];
+                    double delta = R->rhs - jdv * R->jinv;
+                    double sum = R->lam + delta;
+                    if (sum < R->lo) { delta = R->lo - R->lam; R->lam = R->lo; }
+                    else if (sum > R->hi) { delta = R->hi - R->lam; R->lam = R->hi; }
+                    else R->lam = sum;
+                    for (int d = 0; d < nd; d++) dv[d] += R->Rr[d] * delta;
+                    for (int i = 0; i < 6; i++) dvc[i] += R->Rc[i] * delta;
+                    double res = R->jinv != 0.0 ? delta / R->jinv : 0.0;
+                    if (res * res > resid) resid = res * res;
+                }
+            }
         }
         it_used = it + 1;
         if (!(p->flags & PGX_FLAG_NO_RESIDUAL_EXIT) && resid <= p->residual_threshold) break;
@@ -407,6 +687,58 @@ void pgxo_substep(const pgx_model* m, const pgx_sim_params* p, const double base
         qd[d] = vn[d];
         q[d] += dt * vn[d];
     }
+    if (W) { /* contact cache: this step's features and normal impulses, per group */
+        double* cache = obj + 13;
+        for (int s = 0; s < 12; s++) { cache[2 * s] = -1.0; cache[2 * s + 1] = 0.0; }
+        int used[3] = {0, 0, 0};
+        for (int c = 0; c < ncon; c++) {
+            int g = con[c].grp, s = used[g]++;
+            cache[8 * g + 2 * s] = con[c].id;
+            cache[8 * g + 2 * s + 1] = cr[3 * c].lam;
+        }
+    }
+    if (has_obj) {
+        double* pos = obj;
+        double* qt = obj + 3;
+        double* v = obj + 7;
+        double* w = obj + 10;
+        for (int i = 0; i < 3; i++) {
+            v[i] = vcu[i] + dvc[i];
+            w[i] = wcu[i] + dvc[3 + i];
+            pos[i] += dt * v[i];
+        }
+        /* btMultiBody::stepPositionsMultiDof, base: exponential map of w dt */
+        double ang = v3_norm(w), ax[3];
+        if (ang * dt > 0.25 * 1.5707963267948966) ang = 0.25 * 1.5707963267948966 / dt;
+        double f = ang < 0.001 ? (0.5 * dt - dt * dt * dt * 0.020833333333 * ang * ang) : sin(0.5 * ang * dt) / ang;
+        for (int i = 0; i < 3; i++) ax[i] = w[i] * f;
+        double dq[4] = {ax[0], ax[1], ax[2], cos(ang * dt * 0.5)}, nq[4];
+        quat_mul(dq, qt, nq);
+        double nn = sqrt(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+        for (int i = 0; i < 4; i++) qt[i] = nq[i] / nn;
+    }
+}
+
+void pgxo_substep(const pgx_model* m, const pgx_sim_params* p, const double base[3], double* q, double* qd,
+                  const pgxo_motor* motors, pgxo_stats* st) {
+    substep_impl(m, p, base, q, qd, motors, st, NULL, NULL);
+}
+
+static void world_of(const pgx_config* c, world_t* W) {
+    W->contacts = c->contacts;
+    W->has_object = c->task != PGX_TASK_REACH;
+    W->half = c->object_half;
+    W->mass = c->object_mass;
+    W->inertia = c->object_inertia;
+    for (int i = 0; i < 3; i++) { W->tc[i] = c->table_center[i]; W->th[i] = c->table_half[i]; }
+    W->plane_z = c->plane_z;
+}
+
+void pgxo_world_substep(const pgx_config* c, double* q, double* qd, double* obj, const pgxo_motor* motors,
+                        pgxo_stats* st) {
+    world_t W;
+    world_of(c, &W);
+    substep_impl(c->model, c->params, c->base_pos, q, qd, motors, st, &W, obj);
 }
 
 /* ------------------------------------------------------------------- IK */
@@ -603,8 +935,20 @@ static int action_dim(const pgx_config* c) {
     return a + (c->block_gripper ? 0 : 1);
 }
 
-static void env_obs(const pgx_config* c, const double* q, const double* qd, const double* goal, float* obs, float* ag,
-                    float* dg) {
+/* pybullet getEulerFromQuaternion (PyBullet.get_base_rotation, pybullet.py:216-219) */
+static void quat_to_euler(const double* q, double* rpy) {
+    double sqx = q[0] * q[0], sqy = q[1] * q[1], sqz = q[2] * q[2], squ = q[3] * q[3];
+    double sarg = -2.0 * (q[0] * q[2] - q[3] * q[1]);
+    rpy[1] = sarg <= -1.0 ? -0.5 * 3.141592538 : (sarg >= 1.0 ? 0.5 * 3.141592538 : asin(sarg));
+    rpy[0] = atan2(2.0 * (q[1] * q[2] + q[3] * q[0]), squ - sqx - sqy + sqz);
+    rpy[2] = atan2(2.0 * (q[0] * q[1] + q[3] * q[2]), squ + sqx - sqy - sqz);
+}
+
+/* RobotTaskEnv._get_obs (core.py:286-296): robot obs (panda.py:264-288) + task obs
+ * (push.py:49-63 / pick_and_place.py:52-59: object position, euler, velocity, angular
+ * velocity); achieved goal = EE position (Reach) or object position (Push/PnP). */
+static void env_obs(const pgx_config* c, const double* q, const double* qd, const double* goal, const double* obj,
+                    float* obs, float* ag, float* dg) {
     const pgx_model* m = c->model;
     kin_t k;
     fk(m, c->base_pos, q, &k);
@@ -615,20 +959,47 @@ static void env_obs(const pgx_config* c, const double* q, const double* qd, cons
     for (int i = 0; i < 3; i++) o[n++] = (float)k.p[m->ee_link][i];
     for (int i = 0; i < 3; i++) o[n++] = (float)v[i];
     if (!c->block_gripper) o[n++] = 0.0f; /* fixed finger joints in custom_0: width 0 */
+    const int has_obj = c->task != PGX_TASK_REACH;
+    if (has_obj) {
+        double rpy[3];
+        quat_to_euler(obj + 3, rpy);
+        for (int i = 0; i < 3; i++) o[n++] = (float)obj[i];
+        for (int i = 0; i < 3; i++) o[n++] = (float)rpy[i];
+        for (int i = 0; i < 3; i++) o[n++] = (float)obj[7 + i];
+        for (int i = 0; i < 3; i++) o[n++] = (float)obj[10 + i];
+    }
     if (obs) memcpy(obs, o, sizeof(float) * n);
-    if (ag) for (int i = 0; i < 3; i++) ag[i] = (float)k.p[m->ee_link][i];
+    if (ag) for (int i = 0; i < 3; i++) ag[i] = (float)(has_obj ? obj[i] : k.p[m->ee_link][i]);
     if (dg) for (int i = 0; i < 3; i++) dg[i] = (float)goal[i];
 }
 
-static void reset_one(const pgx_config* c, int64_t e, const double* inject_goal, double* q, double* qd, double* goal,
-                      int32_t* elapsed, uint32_t* episode) {
+/* Panda.reset (panda.py:290-298) + Task.reset: Reach reach.py:63-78, Push push.py:69-87,
+ * PickAndPlace pick_and_place.py:65-85 -- draws in the reference's order: goal noise
+ * (3), PickAndPlace's random() < 0.3 (1), object noise (3).  The object is re-posed
+ * with identity orientation; its velocity is kept (resetBasePositionAndOrientation). */
+static void reset_one(const pgx_config* c, int64_t e, const double* inject_goal, const double* inject_obj, double* q,
+                      double* qd, double* goal, double* obj, int32_t* elapsed, uint32_t* episode) {
     int nd = c->model->n_dofs;
     for (int d = 0; d < nd; d++) { q[d] = c->neutral_q[d]; qd[d] = 0.0; }
     uint64_t env = c->env_id_offset + (uint64_t)e;
-    for (int i = 0; i < 3; i++) {
-        if (inject_goal) goal[i] = inject_goal[i];
-        else goal[i] = c->goal_low[i] + (c->goal_high[i] - c->goal_low[i]) * reset_uniform(c, env, *episode, i);
+    double noise[3];
+    for (int i = 0; i < 3; i++)
+        noise[i] = c->goal_low[i] + (c->goal_high[i] - c->goal_low[i]) * reset_uniform(c, env, *episode, i);
+    int kk = 3;
+    if (c->task == PGX_TASK_PICK_AND_PLACE) {
+        if (reset_uniform(c, env, *episode, kk) < c->goal_z_zero_prob) noise[2] = 0.0;
+        kk++;
     }
+    for (int i = 0; i < 3; i++) goal[i] = inject_goal ? inject_goal[i] : c->goal_offset[i] + noise[i];
+    if (c->task != PGX_TASK_REACH && obj) {
+        for (int i = 0; i < 3; i++) {
+            double nz = c->obj_low[i] + (c->obj_high[i] - c->obj_low[i]) * reset_uniform(c, env, *episode, kk + i);
+            obj[i] = inject_obj ? inject_obj[i] : c->obj_offset[i] + nz;
+        }
+        obj[3] = 0.0; obj[4] = 0.0; obj[5] = 0.0; obj[6] = 1.0;
+    }
+    if (obj)
+        for (int s = 0; s < 12; s++) { obj[13 + 2 * s] = -1.0; obj[13 + 2 * s + 1] = 0.0; }
     *elapsed = 0;
     *episode += 1;
 }
@@ -636,14 +1007,13 @@ static void reset_one(const pgx_config* c, int64_t e, const double* inject_goal,
 int pgxo_vec_reset(const pgx_config* c, int64_t n, const uint8_t* mask, const double* inject_goal,
                    const double* inject_obj, double* q, double* qd, double* goal, double* obj, int32_t* elapsed,
                    uint32_t* episode, float* obs, float* ag, float* dg) {
-    (void)inject_obj; (void)obj;
-    if (c->task != PGX_TASK_REACH) return PGX_E_UNSUPPORTED;
     int nd = c->model->n_dofs, od = obs_dim(c);
     for (int64_t e = 0; e < n; e++) {
         if (mask && !mask[e]) continue;
-        reset_one(c, e, inject_goal ? inject_goal + 3 * e : NULL, q + nd * e, qd + nd * e, goal + 3 * e, elapsed + e,
-                  episode + e);
-        env_obs(c, q + nd * e, qd + nd * e, goal + 3 * e, obs ? obs + od * e : NULL, ag ? ag + 3 * e : NULL,
+        double* oe = obj ? obj + OBJ_N * e : NULL;
+        reset_one(c, e, inject_goal ? inject_goal + 3 * e : NULL, inject_obj ? inject_obj + 3 * e : NULL, q + nd * e,
+                  qd + nd * e, goal + 3 * e, oe, elapsed + e, episode + e);
+        env_obs(c, q + nd * e, qd + nd * e, goal + 3 * e, oe, obs ? obs + od * e : NULL, ag ? ag + 3 * e : NULL,
                 dg ? dg + 3 * e : NULL);
     }
     return PGX_OK;
@@ -653,8 +1023,6 @@ int pgxo_vec_reset(const pgx_config* c, int64_t n, const uint8_t* mask, const do
 int pgxo_vec_step(const pgx_config* c, int64_t n, double* q, double* qd, double* goal, double* obj, int32_t* elapsed,
                   uint32_t* episode, const float* action, float* obs, float* ag, float* dg, float* reward,
                   uint8_t* success, uint8_t* terminated, uint8_t* truncated, float* terminal_obs) {
-    (void)obj;
-    if (c->task != PGX_TASK_REACH) return PGX_E_UNSUPPORTED;
     const pgx_model* m = c->model;
     const pgx_sim_params* p = c->params;
     int nd = m->n_dofs, A = action_dim(c), od = obs_dim(c);
@@ -662,6 +1030,7 @@ int pgxo_vec_step(const pgx_config* c, int64_t n, double* q, double* qd, double*
         double* qe = q + nd * e;
         double* qde = qd + nd * e;
         double* ge = goal + 3 * e;
+        double* oe = obj + OBJ_N * e;
         /* Panda.set_action (panda.py:120-172): clip to the action space (float32) */
         float a[8];
         for (int i = 0; i < A; i++) {
@@ -693,10 +1062,10 @@ int pgxo_vec_step(const pgx_config* c, int64_t n, double* q, double* qd, double*
             mot[d].kd = p->motor_kd;
             mot[d].max_impulse = c->joint_forces[d] * p->dt;
         }
-        for (int s = 0; s < p->n_substeps; s++) pgxo_substep(m, p, c->base_pos, qe, qde, mot, NULL);
+        for (int s = 0; s < p->n_substeps; s++) pgxo_world_substep(c, qe, qde, oe, mot, NULL);
 
         float o[32], agv[3], dgv[3];
-        env_obs(c, qe, qde, ge, o, agv, dgv);
+        env_obs(c, qe, qde, ge, oe, o, agv, dgv);
         double d = pgxo_distance_f32_f64(agv, ge);
         uint8_t succ = d < c->distance_threshold;
         float rew = (c->reward == PGX_REWARD_SPARSE) ? -(d > c->distance_threshold ? 1.0f : 0.0f) : -(float)d;
@@ -709,8 +1078,8 @@ int pgxo_vec_step(const pgx_config* c, int64_t n, double* q, double* qd, double*
         if (truncated) truncated[e] = trunc;
         if (trunc || term) {
             if (terminal_obs) memcpy(terminal_obs + od * e, o, sizeof(float) * od);
-            reset_one(c, e, NULL, qe, qde, ge, elapsed + e, episode + e);
-            env_obs(c, qe, qde, ge, o, agv, dgv);
+            reset_one(c, e, NULL, NULL, qe, qde, ge, oe, elapsed + e, episode + e);
+            env_obs(c, qe, qde, ge, oe, o, agv, dgv);
         }
         if (obs) memcpy(obs + od * e, o, sizeof(float) * od);
         if (ag) memcpy(ag + 3 * e, agv, sizeof agv);

@@ -30,7 +30,7 @@ typedef struct pgxo_stats {
     int32_t ik_iterations;
     double ik_residual;
     int32_t limits_far;   /* diagnostics: the kernel's exact limit-row skip test holds */
-    int32_t pad;
+    int32_t n_contacts;   /* contact points of the last substep */
 } pgxo_stats;
 
 void pgxo_fk(const pgx_model* m, const double base[3], const double* q, double* com_pos,
@@ -45,6 +45,11 @@ int pgxo_ik(const pgx_model* m, const pgx_sim_params* p, const double base[3], c
             pgxo_stats* st);
 void pgxo_substep(const pgx_model* m, const pgx_sim_params* p, const double base[3], double* q,
                   double* qd, const pgxo_motor* motors, pgxo_stats* st);
+/* One substep of the task's scene (table, plane, object, contacts): obj[37] = pos3,
+ * quat4 (x,y,z,w), linvel3, angvel3, contact cache 12 x (feature id, normal impulse). */
+void pgxo_world_substep(const pgx_config* cfg, double* q, double* qd, double* obj,
+                        const pgxo_motor* motors, pgxo_stats* st);
+#define PGXO_OBJ_N 37
 
 /* reward / success, reference utils.distance + Reach.is_success / compute_reward */
 double pgxo_distance_f32_f64(const float ag[3], const double g[3]);
@@ -56,7 +61,7 @@ void pgxo_compute_reward_f32(const float* ag, const float* dg, int64_t n, int re
 void pgxo_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 
 /* Batched env step with the kernel's vec-env semantics (TimeLimit + auto-reset).
- * State arrays are AoS per env here: q[N*nd], qd[N*nd], goal[N*3], obj[N*13]. */
+ * State arrays are AoS per env here: q[N*nd], qd[N*nd], goal[N*3], obj[N*PGXO_OBJ_N]. */
 int pgxo_vec_step(const pgx_config* cfg, int64_t n, double* q, double* qd, double* goal,
                   double* obj, int32_t* elapsed, uint32_t* episode, const float* action,
                   float* obs, float* ag, float* dg, float* reward, uint8_t* success,

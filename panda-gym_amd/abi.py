@@ -16,6 +16,9 @@ import numpy as np
 from .model import Model, MAX_LINKS, MAX_DOFS, load_model
 
 MAX_ROWS = 27
+MAX_CAPSULES = 16
+CONTACT_SLOTS = 12
+CAP_VS_TABLE, CAP_VS_OBJECT = 1, 2
 
 TASK_REACH, TASK_PUSH, TASK_PICK_AND_PLACE = 0, 1, 2
 CONTROL_EE, CONTROL_JOINTS = 0, 1
@@ -41,6 +44,10 @@ class PgxModel(C.Structure):
         ("axis", (C.c_double * 3) * MAX_LINKS), ("com", (C.c_double * 3) * MAX_LINKS),
         ("mass", C.c_double * MAX_LINKS), ("inertia", (C.c_double * 3) * MAX_LINKS),
         ("lower", C.c_double * MAX_DOFS), ("upper", C.c_double * MAX_DOFS),
+        ("n_capsules", C.c_int32), ("pad1", C.c_int32),
+        ("cap_link", C.c_int32 * MAX_CAPSULES), ("cap_flags", C.c_int32 * MAX_CAPSULES),
+        ("cap_a", (C.c_double * 3) * MAX_CAPSULES), ("cap_b", (C.c_double * 3) * MAX_CAPSULES),
+        ("cap_radius", C.c_double * MAX_CAPSULES),
     ]
 
 
@@ -52,6 +59,8 @@ class PgxSimParams(C.Structure):
         ("motor_kd", C.c_double), ("ik_residual", C.c_double), ("ik_damping", C.c_double),
         ("ik_max_angle", C.c_double), ("n_substeps", C.c_int32), ("num_iterations", C.c_int32),
         ("ik_max_iters", C.c_int32), ("flags", C.c_int32),
+        ("contact_distance", C.c_double), ("contact_erp", C.c_double), ("friction", C.c_double),
+        ("warmstart", C.c_double),
     ]
 
 
@@ -65,6 +74,11 @@ class PgxConfig(C.Structure):
         ("joint_forces", C.c_double * MAX_DOFS), ("neutral_q", C.c_double * MAX_DOFS),
         ("ee_step", C.c_double), ("joint_step", C.c_double),
         ("model", C.POINTER(PgxModel)), ("params", C.POINTER(PgxSimParams)),
+        ("contacts", C.c_int32), ("pad2", C.c_int32),
+        ("goal_offset", C.c_double * 3), ("goal_z_zero_prob", C.c_double),
+        ("obj_low", C.c_double * 3), ("obj_high", C.c_double * 3), ("obj_offset", C.c_double * 3),
+        ("object_half", C.c_double), ("object_mass", C.c_double), ("object_inertia", C.c_double),
+        ("table_center", C.c_double * 3), ("table_half", C.c_double * 3), ("plane_z", C.c_double),
     ]
 
 
@@ -80,7 +94,7 @@ class PgxStepOut(C.Structure):
 class PgxStateView(C.Structure):
     _fields_ = [
         ("q", C.c_void_p), ("qd", C.c_void_p), ("goal", C.c_void_p), ("object", C.c_void_p),
-        ("elapsed", C.c_void_p), ("episode", C.c_void_p),
+        ("contacts", C.c_void_p), ("elapsed", C.c_void_p), ("episode", C.c_void_p),
     ]
 
 
@@ -140,6 +154,13 @@ def make_model(model: Model, ee_link: int = 11) -> PgxModel:
         m.upper[d] = model.upper[d]
     for r, (k, d) in enumerate(zip(kinds, dofs)):
         m.row_kind[r], m.row_dof[r] = int(k), int(d)
+    caps = model.capsules()
+    assert len(caps) <= MAX_CAPSULES
+    m.n_capsules = len(caps)
+    for i, c in enumerate(caps):
+        m.cap_link[i], m.cap_flags[i], m.cap_radius[i] = c["link"], c["flags"], c["r"]
+        for k in range(3):
+            m.cap_a[i][k], m.cap_b[i][k] = c["a"][k], c["b"][k]
     return m
 
 
@@ -163,6 +184,10 @@ def default_sim_params(n_substeps: int = 20, flags: int = 0) -> PgxSimParams:
     p.num_iterations = 50                    # pybullet numSolverIterations
     p.ik_max_iters = 20                      # calculateInverseKinematics maxNumIterations
     p.flags = flags
+    p.contact_distance = 0.02                # gContactBreakingThreshold (contact processing threshold)
+    p.contact_erp = 0.2                      # btMultiBodyConstraintSolver: contacts use m_erp
+    p.friction = 0.5 * 0.5                   # default lateral friction 0.5 per body, product combine
+    p.warmstart = 0.85                       # btContactSolverInfo m_warmstartingFactor
     return p
 
 
@@ -183,6 +208,10 @@ class EnvSpec:
     distance_threshold: float = 0.05                   # reach.py:15
     goal_range: float = 0.3                            # reach.py:16
 
+    def obj_bounds(self):
+        """push.py:26-27 / pick_and_place.py:28-29: noise ranges of the object position."""
+        return [-0.15, -0.15, 0.0], [0.15, 0.15, 0.0]
+
     def goal_bounds(self):
         if self.task == TASK_REACH:   # reach.py:24-25
             g = self.goal_range
@@ -201,7 +230,7 @@ class EnvSpec:
 
 
 def make_config(spec: EnvSpec, n_envs: int, model: PgxModel, params: PgxSimParams, seed: int = 0,
-                env_id_offset: int = 0) -> PgxConfig:
+                env_id_offset: int = 0, contacts: bool = True) -> PgxConfig:
     c = PgxConfig()
     c.task, c.control, c.reward = spec.task, spec.control, spec.reward
     c.n_envs = n_envs
@@ -222,7 +251,36 @@ def make_config(spec: EnvSpec, n_envs: int, model: PgxModel, params: PgxSimParam
     c.joint_step = 0.05     # panda.py:74 max_change_position
     c.model = C.pointer(model)
     c.params = C.pointer(params)
+    c.contacts = 1 if contacts else 0
+    half = OBJECT_SIZE / 2
+    if spec.task != TASK_REACH:
+        c.goal_offset[2] = half                   # push.py:71 / pick_and_place.py:68 (cube centre)
+        c.obj_offset[2] = half
+        olo, ohi = spec.obj_bounds()
+        for i in range(3):
+            c.obj_low[i], c.obj_high[i] = olo[i], ohi[i]
+    c.goal_z_zero_prob = 0.3 if spec.task == TASK_PICK_AND_PLACE else 0.0   # pick_and_place.py:73
+    c.object_half = half
+    c.object_mass = 1.0                           # push.py:37
+    c.object_inertia = box_inertia(OBJECT_MASS, half)
+    for i in range(3):                            # create_table(1.1, 0.7, 0.4, x_offset=-0.3)
+        c.table_center[i] = (-0.3, 0.0, -0.2)[i]
+        c.table_half[i] = (0.55, 0.35, 0.2)[i]
+    c.plane_z = -0.4                              # create_plane(z_offset=-0.4): box top
     return c
+
+
+OBJECT_SIZE = 0.04     # push.py:23
+OBJECT_MASS = 1.0
+
+
+def box_inertia(mass: float, half: float) -> float:
+    """Principal inertia of the cube as pybullet computes it for createMultiBody: the
+    URDF importer's compound (margin 0.001) around the box child, inertia from the
+    compound AABB (btCompoundShape::calculateLocalInertia): half extents h + 0.001."""
+    from .model import URDF_MARGIN
+    e = 2.0 * (half + URDF_MARGIN)
+    return mass / 12.0 * (e * e + e * e)
 
 
 def ptr(a: Optional[np.ndarray]):

@@ -76,6 +76,12 @@ def register_envs(max_ep_steps: int = 50) -> None:
             cs = "Joints" if control == abi.CONTROL_JOINTS else ""
             _REGISTRY[f"PandaReach{cs}{rs}-v3"] = abi.EnvSpec(task=abi.TASK_REACH, control=control, reward=reward,
                                                              max_episode_steps=max_ep_steps, block_gripper=True)
+            # panda_tasks.py:50-58 (Push: block_gripper=True), :37-48 (PickAndPlace: block_gripper=False)
+            _REGISTRY[f"PandaPush{cs}{rs}-v3"] = abi.EnvSpec(task=abi.TASK_PUSH, control=control, reward=reward,
+                                                            max_episode_steps=max_ep_steps, block_gripper=True)
+            _REGISTRY[f"PandaPickAndPlace{cs}{rs}-v3"] = abi.EnvSpec(
+                task=abi.TASK_PICK_AND_PLACE, control=control, reward=reward, max_episode_steps=max_ep_steps,
+                block_gripper=False)
 
 
 def registered_ids() -> List[str]:
@@ -92,11 +98,31 @@ def spec(env_id: str) -> abi.EnvSpec:
 
 def seeded_goal(env_spec: abi.EnvSpec, seed: Optional[int]) -> Optional[np.ndarray]:
     """Goal draw of RobotTaskEnv.reset(seed) (core.py:302 reseeds PCG64 every reset; reach.py:75-78)."""
+    r = seeded_reset(env_spec, seed)
+    return None if r is None else r[0]
+
+
+def seeded_reset(env_spec: abi.EnvSpec, seed: Optional[int]) -> Optional[Tuple[np.ndarray, Optional[np.ndarray]]]:
+    """(goal, object position) of RobotTaskEnv.reset(seed): a fresh PCG64(SeedSequence(seed))
+    (core.py:302), then the task's draws in its own order -- Reach reach.py:75-78; Push
+    push.py:158-176 (goal noise, object noise, both around the cube centre height);
+    PickAndPlace pick_and_place.py:258-272 (goal noise, random() < 0.3 zeroes its z, object)."""
     if seed is None:
         return None
     rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed)))
     lo, hi = env_spec.goal_bounds()
-    return rng.uniform(np.array(lo), np.array(hi))
+    if env_spec.task == abi.TASK_REACH:
+        return rng.uniform(np.array(lo), np.array(hi)), None
+    half = abi.OBJECT_SIZE / 2
+    goal = np.array([0.0, 0.0, half])
+    noise = rng.uniform(np.array(lo), np.array(hi))
+    if env_spec.task == abi.TASK_PICK_AND_PLACE and rng.random() < 0.3:
+        noise[2] = 0.0
+    goal += noise
+    obj = np.array([0.0, 0.0, half])
+    olo, ohi = env_spec.obj_bounds()
+    obj += rng.uniform(np.array(olo), np.array(ohi))
+    return goal, obj
 
 
 # ------------------------------------------------------------ vec env

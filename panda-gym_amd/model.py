@@ -118,6 +118,49 @@ class Model:
                 dofs.append(dof)
         return np.array(kinds, dtype=np.int32), np.array(dofs, dtype=np.int32)
 
+    def capsules(self, table_from_link: int = 1, object_from_link: int = 4) -> List[dict]:
+        """Contact geometry: every <collision> cylinder with the spheres capping its ends
+        fused into a capsule, spheres not contained in a capsule as zero-length capsules.
+
+        In franka_panda_custom_0 every cylinder is capped by two spheres of its own
+        radius (panda.urdf:21-438), so the union Bullet collides (one compound child per
+        primitive) is exactly a set of capsules; the only exception is panda_link7's
+        r=0.025 sphere on the r=0.04 cylinder's top face, which the capsule's end cap
+        contains.  Endpoints are in the URDF frame of the owning link.  Flags: links
+        below ``table_from_link`` (panda_link1, whose sphere rests on the joint-1 axis
+        inside the table top) do not touch the table -- like reach_ao.py:898, and
+        dynamically inert in Bullet because the contact point lies on the joint axis;
+        links from ``object_from_link`` (panda_link5) on can touch the object."""
+        caps, spheres = [], []
+        for p in self.collision:
+            li = p["link"]
+            rot = np.array(p["rot"]).reshape(3, 3)
+            center = np.array(p["pos"]) + np.array(self.com[li])   # inertial frame -> URDF frame
+            if p["kind"] == "cylinder":
+                r, h = p["size"][0], p["size"][1]
+                ax = rot @ np.array([0.0, 0.0, 1.0])
+                caps.append(dict(link=li, a=(center - ax * h / 2), b=(center + ax * h / 2), r=r))
+            elif p["kind"] == "sphere":
+                spheres.append(dict(link=li, c=center, r=p["size"][0]))
+        for s in spheres:
+            inside = False
+            for c in caps:
+                if c["link"] != s["link"]:
+                    continue
+                ab = c["b"] - c["a"]
+                t = np.clip(np.dot(s["c"] - c["a"], ab) / max(np.dot(ab, ab), 1e-300), 0.0, 1.0)
+                if np.linalg.norm(s["c"] - (c["a"] + t * ab)) + s["r"] <= c["r"] + 1e-9:
+                    inside = True
+                    break
+            if not inside:
+                caps.append(dict(link=s["link"], a=s["c"].copy(), b=s["c"].copy(), r=s["r"]))
+        out = []
+        for c in sorted(caps, key=lambda c: c["link"]):
+            flags = (1 if c["link"] >= table_from_link else 0) | (2 if c["link"] >= object_from_link else 0)
+            out.append(dict(link=int(c["link"]), a=[float(x) for x in c["a"]], b=[float(x) for x in c["b"]],
+                            r=float(c["r"]), flags=flags))
+        return out
+
 
 def bullet_quicksort_equal_keys(items: List) -> List:
     """btAlignedObjectArray::quickSortInternal on a list whose keys all compare equal.

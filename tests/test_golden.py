@@ -53,3 +53,18 @@ def test_host_seeded_goal_matches_golden():
     sp = abi.EnvSpec()
     for s, gl in zip(gold["seeds"], gold["reach_goal"]):
         assert np.array_equal(seeded_goal(sp, int(s)), gl)
+
+
+def test_host_seeded_push_and_pnp_resets_match_golden():
+    """Push / PickAndPlace reset draws (goal then object, PnP's z coin in between) against
+    the fixture generated from the reference's task code order (make_golden.py)."""
+    from panda_gym_amd.envs import seeded_reset
+
+    gold = np.load(os.path.join(GOLD, "reset_golden.npz"))
+    push = abi.EnvSpec(task=abi.TASK_PUSH)
+    pnp = abi.EnvSpec(task=abi.TASK_PICK_AND_PLACE, block_gripper=False)
+    for s, gp, gq in zip(gold["seeds"], gold["push_goal_obj"], gold["pnp_goal_obj"]):
+        g, o = seeded_reset(push, int(s))
+        assert np.array_equal(np.concatenate([g, o]), gp)
+        g, o = seeded_reset(pnp, int(s))
+        assert np.array_equal(np.concatenate([g, o]), gq)
