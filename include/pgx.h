@@ -48,7 +48,7 @@ extern "C" {
 #define PGX_MAX_DOFS 9
 #define PGX_MAX_ROWS 27
 #define PGX_MAX_CAPSULES 16
-#define PGX_CONTACT_SLOTS 12       /* 3 contact groups x 4 points (Bullet manifold size) */
+#define PGX_CONTACT_SLOTS 8        /* 2 contact groups (object-scene, robot) x 4 points */
 
 #define PGX_OK 0
 #define PGX_E_INVALID -1

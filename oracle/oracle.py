@@ -47,7 +47,7 @@ class PgxoStats(C.Structure):
                 ("limits_far", C.c_int32), ("n_contacts", C.c_int32)]
 
 
-OBJ_N = 37   # pos3 quat4 linvel3 angvel3 + 12 x (contact feature id, normal impulse)
+OBJ_N = 29   # pos3 quat4 linvel3 angvel3 + 8 x (contact feature id, normal impulse)
 
 
 def _p(a):

@@ -307,8 +307,10 @@ static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x >
  * Contacts restated from Bullet 3.2.x (btMultiBodyDynamicsWorld +
  * btMultiBodyConstraintSolver) -- unpinned: no known answer exists:
  *  - detection at the start of the step, points with separation < contact_distance
- *    (0.02, speculative), at most 4 per contact group (btPersistentManifold size),
- *    the 4 deepest (ties: lower feature id); features with a fixed identity (cube
+ *    (0.02, speculative); two contact groups -- object vs table/plane, robot vs
+ *    table/plane/object -- each keeping its 4 deepest points (ties: lower feature id;
+ *    4 = btPersistentManifold size, applied per group rather than per link pair to
+ *    bound the kernel's per-env row storage); features with a fixed identity (cube
  *    vertex, capsule end, capsule sample sphere) carry the normal impulse to the next
  *    step (warm start x 0.85) like a manifold point does;
  *  - cube vs table / plane: cube vertices against the top face of the box under them;
@@ -326,7 +328,7 @@ static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x >
  * I w (k + k|w|), the base bias term m (w x v) (computeAccelerations...MultiDof:
  * "zeroAccSpatFrc[0].addLinear(m_baseMass * omega.cross(vel))"), gyroscopic w x I w
  * (zero for a cube); orientation by the exponential map (stepPositionsMultiDof). */
-#define OBJ_N 37              /* pos3 quat4 (x,y,z,w) linvel3 angvel3 + 12 x (id, impulse) */
+#define OBJ_N 29              /* pos3 quat4 (x,y,z,w) linvel3 angvel3 + 8 x (id, impulse) */
 static void quat_mul(const double* a, const double* b, double* o);
 #define NC_MAX PGX_CONTACT_SLOTS
 
@@ -380,8 +382,8 @@ static int capsule_samples(const double* a, const double* b, double r) {
 static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W, const kin_t* k, const double* obj,
                   contact_t* out) {
     const double tau = p->contact_distance;
-    contact_t g0[4], g1[4], g2[4];
-    int n0 = 0, n1 = 0, n2 = 0;
+    contact_t g0[4], g1[4];
+    int n0 = 0, n1 = 0;
     double Rc[9];
     if (W->has_object) {
         quat_to_mat(obj + 3, Rc);
@@ -445,20 +447,19 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
                 }
                 if (depth < tau) {
                     contact_t c;
-                    c.grp = 2; c.id = ci * 16 + s; c.link = li; c.dist = depth;
+                    c.grp = 2; c.id = 32 + ci * 16 + s; c.link = li; c.dist = depth;
                     m3_v(Rc, nl, c.n);
                     m3_v(Rc, qb, c.pb);
                     for (int i = 0; i < 3; i++) { c.pb[i] += obj[i]; c.pa[i] = C[i] - r * c.n[i]; }
-                    keep4(g2, &n2, &c);
+                    keep4(g1, &n1, &c);
                 }
             }
         }
     }
-    sort_by_id(g0, n0); sort_by_id(g1, n1); sort_by_id(g2, n2);
+    sort_by_id(g0, n0); sort_by_id(g1, n1);
     int n = 0;
     for (int i = 0; i < n0; i++) out[n++] = g0[i];
     for (int i = 0; i < n1; i++) out[n++] = g1[i];
-    for (int i = 0; i < n2; i++) out[n++] = g2[i];
     return n;
 }
 
@@ -617,7 +618,7 @@ static void substep_impl(const pgx_model* m, const pgx_sim_params* p, const doub
                 R->lo = 0.0;
                 R->hi = 1e10;
                 /* warm start from the same feature's impulse of the previous step */
-                const double* cache = obj + 13 + 8 * ct->grp;
+                const double* cache = obj + 13 + 8 * (ct->grp != 0);
                 for (int s = 0; s < 4; s++)
                     if ((int)cache[2 * s] == ct->id) R->lam = p->warmstart * cache[2 * s + 1];
                 if (R->lam != 0.0) {
@@ -689,10 +690,10 @@ static void substep_impl(const pgx_model* m, const pgx_sim_params* p, const doub
     }
     if (W) { /* contact cache: this step's features and normal impulses, per group */
         double* cache = obj + 13;
-        for (int s = 0; s < 12; s++) { cache[2 * s] = -1.0; cache[2 * s + 1] = 0.0; }
-        int used[3] = {0, 0, 0};
+        for (int s = 0; s < 8; s++) { cache[2 * s] = -1.0; cache[2 * s + 1] = 0.0; }
+        int used[2] = {0, 0};
         for (int c = 0; c < ncon; c++) {
-            int g = con[c].grp, s = used[g]++;
+            int g = con[c].grp != 0, s = used[g]++;
             cache[8 * g + 2 * s] = con[c].id;
             cache[8 * g + 2 * s + 1] = cr[3 * c].lam;
         }
@@ -999,7 +1000,7 @@ static void reset_one(const pgx_config* c, int64_t e, const double* inject_goal,
         obj[3] = 0.0; obj[4] = 0.0; obj[5] = 0.0; obj[6] = 1.0;
     }
     if (obj)
-        for (int s = 0; s < 12; s++) { obj[13 + 2 * s] = -1.0; obj[13 + 2 * s + 1] = 0.0; }
+        for (int s = 0; s < 8; s++) { obj[13 + 2 * s] = -1.0; obj[13 + 2 * s + 1] = 0.0; }
     *elapsed = 0;
     *episode += 1;
 }

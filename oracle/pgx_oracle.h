@@ -45,11 +45,11 @@ int pgxo_ik(const pgx_model* m, const pgx_sim_params* p, const double base[3], c
             pgxo_stats* st);
 void pgxo_substep(const pgx_model* m, const pgx_sim_params* p, const double base[3], double* q,
                   double* qd, const pgxo_motor* motors, pgxo_stats* st);
-/* One substep of the task's scene (table, plane, object, contacts): obj[37] = pos3,
- * quat4 (x,y,z,w), linvel3, angvel3, contact cache 12 x (feature id, normal impulse). */
+/* One substep of the task's scene (table, plane, object, contacts): obj[29] = pos3,
+ * quat4 (x,y,z,w), linvel3, angvel3, contact cache 8 x (feature id, normal impulse). */
 void pgxo_world_substep(const pgx_config* cfg, double* q, double* qd, double* obj,
                         const pgxo_motor* motors, pgxo_stats* st);
-#define PGXO_OBJ_N 37
+#define PGXO_OBJ_N 29
 
 /* reward / success, reference utils.distance + Reach.is_success / compute_reward */
 double pgxo_distance_f32_f64(const float ag[3], const double g[3]);

@@ -17,7 +17,7 @@ from .model import Model, MAX_LINKS, MAX_DOFS, load_model
 
 MAX_ROWS = 27
 MAX_CAPSULES = 16
-CONTACT_SLOTS = 12
+CONTACT_SLOTS = 8
 CAP_VS_TABLE, CAP_VS_OBJECT = 1, 2
 
 TASK_REACH, TASK_PUSH, TASK_PICK_AND_PLACE = 0, 1, 2

@@ -114,6 +114,32 @@ static int check_compiled_tables(const PgxDevModel& dm) {
     return rc;
 }
 
+/* The contact capsules folded onto the arm joints (link-7 group in link 7's frame)
+ * must equal the compiled kCap* tables. */
+static int check_capsules(const pgx_model* m, const double (*R)[9], const double (*O)[3]) {
+    if (m->n_capsules != PGX_NCAP)
+        return fail(PGX_E_UNSUPPORTED, "model has %d contact capsules, kernel %d", m->n_capsules, PGX_NCAP);
+    const int last = PGX_NJ - 1;
+    for (int c = 0; c < PGX_NCAP; c++) {
+        int li = m->cap_link[c];
+        int j = li < last ? li : last;
+        double a[3], b[3];
+        if (li > last) {
+            m3v(R[li], m->cap_a[c], a);
+            m3v(R[li], m->cap_b[c], b);
+            for (int k = 0; k < 3; k++) { a[k] += O[li][k]; b[k] += O[li][k]; }
+        } else {
+            for (int k = 0; k < 3; k++) { a[k] = m->cap_a[c][k]; b[k] = m->cap_b[c][k]; }
+        }
+        bool ok = j == kCapJ[c] && m->cap_flags[c] == kCapFlags[c] &&
+                  std::fabs(m->cap_radius[c] - kCapR[c]) <= 1e-6;
+        for (int k = 0; k < 3; k++)
+            ok = ok && std::fabs(a[k] - kCapA[c][k]) <= 1e-6 && std::fabs(b[k] - kCapB[c][k]) <= 1e-6;
+        if (!ok) return fail(PGX_E_UNSUPPORTED, "contact capsule %d differs from the compiled robot", c);
+    }
+    return PGX_OK;
+}
+
 /* Fold the model into the kernel's constant tables. */
 static int build_dev_model(const pgx_config* cfg, PgxDevModel* dm) {
     const pgx_model* m = cfg->model;
@@ -229,16 +255,26 @@ static int build_dev_model(const pgx_config* cfg, PgxDevModel* dm) {
     dm->ik_max_iters = p->ik_max_iters;
     dm->ee_step = (float)cfg->ee_step;
     dm->joint_step = (float)cfg->joint_step;
+    dm->contact_dist = (float)p->contact_distance;
+    dm->contact_erp = (float)p->contact_erp;
+    dm->friction = (float)p->friction;
+    dm->warmstart = (float)p->warmstart;
     if (p->flags != 0) return fail(PGX_E_UNSUPPORTED, "modelling flags are oracle-only");
-    return check_compiled_tables(*dm);
+    int rc = check_compiled_tables(*dm);
+    if (!rc) rc = check_capsules(m, R, O);
+    return rc;
 }
 
 int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     if (!cfg || !out || !cfg->model || !cfg->params) return fail(PGX_E_INVALID, "null argument");
     *out = nullptr;
     if (cfg->n_envs <= 0) return fail(PGX_E_INVALID, "n_envs must be > 0 (got %d)", cfg->n_envs);
-    if (cfg->task != PGX_TASK_REACH)
-        return fail(PGX_E_UNSUPPORTED, "task %d: only PGX_TASK_REACH is implemented by this build", cfg->task);
+    if (cfg->task != PGX_TASK_REACH && cfg->task != PGX_TASK_PUSH && cfg->task != PGX_TASK_PICK_AND_PLACE)
+        return fail(PGX_E_UNSUPPORTED, "task %d is not implemented by this build", cfg->task);
+    if (cfg->task != PGX_TASK_REACH && !cfg->contacts)
+        return fail(PGX_E_INVALID, "object tasks need contacts");
+    if (cfg->task != PGX_TASK_REACH && (cfg->object_half <= 0 || cfg->object_mass <= 0 || cfg->object_inertia <= 0))
+        return fail(PGX_E_INVALID, "object size, mass and inertia must be > 0");
     if (cfg->control != PGX_CONTROL_EE && cfg->control != PGX_CONTROL_JOINTS)
         return fail(PGX_E_INVALID, "control %d", cfg->control);
     if (cfg->reward != PGX_REWARD_SPARSE && cfg->reward != PGX_REWARD_DENSE)
@@ -260,14 +296,33 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     e.env_id_offset = cfg->env_id_offset;
     e.distance_threshold = cfg->distance_threshold;
     for (int c = 0; c < 3; c++) { e.goal_low[c] = cfg->goal_low[c]; e.goal_high[c] = cfg->goal_high[c]; }
+    for (int c = 0; c < 3; c++) {
+        e.goal_offset[c] = cfg->goal_offset[c];
+        e.obj_low[c] = cfg->obj_low[c];
+        e.obj_high[c] = cfg->obj_high[c];
+        e.obj_offset[c] = cfg->obj_offset[c];
+    }
+    e.goal_z_zero_prob = cfg->goal_z_zero_prob;
+    e.contacts = cfg->contacts ? 1 : 0;
+    e.has_object = cfg->task != PGX_TASK_REACH;
+    e.obj_half = (float)cfg->object_half;
+    e.obj_inv_mass = e.has_object ? (float)(1.0 / cfg->object_mass) : 0.0f;
+    e.obj_inv_inertia = e.has_object ? (float)(1.0 / cfg->object_inertia) : 0.0f;
+    e.table_cx = (float)cfg->table_center[0];
+    e.table_cy = (float)cfg->table_center[1];
+    e.table_hx = (float)cfg->table_half[0];
+    e.table_hy = (float)cfg->table_half[1];
+    e.table_top = (float)(cfg->table_center[2] + cfg->table_half[2]);
+    e.plane_z = (float)cfg->plane_z;
 
     rc = hip_check(hipSetDevice(device), "hipSetDevice");
     if (rc) { delete h; return rc; }
     const size_t N = (size_t)cfg->n_envs;
     auto align = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t off_goal = align(sizeof(PgxDevModel)), off_q = align(off_goal + 3 * N * 8), off_qd = align(off_q + PGX_NJ * N * 4),
-           off_obj = align(off_qd + PGX_NJ * N * 4), off_el = align(off_obj + 13 * N * 4),
-           off_ep = align(off_el + N * 4), total = align(off_ep + N * 4);
+           off_obj = align(off_qd + PGX_NJ * N * 4), off_ct = align(off_obj + 13 * N * 4),
+           off_el = align(off_ct + 2 * PGX_CONTACT_SLOTS * N * 4), off_ep = align(off_el + N * 4),
+           total = align(off_ep + N * 4);
     rc = hip_check(hipMalloc(&h->blob, total), "hipMalloc(state)");
     if (rc) { delete h; return rc; }
     h->blob_bytes = total;
@@ -276,6 +331,7 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     h->ds.q = (float*)(b + off_q);
     h->ds.qd = (float*)(b + off_qd);
     h->ds.object = (float*)(b + off_obj);
+    h->ds.contacts = (float*)(b + off_ct);
     h->ds.elapsed = (int32_t*)(b + off_el);
     h->ds.episode = (uint32_t*)(b + off_ep);
     h->dm_dev = (PgxDevModel*)b;
@@ -284,7 +340,8 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     if (!rc) {
         PgxDevOut none;
         std::memset(&none, 0, sizeof none);
-        rc = hip_check((hipError_t)pgx_launch_reset(h->dm_dev, h->de, h->ds, nullptr, nullptr, none, nullptr), "reset launch");
+        rc = hip_check((hipError_t)pgx_launch_reset(h->dm_dev, h->de, h->ds, nullptr, nullptr, nullptr, none, nullptr),
+                       "reset launch");
         /* episodes count resets; the construction reset (core.py:270) is not counted */
         if (!rc) rc = hip_check(hipMemset(h->ds.episode, 0, N * 4), "hipMemset(episode)");
         if (!rc) rc = hip_check(hipDeviceSynchronize(), "create sync");
@@ -307,6 +364,7 @@ int pgx_get_state(pgx_handle h, pgx_state_view* out) {
     out->qd = h->ds.qd;
     out->goal = h->ds.goal;
     out->object = h->ds.object;
+    out->contacts = h->ds.contacts;
     out->elapsed = h->ds.elapsed;
     out->episode = h->ds.episode;
     return PGX_OK;
@@ -332,8 +390,9 @@ static PgxDevOut to_dev_out(const pgx_step_out* o) {
 int pgx_reset(pgx_handle h, const uint8_t* env_mask, const double* inject_goal, const double* inject_object,
               pgx_step_out* out, void* stream) {
     if (!h) return fail(PGX_E_INVALID, "null handle");
-    if (inject_object) return fail(PGX_E_UNSUPPORTED, "object injection needs an object task");
-    return hip_check((hipError_t)pgx_launch_reset(h->dm_dev, h->de, h->ds, env_mask, inject_goal, to_dev_out(out), stream),
+    if (inject_object && !h->de.has_object) return fail(PGX_E_INVALID, "object injection needs an object task");
+    return hip_check((hipError_t)pgx_launch_reset(h->dm_dev, h->de, h->ds, env_mask, inject_goal, inject_object,
+                                                  to_dev_out(out), stream),
                      "reset launch");
 }
 

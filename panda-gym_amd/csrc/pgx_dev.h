@@ -38,6 +38,8 @@ struct PgxDevModel {
     float base[3];
     float ee_step, joint_step;
     float neutral_q[PGX_NJ];
+    /* contacts (pgx_sim_params) */
+    float contact_dist, contact_erp, friction, warmstart;
 };
 
 struct PgxDevEnv {
@@ -46,13 +48,20 @@ struct PgxDevEnv {
     uint64_t seed, env_id_offset;
     double distance_threshold;
     double goal_low[3], goal_high[3];
+    /* scene (pgx_config): reset draws and the static boxes / object */
+    double goal_offset[3], goal_z_zero_prob;
+    double obj_low[3], obj_high[3], obj_offset[3];
+    int32_t contacts, has_object;
+    float obj_half, obj_inv_mass, obj_inv_inertia;
+    float table_cx, table_cy, table_hx, table_hy, table_top, plane_z;
 };
 
 struct PgxDevState {
     float* q;          /* [7][N] */
     float* qd;         /* [7][N] */
     double* goal;      /* [3][N] */
-    float* object;     /* [13][N] */
+    float* object;     /* [13][N] pos3 quat4 (x,y,z,w) linvel3 angvel3 */
+    float* contacts;   /* [2*PGX_CONTACT_SLOTS][N] warm-start cache (feature id, normal impulse) */
     int32_t* elapsed;  /* [N] */
     uint32_t* episode; /* [N] */
 };
@@ -74,7 +83,7 @@ struct PgxDevOut {
 int pgx_launch_step(const PgxDevModel* m_device, const PgxDevEnv& e, const PgxDevState& s, const float* action,
                     const PgxDevOut& o, void* stream);
 int pgx_launch_reset(const PgxDevModel* m_device, const PgxDevEnv& e, const PgxDevState& s, const uint8_t* mask,
-                     const double* inject_goal, const PgxDevOut& o, void* stream);
+                     const double* inject_goal, const double* inject_object, const PgxDevOut& o, void* stream);
 int pgx_launch_sample_actions(const PgxDevEnv& e, float* action, uint64_t step, void* stream);
 int pgx_launch_compute_reward(const float* ag, const float* dg, int64_t n, int32_t reward_type, double thr,
                               float* out, void* stream);

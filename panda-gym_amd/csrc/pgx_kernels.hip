@@ -23,6 +23,7 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "../../include/pgx.h"
 #include "pgx_common.h"
 #include "pgx_dev.h"
 #include "pgx_model_consts.h"
@@ -328,14 +329,236 @@ __device__ __forceinline__ void ik(MPtr mp, const float* q0, V3 target, const fl
 }
 
 /* --------------------------------------------------------------- physics */
-/* One Bullet stepSimulation() of the fixed-base arm (no contacts):
+/* ------------------------------------------------------------- contacts */
+/* Restated in oracle/pgx_oracle.c ("world: object + contacts"): two contact groups
+ * (object vs table/plane, robot vs table/plane/object) of at most CG points each, the
+ * deepest first, rows ordered by feature id; normal rows use ERP / speculative rhs, two
+ * friction rows per point along btPlaneSpace1(n) bounded by mu * normal impulse.
+ * Per-env contact data lives in LDS, lane-minor (x[...][lane]): conflict-free and
+ * dynamically indexable, unlike VGPRs. */
+constexpr int CG = 4;
+constexpr int CACHE_N = 2 * PGX_CONTACT_SLOTS;
+constexpr float kTableIdLimit = 32.0f;   /* robot feature ids < 32: capsule end vs table/plane */
+
+struct ContactLds {
+    /* group 0: object vertices vs table / plane (normal +z) */
+    float g0r[CG][3][64];          /* contact point - object COM */
+    float g0d[CG][64], g0id[CG][64];
+    float g0row[CG][3][4][64];     /* per direction: jinv, den, rhs, lambda */
+    /* group 1: robot vs table / plane / object */
+    float g1p[CG][3][64];          /* point on the robot */
+    float g1n[CG][3][64];          /* normal, from the other body to the robot */
+    float g1rb[CG][3][64];         /* object contacts: point on the object - object COM */
+    float g1d[CG][64], g1id[CG][64];
+    int g1j[CG][64];               /* arm joint carrying the robot link */
+    float g1J[CG][3][PGX_NJ][64];  /* robot Jacobian row per direction */
+    float g1R[CG][3][PGX_NJ][64];  /* M^-1 J^T */
+    float g1c[CG][3][6][64];       /* object part (linear, angular) of the row; 0 vs table */
+    float g1row[CG][3][4][64];
+    int cnt[2][64];
+    float cache[CACHE_N][64];      /* (feature id, normal impulse) x 4 per group */
+    float capA[PGX_NCAP][3][64], capB[PGX_NCAP][3][64];   /* capsule end points, world */
+};
+
+struct ObjState {
+    V3 p, v, w;
+    float qx, qy, qz, qw;
+};
+
+/* btPlaneSpace1 */
+__device__ __forceinline__ void plane_space(V3 n, V3& p, V3& q) {
+    if (fabsf(n.z) > 0.70710678f) {
+        float a = n.y * n.y + n.z * n.z, k = __builtin_amdgcn_rsqf(a);
+        p = v3(0.0f, -n.z * k, n.y * k);
+        q = v3(a * k, -n.x * p.z, n.x * p.y);
+    } else {
+        float a = n.x * n.x + n.y * n.y, k = __builtin_amdgcn_rsqf(a);
+        p = v3(-n.y * k, n.x * k, 0.0f);
+        q = v3(-n.z * p.y, n.z * p.x, a * k);
+    }
+}
+
+__device__ __forceinline__ float ground_z(const PgxDevEnv& e, float x, float y) {
+    return (fabsf(x - e.table_cx) <= e.table_hx && fabsf(y - e.table_cy) <= e.table_hy) ? e.table_top : e.plane_z;
+}
+
+/* keep the CG deepest candidates of group 0 (stable: an equal depth does not displace) */
+__device__ __forceinline__ void g0_insert(ContactLds& L, int ln, float d, float id, V3 r) {
+    int c = L.cnt[0][ln], pos;
+    if (c < CG) { pos = c; L.cnt[0][ln] = c + 1; }
+    else if (d < L.g0d[CG - 1][ln]) pos = CG - 1;
+    else return;
+    while (pos > 0 && d < L.g0d[pos - 1][ln]) {
+        L.g0d[pos][ln] = L.g0d[pos - 1][ln];
+        L.g0id[pos][ln] = L.g0id[pos - 1][ln];
+        for (int k = 0; k < 3; k++) L.g0r[pos][k][ln] = L.g0r[pos - 1][k][ln];
+        pos--;
+    }
+    L.g0d[pos][ln] = d; L.g0id[pos][ln] = id;
+    L.g0r[pos][0][ln] = r.x; L.g0r[pos][1][ln] = r.y; L.g0r[pos][2][ln] = r.z;
+}
+__device__ __forceinline__ void g1_copy(ContactLds& L, int ln, int to, int from) {
+    L.g1d[to][ln] = L.g1d[from][ln];
+    L.g1id[to][ln] = L.g1id[from][ln];
+    L.g1j[to][ln] = L.g1j[from][ln];
+    for (int k = 0; k < 3; k++) {
+        L.g1p[to][k][ln] = L.g1p[from][k][ln];
+        L.g1n[to][k][ln] = L.g1n[from][k][ln];
+        L.g1rb[to][k][ln] = L.g1rb[from][k][ln];
+    }
+}
+__device__ __forceinline__ void g1_insert(ContactLds& L, int ln, float d, float id, int j, V3 p, V3 n, V3 rb) {
+    int c = L.cnt[1][ln], pos;
+    if (c < CG) { pos = c; L.cnt[1][ln] = c + 1; }
+    else if (d < L.g1d[CG - 1][ln]) pos = CG - 1;
+    else return;
+    while (pos > 0 && d < L.g1d[pos - 1][ln]) { g1_copy(L, ln, pos, pos - 1); pos--; }
+    L.g1d[pos][ln] = d; L.g1id[pos][ln] = id; L.g1j[pos][ln] = j;
+    L.g1p[pos][0][ln] = p.x; L.g1p[pos][1][ln] = p.y; L.g1p[pos][2][ln] = p.z;
+    L.g1n[pos][0][ln] = n.x; L.g1n[pos][1][ln] = n.y; L.g1n[pos][2][ln] = n.z;
+    L.g1rb[pos][0][ln] = rb.x; L.g1rb[pos][1][ln] = rb.y; L.g1rb[pos][2][ln] = rb.z;
+}
+/* rows are ordered by feature id (insertion sort of <= 4 entries, via a spare slot-free swap) */
+__device__ __forceinline__ void sort_groups(ContactLds& L, int ln) {
+    const int c0 = L.cnt[0][ln];
+    for (int i = 1; i < c0; i++)
+        for (int j = i; j > 0 && L.g0id[j][ln] < L.g0id[j - 1][ln]; j--) {
+            float t = L.g0id[j][ln]; L.g0id[j][ln] = L.g0id[j - 1][ln]; L.g0id[j - 1][ln] = t;
+            t = L.g0d[j][ln]; L.g0d[j][ln] = L.g0d[j - 1][ln]; L.g0d[j - 1][ln] = t;
+            for (int k = 0; k < 3; k++) { t = L.g0r[j][k][ln]; L.g0r[j][k][ln] = L.g0r[j - 1][k][ln]; L.g0r[j - 1][k][ln] = t; }
+        }
+    const int c1 = L.cnt[1][ln];
+    for (int i = 1; i < c1; i++)
+        for (int j = i; j > 0 && L.g1id[j][ln] < L.g1id[j - 1][ln]; j--) {
+            float d = L.g1d[j][ln], id = L.g1id[j][ln];
+            int jj = L.g1j[j][ln];
+            float p[3], n[3], rb[3];
+            for (int k = 0; k < 3; k++) { p[k] = L.g1p[j][k][ln]; n[k] = L.g1n[j][k][ln]; rb[k] = L.g1rb[j][k][ln]; }
+            g1_copy(L, ln, j, j - 1);
+            L.g1d[j - 1][ln] = d; L.g1id[j - 1][ln] = id; L.g1j[j - 1][ln] = jj;
+            for (int k = 0; k < 3; k++) { L.g1p[j - 1][k][ln] = p[k]; L.g1n[j - 1][k][ln] = n[k]; L.g1rb[j - 1][k][ln] = rb[k]; }
+        }
+}
+
+/* object-frame helpers: R(q) v and R(q)^T v for the unit quaternion (x,y,z,w) */
+__device__ __forceinline__ M3 quat_mat(const ObjState& o) {
+    const float x = o.qx, y = o.qy, z = o.qz, w = o.qw;
+    return M3{{1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w),
+               2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
+               2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)}};
+}
+__device__ __forceinline__ V3 mul_t(const M3& A, V3 v) {
+    return v3(A.m[0] * v.x + A.m[3] * v.y + A.m[6] * v.z, A.m[1] * v.x + A.m[4] * v.y + A.m[7] * v.z,
+              A.m[2] * v.x + A.m[5] * v.y + A.m[8] * v.z);
+}
+
+/* Robot capsules against the table/plane (end spheres) and the object (spheres sampled
+ * along the axis), from the world end points the FK pass left in LDS.  A runtime loop
+ * over the capsule table (wave-uniform index: scalar loads) keeps the code compact. */
+template <int OBJ>
+__device__ __forceinline__ void robot_contacts(const PgxDevEnv& e, float tau, ContactLds& L, int ln, const ObjState& ob,
+                                            const M3& Rc) {
+    for (int c = 0; c < PGX_NCAP; c++) {
+        const V3 A = v3(L.capA[c][0][ln], L.capA[c][1][ln], L.capA[c][2][ln]);
+        const V3 B = v3(L.capB[c][0][ln], L.capB[c][1][ln], L.capB[c][2][ln]);
+        const float r = kCapR[c];
+        const int flags = kCapFlags[c], jc = kCapJ[c], ns = kCapNs[c];
+        if (flags & PGX_CAP_VS_TABLE) {
+            for (int end = 0; end < (ns == 1 ? 1 : 2); end++) {
+                const V3 P = end ? B : A;
+                const float zt = ground_z(e, P.x, P.y);
+                const float d = P.z - r - zt;
+                if (d < tau) g1_insert(L, ln, d, (float)(2 * c + end), jc, v3(P.x, P.y, P.z - r), v3(0.0f, 0.0f, 1.0f),
+                                       v3(0.0f, 0.0f, 0.0f));
+            }
+        }
+        if (OBJ && (flags & PGX_CAP_VS_OBJECT)) {
+            const float h = e.obj_half;
+            /* cull: segment farther from the object centre than r + h*sqrt(3) + tau */
+            const V3 ab = B - A;
+            const float l2 = dot(ab, ab);
+            float t = l2 > 0.0f ? dot(ob.p - A, ab) * fast_rcp(l2) : 0.0f;
+            t = fminf(fmaxf(t, 0.0f), 1.0f);
+            const V3 cp = A + t * ab - ob.p;
+            const float reach = r + 1.7320508f * h + tau;
+            if (dot(cp, cp) < reach * reach) {
+                const float inv_n = ns > 1 ? 1.0f / (float)(ns - 1) : 0.0f;
+                for (int s = 0; s < ns; s++) {
+                    const V3 C = A + ((float)s * inv_n) * ab;
+                    const V3 cl = mul_t(Rc, C - ob.p);
+                    V3 qb = v3(fminf(fmaxf(cl.x, -h), h), fminf(fmaxf(cl.y, -h), h), fminf(fmaxf(cl.z, -h), h));
+                    const V3 diff = cl - qb;
+                    const float d2 = dot(diff, diff);
+                    V3 nl;
+                    float depth;
+                    if (d2 > 1e-24f) {
+                        const float dist = fast_sqrt(d2);
+                        nl = fast_rcp(dist) * diff;
+                        depth = dist - r;
+                    } else { /* centre inside the box: out through the nearest face */
+                        const float bx = h - fabsf(cl.x), by = h - fabsf(cl.y), bz = h - fabsf(cl.z);
+                        int ax = 0;
+                        float best = bx;
+                        if (by < best) { best = by; ax = 1; }
+                        if (bz < best) { best = bz; ax = 2; }
+                        const float sx = cl.x < 0.0f ? -1.0f : 1.0f, sy = cl.y < 0.0f ? -1.0f : 1.0f,
+                                    sz = cl.z < 0.0f ? -1.0f : 1.0f;
+                        nl = v3(ax == 0 ? sx : 0.0f, ax == 1 ? sy : 0.0f, ax == 2 ? sz : 0.0f);
+                        if (ax == 0) qb.x = sx * h;
+                        if (ax == 1) qb.y = sy * h;
+                        if (ax == 2) qb.z = sz * h;
+                        depth = -best - r;
+                    }
+                    if (depth < tau) {
+                        const V3 n = mul(Rc, nl);
+                        g1_insert(L, ln, depth, (float)(32 + 16 * c + s), jc, C - r * n, n, mul(Rc, qb));
+                    }
+                }
+            }
+        }
+    }
+}
+
+/* world end points of the capsules carried by arm joint j (compile-time walk) */
+template <int C = 0>
+__device__ __forceinline__ void link_capsules(int j, ContactLds& L, int ln, const M3& R, V3 oj) {
+    if constexpr (C < PGX_NCAP) {
+        if (kCapJ[C] == j) {
+            const V3 A = oj + mulc(R, kCapA[C]), B = oj + mulc(R, kCapB[C]);
+            L.capA[C][0][ln] = A.x; L.capA[C][1][ln] = A.y; L.capA[C][2][ln] = A.z;
+            L.capB[C][0][ln] = B.x; L.capB[C][1][ln] = B.y; L.capB[C][2][ln] = B.z;
+        }
+        link_capsules<C + 1>(j, L, ln, R, oj);
+    }
+}
+
+/* One Bullet stepSimulation() of the arm (+ object and contacts when compiled in):
+ *   contacts at the current poses (CONT)
  *   qd_u = clamp(qd + dt * M^-1 (-b(q,qd)))          (ABA + applyDeltaVee)
+ *   object: v_u = v + dt (g - (k + k|v|) v - w x v), w_u = w - dt (k + k|w|) w
  *   PGS over the motor/limit rows in Bullet's sorted order, reversed on even
- *   sweeps, early exit when max squared row residual <= residual_thr
+ *   sweeps, then the contact normal rows, then the friction rows; early exit when
+ *   the max squared row residual <= residual_thr
  *   qd = clamp(qd_u + M^-1 J^T lambda); q += dt*qd   (constraint pass, stepPositions)
+ *   object: p += dt v, orientation by the exponential map of w dt
  * M by composite-rigid-body, b by Newton-Euler with Bullet's link damping. */
-__device__ __forceinline__ void substep(MPtr mp, float* q, float* qd, const float* tq) {
+template <int OBJ, int CONT>
+__device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, float* qd, const float* tq,
+                                        ObjState& ob, ContactLds* Lp, int ln) {
     MRef m = *fresh(mp);
+    M3 Rc;
+    if (OBJ) Rc = quat_mat(ob);
+    if (CONT) { Lp->cnt[0][ln] = 0; Lp->cnt[1][ln] = 0; }
+    if (OBJ) { /* object vertices vs the box top under them */
+        const float h = e.obj_half;
+#pragma unroll
+        for (int vtx = 0; vtx < 8; vtx++) {
+            const V3 r = mul(Rc, v3((vtx & 1) ? h : -h, (vtx & 2) ? h : -h, (vtx & 4) ? h : -h));
+            const V3 P = ob.p + r;
+            const float d = P.z - ground_z(e, P.x, P.y);
+            if (d < m.contact_dist) g0_insert(*Lp, ln, d, (float)vtx, r);
+        }
+    }
     /* FK fused with the per-link quantities the dynamics need, so the 3x3
      * rotations die immediately (only panda_link7's survives for its group). */
     V3 z[NJ], o[NJ], c[NJ];
@@ -361,9 +584,14 @@ __device__ __forceinline__ void substep(MPtr mp, float* q, float* qd, const floa
             c[j] = oj + mulc(R, kCom[j]);
             if (j < NJ - 1) Iw[j] = rot_diag(R, kInertia[j]);
             else { Iw[j] = rot_sym(R, kI6c); R6 = R; }
+            if constexpr (CONT) link_capsules(j, *Lp, ln, R, oj);
             PR = R;
             PO = oj;
         }
+    }
+    if (CONT) {
+        robot_contacts<OBJ>(e, m.contact_dist, *Lp, ln, ob, Rc);
+        sort_groups(*Lp, ln);
     }
     const V3 g = v3(m.gravity[0], m.gravity[1], m.gravity[2]);
 
@@ -484,6 +712,121 @@ __device__ __forceinline__ void substep(MPtr mp, float* q, float* qd, const floa
     }
 #define MINV(a, b) ((a) >= (b) ? Mi[a][b] : Mi[b][a])
 
+    /* object: unconstrained velocities (btMultiBody floating base) */
+    V3 vcu = v3(0, 0, 0), wcu = v3(0, 0, 0);
+    if (OBJ) {
+        const float vn = norm(ob.v), wn = norm(ob.w);
+        vcu = ob.v + m.dt * (g - (m.lin_damp + m.lin_damp * vn) * ob.v - cross(ob.w, ob.v));
+        wcu = ob.w - (m.dt * (m.ang_damp + m.ang_damp * wn)) * ob.w;
+    }
+    float dv[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; j++) dv[j] = 0.0f;
+    V3 dvl = v3(0, 0, 0), dvw = v3(0, 0, 0);   /* object velocity deltas */
+    const float inv_m = e.obj_inv_mass, inv_i = e.obj_inv_inertia;
+
+    /* ---- contact rows (setup + warm start) */
+    int n0 = 0, n1 = 0;
+    if (CONT) {
+        ContactLds& L = *Lp;
+        n0 = L.cnt[0][ln];
+        n1 = L.cnt[1][ln];
+        const float erp_dt = m.contact_erp * m.inv_dt;
+        for (int k = 0; k < CG; k++) {
+            if (OBJ && k < n0) {
+                const V3 r = v3(L.g0r[k][0][ln], L.g0r[k][1][ln], L.g0r[k][2][ln]);
+                const float id = L.g0id[k][ln];
+                float warm = 0.0f;
+#pragma unroll
+                for (int s = 0; s < CG; s++) if (L.cache[2 * s][ln] == id) warm = m.warmstart * L.cache[2 * s + 1][ln];
+#pragma unroll
+                for (int dir = 0; dir < 3; dir++) {
+                    /* u = +z, -y, +x (btPlaneSpace1(+z)); ang = r x u */
+                    const V3 lin = dir == 0 ? v3(0, 0, 1) : (dir == 1 ? v3(0, -1, 0) : v3(1, 0, 0));
+                    const V3 ang = dir == 0 ? v3(r.y, -r.x, 0) : (dir == 1 ? v3(r.z, 0, -r.x) : v3(0, r.z, -r.y));
+                    const float den = inv_m + dot(ang, ang) * inv_i;
+                    const float jinv = den > 2.220446e-16f ? fast_rcp(den) : 0.0f;
+                    const float rel = dot(lin, vcu) + dot(ang, wcu);
+                    float rhs;
+                    if (dir == 0) {
+                        const float pen = L.g0d[k][ln];
+                        rhs = (pen > 0.0f ? (-rel - pen * m.inv_dt) : (-pen * erp_dt - rel)) * jinv;
+                    } else {
+                        rhs = -rel * jinv;
+                    }
+                    const float lam = dir == 0 ? warm : 0.0f;
+                    L.g0row[k][dir][0][ln] = jinv;
+                    L.g0row[k][dir][1][ln] = den;
+                    L.g0row[k][dir][2][ln] = rhs;
+                    L.g0row[k][dir][3][ln] = lam;
+                    if (dir == 0) { dvl = dvl + (lam * inv_m) * lin; dvw = dvw + (lam * inv_i) * ang; }
+                }
+            }
+            if (k < n1) {
+                const V3 P = v3(L.g1p[k][0][ln], L.g1p[k][1][ln], L.g1p[k][2][ln]);
+                const V3 n = v3(L.g1n[k][0][ln], L.g1n[k][1][ln], L.g1n[k][2][ln]);
+                const V3 rb = v3(L.g1rb[k][0][ln], L.g1rb[k][1][ln], L.g1rb[k][2][ln]);
+                const int jl = L.g1j[k][ln];
+                const float id = L.g1id[k][ln];
+                const bool vs_obj = OBJ && id >= kTableIdLimit;
+                float warm = 0.0f;
+#pragma unroll
+                for (int s = 0; s < CG; s++)
+                    if (L.cache[8 + 2 * s][ln] == id) warm = m.warmstart * L.cache[8 + 2 * s + 1][ln];
+                V3 t1, t2;
+                plane_space(n, t1, t2);
+                V3 Jv[NJ];
+#pragma unroll
+                for (int a = 0; a < NJ; a++) Jv[a] = a <= jl ? cross(z[a], P - o[a]) : v3(0, 0, 0);
+#pragma unroll
+                for (int dir = 0; dir < 3; dir++) {
+                    const V3 u = dir == 0 ? n : (dir == 1 ? t1 : t2);
+                    float J[NJ], Rs[NJ];
+                    float den = 0.0f, rel = 0.0f;
+#pragma unroll
+                    for (int a = 0; a < NJ; a++) { J[a] = dot(u, Jv[a]); rel += J[a] * vu[a]; }
+#pragma unroll
+                    for (int a = 0; a < NJ; a++) {
+                        float s = 0.0f;
+#pragma unroll
+                        for (int b = 0; b < NJ; b++) s += MINV(a, b) * J[b];
+                        Rs[a] = s;
+                        den += J[a] * s;
+                    }
+                    V3 cl = v3(0, 0, 0), ca = v3(0, 0, 0);
+                    if (vs_obj) {
+                        cl = -1.0f * u;
+                        ca = -1.0f * cross(rb, u);
+                        den += inv_m * dot(cl, cl) + inv_i * dot(ca, ca);
+                        rel += dot(cl, vcu) + dot(ca, wcu);
+                    }
+                    const float jinv = den > 2.220446e-16f ? fast_rcp(den) : 0.0f;
+                    float rhs;
+                    if (dir == 0) {
+                        const float pen = L.g1d[k][ln];
+                        rhs = (pen > 0.0f ? (-rel - pen * m.inv_dt) : (-pen * erp_dt - rel)) * jinv;
+                    } else {
+                        rhs = -rel * jinv;
+                    }
+                    const float lam = dir == 0 ? warm : 0.0f;
+#pragma unroll
+                    for (int a = 0; a < NJ; a++) { L.g1J[k][dir][a][ln] = J[a]; L.g1R[k][dir][a][ln] = Rs[a]; }
+                    L.g1c[k][dir][0][ln] = cl.x; L.g1c[k][dir][1][ln] = cl.y; L.g1c[k][dir][2][ln] = cl.z;
+                    L.g1c[k][dir][3][ln] = ca.x; L.g1c[k][dir][4][ln] = ca.y; L.g1c[k][dir][5][ln] = ca.z;
+                    L.g1row[k][dir][0][ln] = jinv;
+                    L.g1row[k][dir][1][ln] = den;
+                    L.g1row[k][dir][2][ln] = rhs;
+                    L.g1row[k][dir][3][ln] = lam;
+                    if (dir == 0) {
+#pragma unroll
+                        for (int a = 0; a < NJ; a++) dv[a] += Rs[a] * lam;
+                        if (OBJ) { dvl = dvl + (lam * inv_m) * cl; dvw = dvw + (lam * inv_i) * ca; }
+                    }
+                }
+            }
+        }
+    }
+
     /* rows (btMultiBodyJointMotor / btMultiBodyJointLimitConstraint::createConstraintRows):
      * jinv depends only on the dof, bounds are constants, so per row only rhs and
      * the accumulated impulse live in registers. */
@@ -523,8 +866,9 @@ __device__ __forceinline__ void substep(MPtr mp, float* q, float* qd, const floa
      * can only get a positive impulse once vu_d + dv_d crosses -pen/dt (lower) or
      * +pen/dt (upper); if that is impossible for every limit row, none ever leaves 0
      * during the sweep (by induction), every evaluation of them clamps to delta = 0,
-     * and dropping them changes no bit of the result or of the exit iteration. */
-    bool far = true;
+     * and dropping them changes no bit of the result or of the exit iteration.  Robot
+     * contact impulses are unbounded, so the skip needs an env without robot contacts. */
+    bool far = n1 == 0;
 #pragma unroll
     for (int d = 0; d < NJ; d++) {
         float B = 0.0f;
@@ -534,9 +878,6 @@ __device__ __forceinline__ void substep(MPtr mp, float* q, float* qd, const floa
         const float penl = q[d] - kLower[d], penu = kUpper[d] - q[d];
         far = far && penl > 0.0f && penu > 0.0f && (vu[d] - B) > -penl * m.inv_dt && (vu[d] + B) < penu * m.inv_dt;
     }
-    float dv[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; j++) dv[j] = 0.0f;
     /* resolveSingleConstraintRowGeneric, branch-free: clamp the accumulated impulse,
      * apply the clamped delta through the unit response M^-1 J^T (a column of M^-1). */
     auto row = [&](const int r, float& resid) {
@@ -558,6 +899,72 @@ __device__ __forceinline__ void substep(MPtr mp, float* q, float* qd, const floa
          * once per sweep equals the max of the squares */
         resid = fmaxf(resid, fabsf(delta * den[d]));
     };
+    /* contact rows: normal rows of both groups, then friction rows (bounds from the
+     * current normal impulse, skipped while it is 0) */
+    auto contact_rows = [&](float& resid) {
+        ContactLds& L = *Lp;
+#pragma unroll
+        for (int fr = 0; fr < 2; fr++) {
+            if (OBJ) {
+                for (int k = 0; k < CG; k++) {
+                    if (!__any(k < n0)) break;
+                    if (k < n0) {
+                        const V3 r = v3(L.g0r[k][0][ln], L.g0r[k][1][ln], L.g0r[k][2][ln]);
+                        const float ln_n = L.g0row[k][0][3][ln];
+#pragma unroll
+                        for (int dir = fr ? 1 : 0; dir < (fr ? 3 : 1); dir++) {
+                            if (fr && !(ln_n > 0.0f)) continue;
+                            const V3 lin = dir == 0 ? v3(0, 0, 1) : (dir == 1 ? v3(0, -1, 0) : v3(1, 0, 0));
+                            const V3 ang = dir == 0 ? v3(r.y, -r.x, 0) : (dir == 1 ? v3(r.z, 0, -r.x) : v3(0, r.z, -r.y));
+                            const float jv = L.g0row[k][dir][0][ln], dn = L.g0row[k][dir][1][ln];
+                            const float rh = L.g0row[k][dir][2][ln], lm = L.g0row[k][dir][3][ln];
+                            const float lo = fr ? -m.friction * ln_n : 0.0f;
+                            const float hi = fr ? m.friction * ln_n : 1e10f;
+                            float delta = rh - (dot(lin, dvl) + dot(ang, dvw)) * jv;
+                            const float nl = __builtin_amdgcn_fmed3f(lm + delta, lo, hi);
+                            delta = nl - lm;
+                            L.g0row[k][dir][3][ln] = nl;
+                            dvl = dvl + (delta * inv_m) * lin;
+                            dvw = dvw + (delta * inv_i) * ang;
+                            resid = fmaxf(resid, fabsf(delta * dn));
+                        }
+                    }
+                }
+            }
+            for (int k = 0; k < CG; k++) {
+                if (!__any(k < n1)) break;
+                if (k < n1) {
+                    const float ln_n = L.g1row[k][0][3][ln];
+#pragma unroll
+                    for (int dir = fr ? 1 : 0; dir < (fr ? 3 : 1); dir++) {
+                        if (fr && !(ln_n > 0.0f)) continue;
+                        const float jv = L.g1row[k][dir][0][ln], dn = L.g1row[k][dir][1][ln];
+                        const float rh = L.g1row[k][dir][2][ln], lm = L.g1row[k][dir][3][ln];
+                        const float lo = fr ? -m.friction * ln_n : 0.0f;
+                        const float hi = fr ? m.friction * ln_n : 1e10f;
+                        float jdv = 0.0f;
+#pragma unroll
+                        for (int a = 0; a < NJ; a++) jdv += L.g1J[k][dir][a][ln] * dv[a];
+                        V3 cl = v3(0, 0, 0), ca = v3(0, 0, 0);
+                        if (OBJ) {
+                            cl = v3(L.g1c[k][dir][0][ln], L.g1c[k][dir][1][ln], L.g1c[k][dir][2][ln]);
+                            ca = v3(L.g1c[k][dir][3][ln], L.g1c[k][dir][4][ln], L.g1c[k][dir][5][ln]);
+                            jdv += dot(cl, dvl) + dot(ca, dvw);
+                        }
+                        float delta = rh - jdv * jv;
+                        const float nl = __builtin_amdgcn_fmed3f(lm + delta, lo, hi);
+                        delta = nl - lm;
+                        L.g1row[k][dir][3][ln] = nl;
+#pragma unroll
+                        for (int a = 0; a < NJ; a++) dv[a] += L.g1R[k][dir][a][ln] * delta;
+                        if (OBJ) { dvl = dvl + (delta * inv_m) * cl; dvw = dvw + (delta * inv_i) * ca; }
+                        resid = fmaxf(resid, fabsf(delta * dn));
+                    }
+                }
+            }
+        }
+    };
+    const bool any_contact = CONT && __any(n0 > 0 || n1 > 0);
     if (__all(far)) {
         for (int it = 0; it < m.num_iterations; it++) {
             float resid = 0.0f;
@@ -570,6 +977,7 @@ __device__ __forceinline__ void substep(MPtr mp, float* q, float* qd, const floa
                 for (int r = PGX_N_ROWS - 1; r >= 0; r--)
                     if ((kPgxRowCode[r] >> 4) == 0) row(r, resid);
             }
+            if (CONT && any_contact) contact_rows(resid);
             if (resid * resid <= m.residual_thr) break;
         }
     } else {
@@ -583,6 +991,7 @@ __device__ __forceinline__ void substep(MPtr mp, float* q, float* qd, const floa
 #pragma unroll
                 for (int r = PGX_N_ROWS - 1; r >= 0; r--) row(r, resid);
             }
+            if (CONT && any_contact) contact_rows(resid);
             if (resid * resid <= m.residual_thr) break;
         }
     }
@@ -592,6 +1001,35 @@ __device__ __forceinline__ void substep(MPtr mp, float* q, float* qd, const floa
         float vn = fminf(fmaxf(vu[j] + dv[j], -m.max_vel), m.max_vel);
         qd[j] = vn;
         q[j] += m.dt * vn;
+    }
+    if (CONT) { /* contact cache: this step's features and normal impulses */
+        ContactLds& L = *Lp;
+#pragma unroll
+        for (int s = 0; s < CG; s++) {
+            L.cache[2 * s][ln] = s < n0 ? L.g0id[s][ln] : -1.0f;
+            L.cache[2 * s + 1][ln] = s < n0 ? L.g0row[s][0][3][ln] : 0.0f;
+            L.cache[8 + 2 * s][ln] = s < n1 ? L.g1id[s][ln] : -1.0f;
+            L.cache[8 + 2 * s + 1][ln] = s < n1 ? L.g1row[s][0][3][ln] : 0.0f;
+        }
+    }
+    if (OBJ) {
+        ob.v = vcu + dvl;
+        ob.w = wcu + dvw;
+        ob.p = ob.p + m.dt * ob.v;
+        /* btMultiBody::stepPositionsMultiDof, base: exponential map of w dt */
+        float ang = norm(ob.w);
+        if (ang * m.dt > 0.39269908f) ang = 0.39269908f * m.inv_dt;
+        const float hdt = 0.5f * m.dt;
+        const float f = ang < 0.001f ? (hdt - m.dt * m.dt * m.dt * 0.020833333333f * ang * ang)
+                                     : __sinf(ang * hdt) * fast_rcp(ang);
+        const float ax = ob.w.x * f, ay = ob.w.y * f, az = ob.w.z * f, aw = __cosf(ang * hdt);
+        /* dq * q (Hamilton, (x,y,z,w)) */
+        const float nx = aw * ob.qx + ax * ob.qw + ay * ob.qz - az * ob.qy;
+        const float ny = aw * ob.qy + ay * ob.qw + az * ob.qx - ax * ob.qz;
+        const float nz = aw * ob.qz + az * ob.qw + ax * ob.qy - ay * ob.qx;
+        const float nw = aw * ob.qw - ax * ob.qx - ay * ob.qy - az * ob.qz;
+        const float inn = __builtin_amdgcn_rsqf(nx * nx + ny * ny + nz * nz + nw * nw);
+        ob.qx = nx * inn; ob.qy = ny * inn; ob.qz = nz * inn; ob.qw = nw * inn;
     }
 }
 
@@ -629,6 +1067,8 @@ __device__ double distance_f32_f64(V3 ag, const double* gl) {
     double d = sqrt(s);
     return rint(d * 1e6) / 1e6;
 }
+/* goal = offset + noise (push.py:71-74), unfused */
+__device__ double goal_add(double a, double b) { return a + b; }
 /* numpy Generator.uniform: low + (high - low) * u, unfused */
 __device__ double uniform_draw(double low, double high, double u) {
     double r = high - low;
@@ -637,71 +1077,143 @@ __device__ double uniform_draw(double low, double high, double u) {
 }
 #pragma clang fp contract(on)
 
-__device__ __forceinline__ void write_obs(const PgxDevEnv& e, float* dst, V3 pos, V3 vel) {
-    dst[0] = pos.x; dst[1] = pos.y; dst[2] = pos.z;
-    dst[3] = vel.x; dst[4] = vel.y; dst[5] = vel.z;
-    if (!e.block_gripper) dst[6] = 0.0f; /* custom_0 fingers are fixed joints: width 0 */
+/* pybullet getEulerFromQuaternion (PyBullet.get_base_rotation, pybullet.py:216-219) */
+__device__ __forceinline__ V3 quat_euler(const ObjState& o) {
+    const float x = o.qx, y = o.qy, z = o.qz, w = o.qw;
+    const float sqx = x * x, sqy = y * y, sqz = z * z, squ = w * w;
+    const float sarg = -2.0f * (x * z - w * y);
+    const float pitch = sarg <= -1.0f ? -0.5f * 3.141592538f : (sarg >= 1.0f ? 0.5f * 3.141592538f : asinf(sarg));
+    const float roll = atan2f(2.0f * (y * z + w * x), squ - sqx - sqy + sqz);
+    const float yaw = atan2f(2.0f * (x * y + w * z), squ + sqx - sqy - sqz);
+    return v3(roll, pitch, yaw);
 }
 
-__device__ __forceinline__ void reset_env(MRef m, const PgxDevEnv& e, int i, uint32_t& episode,
-                                          const double* inject, float* q, float* qd, double* goal) {
+/* RobotTaskEnv._get_obs (core.py:286-296): robot obs (panda.py:264-288), then the task
+ * obs of Push / PickAndPlace (push.py:49-63): object position, euler, velocity, angular
+ * velocity. */
+template <int OBJ>
+__device__ __forceinline__ void write_obs(const PgxDevEnv& e, float* dst, V3 pos, V3 vel, const ObjState& ob) {
+    dst[0] = pos.x; dst[1] = pos.y; dst[2] = pos.z;
+    dst[3] = vel.x; dst[4] = vel.y; dst[5] = vel.z;
+    int n = 6;
+    if (!e.block_gripper) dst[n++] = 0.0f; /* custom_0 fingers are fixed joints: width 0 */
+    if (OBJ) {
+        const V3 rpy = quat_euler(ob);
+        dst[n] = ob.p.x; dst[n + 1] = ob.p.y; dst[n + 2] = ob.p.z;
+        dst[n + 3] = rpy.x; dst[n + 4] = rpy.y; dst[n + 5] = rpy.z;
+        dst[n + 6] = ob.v.x; dst[n + 7] = ob.v.y; dst[n + 8] = ob.v.z;
+        dst[n + 9] = ob.w.x; dst[n + 10] = ob.w.y; dst[n + 11] = ob.w.z;
+    }
+}
+
+/* Panda.reset + Task.reset (reach.py:63-78, push.py:69-87, pick_and_place.py:65-85): draws
+ * in the reference's order (goal noise 0-2, PickAndPlace's z coin 3, object noise); the
+ * object is re-posed upright, its velocity kept (resetBasePositionAndOrientation). */
+template <int OBJ>
+__device__ __forceinline__ void reset_env(MRef m, const PgxDevEnv& e, int i, uint32_t& episode, const double* inject,
+                                          const double* inject_obj, float* q, float* qd, double* goal,
+                                          ObjState& ob) {
 #pragma unroll
     for (int j = 0; j < NJ; j++) { q[j] = m.neutral_q[j]; qd[j] = 0.0f; }
     uint64_t env = e.env_id_offset + (uint64_t)i;
+    double noise[3];
 #pragma unroll
-    for (int c = 0; c < 3; c++)
-        goal[c] = inject ? inject[c] : uniform_draw(e.goal_low[c], e.goal_high[c], reset_uniform(e, env, episode, c));
+    for (int c = 0; c < 3; c++) noise[c] = uniform_draw(e.goal_low[c], e.goal_high[c], reset_uniform(e, env, episode, c));
+    int k = 3;
+    if (OBJ && e.goal_z_zero_prob > 0.0) {
+        if (reset_uniform(e, env, episode, k) < e.goal_z_zero_prob) noise[2] = 0.0;
+        k++;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; c++) goal[c] = inject ? inject[c] : goal_add(e.goal_offset[c], noise[c]);
+    if (OBJ) {
+        double p[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++)
+            p[c] = inject_obj ? inject_obj[c]
+                              : goal_add(e.obj_offset[c],
+                                         uniform_draw(e.obj_low[c], e.obj_high[c], reset_uniform(e, env, episode, k + c)));
+        ob.p = v3((float)p[0], (float)p[1], (float)p[2]);
+        ob.qx = 0.0f; ob.qy = 0.0f; ob.qz = 0.0f; ob.qw = 1.0f;
+    }
     episode += 1;
 }
 
-template <int CONTROL>
+__device__ __forceinline__ void load_obj(const PgxDevState& s, int N, int i, ObjState& ob) {
+    const float* o = s.object;
+    ob.p = v3(o[0 * N + i], o[1 * N + i], o[2 * N + i]);
+    ob.qx = o[3 * N + i]; ob.qy = o[4 * N + i]; ob.qz = o[5 * N + i]; ob.qw = o[6 * N + i];
+    ob.v = v3(o[7 * N + i], o[8 * N + i], o[9 * N + i]);
+    ob.w = v3(o[10 * N + i], o[11 * N + i], o[12 * N + i]);
+}
+__device__ __forceinline__ void store_obj(const PgxDevState& s, int N, int i, const ObjState& ob) {
+    float* o = s.object;
+    o[0 * N + i] = ob.p.x; o[1 * N + i] = ob.p.y; o[2 * N + i] = ob.p.z;
+    o[3 * N + i] = ob.qx; o[4 * N + i] = ob.qy; o[5 * N + i] = ob.qz; o[6 * N + i] = ob.qw;
+    o[7 * N + i] = ob.v.x; o[8 * N + i] = ob.v.y; o[9 * N + i] = ob.v.z;
+    o[10 * N + i] = ob.w.x; o[11 * N + i] = ob.w.y; o[12 * N + i] = ob.w.z;
+}
+
+template <int CONTROL, int OBJ, int CONT>
 __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict__ mdev, PgxDevEnv e, PgxDevState s,
                                                   const float* __restrict__ action, PgxDevOut o) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ln = threadIdx.x;
+    const int i = blockIdx.x * blockDim.x + ln;
     const int N = e.n_envs;
     if (i >= N) return;
+    const int ii = i;
+    ContactLds* L = nullptr;
+    if constexpr (CONT) {
+        __shared__ ContactLds lds_buf;   /* ~108 KB: one wave per CU holds its envs' contact rows */
+        L = &lds_buf;
+    }
     const MPtr mp = fresh((uint64_t)mdev);
     MRef m = *mp;
     float q[NJ], qd[NJ], tq[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; j++) {
-        q[j] = s.q[j * N + i];
-        qd[j] = s.qd[j * N + i];
+        q[j] = s.q[j * N + ii];
+        qd[j] = s.qd[j * N + ii];
     }
     double goal[3];
 #pragma unroll
-    for (int c = 0; c < 3; c++) goal[c] = s.goal[c * N + i];
+    for (int c = 0; c < 3; c++) goal[c] = s.goal[c * N + ii];
+    ObjState ob;
+    if (OBJ) load_obj(s, N, ii, ob);
+    if (CONT) {
+#pragma unroll
+        for (int k = 0; k < CACHE_N; k++) L->cache[k][ln] = s.contacts[k * N + ii];
+    }
 
     /* Panda.set_action: clip to Box(-1,1) in float32 */
     const int A = e.action_dim;
     if (CONTROL == 0) {
         float a[3];
 #pragma unroll
-        for (int c = 0; c < 3; c++) a[c] = fminf(fmaxf(action[(size_t)i * A + c], -1.0f), 1.0f);
-        V3 pos, vel;
+        for (int c = 0; c < 3; c++) a[c] = fminf(fmaxf(action[(size_t)ii * A + c], -1.0f), 1.0f);
         Chain k;
         fk_chain(m, q, k);
-        pos = k.o[NJ - 1] + mulc(k.R[NJ - 1], kEeCom);
+        V3 pos = k.o[NJ - 1] + mulc(k.R[NJ - 1], kEeCom);
         V3 tgt = pos + v3(a[0] * m.ee_step, a[1] * m.ee_step, a[2] * m.ee_step);
         tgt.z = fmaxf(0.0f, tgt.z);
         const float torn[4] = {1.0f, 0.0f, 0.0f, 0.0f};
         ik(mp, q, tgt, torn, tq);
-        (void)vel;
     } else {
 #pragma unroll
         for (int j = 0; j < NJ; j++) {
-            float a = fminf(fmaxf(action[(size_t)i * A + j], -1.0f), 1.0f);
+            float a = fminf(fmaxf(action[(size_t)ii * A + j], -1.0f), 1.0f);
             tq[j] = q[j] + a * m.joint_step;
         }
     }
 
     const int n_substeps = m.n_substeps;
-    for (int st = 0; st < n_substeps; st++) substep(mp, q, qd, tq);
+    for (int st = 0; st < n_substeps; st++) substep<OBJ, CONT>(mp, e, q, qd, tq, ob, L, ln);
 
     V3 pos, vel;
     ee_state(*fresh(mp), q, qd, pos, vel);
     const int od = e.obs_dim;
-    double d = distance_f32_f64(pos, goal);
+    const V3 ag = OBJ ? ob.p : pos;
+    double d = distance_f32_f64(ag, goal);
     bool succ = d < e.distance_threshold;
     float rew = e.reward == 0 ? -((d > e.distance_threshold) ? 1.0f : 0.0f) : -(float)d;
     int el = s.elapsed[i] + 1;
@@ -712,21 +1224,26 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
     if (o.terminated) o.terminated[i] = 0;
     if (o.truncated) o.truncated[i] = trunc;
     if (trunc) {
-        if (o.terminal_obs) write_obs(e, o.terminal_obs + (size_t)i * od, pos, vel);
+        if (o.terminal_obs) write_obs<OBJ>(e, o.terminal_obs + (size_t)i * od, pos, vel, ob);
         if (o.terminal_ag) {
-            o.terminal_ag[3 * (size_t)i] = pos.x; o.terminal_ag[3 * (size_t)i + 1] = pos.y;
-            o.terminal_ag[3 * (size_t)i + 2] = pos.z;
+            o.terminal_ag[3 * (size_t)i] = ag.x; o.terminal_ag[3 * (size_t)i + 1] = ag.y;
+            o.terminal_ag[3 * (size_t)i + 2] = ag.z;
         }
         if (o.terminal_dg) {
             o.terminal_dg[3 * (size_t)i] = (float)goal[0]; o.terminal_dg[3 * (size_t)i + 1] = (float)goal[1];
             o.terminal_dg[3 * (size_t)i + 2] = (float)goal[2];
         }
-        reset_env(m, e, i, episode, nullptr, q, qd, goal);
+        reset_env<OBJ>(m, e, i, episode, nullptr, nullptr, q, qd, goal, ob);
         el = 0;
         ee_state(m, q, qd, pos, vel);
+        if (CONT) {
+#pragma unroll
+            for (int k = 0; k < CACHE_N; k++) L->cache[k][ln] = (k & 1) ? 0.0f : -1.0f;
+        }
     }
-    if (o.obs) write_obs(e, o.obs + (size_t)i * od, pos, vel);
-    if (o.ag) { o.ag[3 * (size_t)i] = pos.x; o.ag[3 * (size_t)i + 1] = pos.y; o.ag[3 * (size_t)i + 2] = pos.z; }
+    const V3 ag2 = OBJ ? ob.p : pos;
+    if (o.obs) write_obs<OBJ>(e, o.obs + (size_t)i * od, pos, vel, ob);
+    if (o.ag) { o.ag[3 * (size_t)i] = ag2.x; o.ag[3 * (size_t)i + 1] = ag2.y; o.ag[3 * (size_t)i + 2] = ag2.z; }
     if (o.dg) {
         o.dg[3 * (size_t)i] = (float)goal[0]; o.dg[3 * (size_t)i + 1] = (float)goal[1];
         o.dg[3 * (size_t)i + 2] = (float)goal[2];
@@ -738,12 +1255,19 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
     }
 #pragma unroll
     for (int c = 0; c < 3; c++) s.goal[c * N + i] = goal[c];
+    if (OBJ) store_obj(s, N, i, ob);
+    if (CONT) {
+#pragma unroll
+        for (int k = 0; k < CACHE_N; k++) s.contacts[k * N + i] = L->cache[k][ln];
+    }
     s.elapsed[i] = el;
     s.episode[i] = episode;
 }
 
+template <int OBJ>
 __global__ __launch_bounds__(64) void reset_kernel(const PgxDevModel* __restrict__ mdev, PgxDevEnv e, PgxDevState s,
-                                                   const uint8_t* mask, const double* inject_goal, PgxDevOut o) {
+                                                   const uint8_t* mask, const double* inject_goal,
+                                                   const double* inject_obj, PgxDevOut o) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int N = e.n_envs;
     if (i >= N) return;
@@ -751,17 +1275,21 @@ __global__ __launch_bounds__(64) void reset_kernel(const PgxDevModel* __restrict
     if (mask && !mask[i]) return;
     float q[NJ], qd[NJ];
     double goal[3];
+    ObjState ob;
+    if (OBJ) load_obj(s, N, i, ob);
     uint32_t episode = s.episode[i];
-    reset_env(m, e, i, episode, inject_goal ? inject_goal + 3 * (size_t)i : nullptr, q, qd, goal);
+    reset_env<OBJ>(m, e, i, episode, inject_goal ? inject_goal + 3 * (size_t)i : nullptr,
+                   inject_obj ? inject_obj + 3 * (size_t)i : nullptr, q, qd, goal, ob);
     V3 pos, vel;
     ee_state(m, q, qd, pos, vel);
-    if (o.obs) write_obs(e, o.obs + (size_t)i * e.obs_dim, pos, vel);
-    if (o.ag) { o.ag[3 * (size_t)i] = pos.x; o.ag[3 * (size_t)i + 1] = pos.y; o.ag[3 * (size_t)i + 2] = pos.z; }
+    const V3 ag = OBJ ? ob.p : pos;
+    if (o.obs) write_obs<OBJ>(e, o.obs + (size_t)i * e.obs_dim, pos, vel, ob);
+    if (o.ag) { o.ag[3 * (size_t)i] = ag.x; o.ag[3 * (size_t)i + 1] = ag.y; o.ag[3 * (size_t)i + 2] = ag.z; }
     if (o.dg) {
         o.dg[3 * (size_t)i] = (float)goal[0]; o.dg[3 * (size_t)i + 1] = (float)goal[1];
         o.dg[3 * (size_t)i + 2] = (float)goal[2];
     }
-    if (o.success) o.success[i] = distance_f32_f64(pos, goal) < e.distance_threshold;
+    if (o.success) o.success[i] = distance_f32_f64(ag, goal) < e.distance_threshold;
 #pragma unroll
     for (int j = 0; j < NJ; j++) {
         s.q[j * N + i] = q[j];
@@ -769,6 +1297,9 @@ __global__ __launch_bounds__(64) void reset_kernel(const PgxDevModel* __restrict
     }
 #pragma unroll
     for (int c = 0; c < 3; c++) s.goal[c * N + i] = goal[c];
+    if (OBJ) store_obj(s, N, i, ob);
+#pragma unroll
+    for (int k = 0; k < CACHE_N; k++) s.contacts[k * N + i] = (k & 1) ? 0.0f : -1.0f;
     s.elapsed[i] = 0;
     s.episode[i] = episode;
 }
@@ -803,17 +1334,26 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
                     const PgxDevOut& o, void* stream) {
     dim3 block(64), grid((e.n_envs + 63) / 64);
     hipStream_t st = (hipStream_t)stream;
-    if (e.control == 0)
-        hipLaunchKernelGGL(step_kernel<0>, grid, block, 0, st, m, e, s, action, o);
-    else
-        hipLaunchKernelGGL(step_kernel<1>, grid, block, 0, st, m, e, s, action, o);
+    const int variant = e.control * 4 + (e.has_object ? 2 : 0) + (e.contacts ? 1 : 0);
+    switch (variant) {
+        case 0: hipLaunchKernelGGL((step_kernel<0, 0, 0>), grid, block, 0, st, m, e, s, action, o); break;
+        case 1: hipLaunchKernelGGL((step_kernel<0, 0, 1>), grid, block, 0, st, m, e, s, action, o); break;
+        case 3: hipLaunchKernelGGL((step_kernel<0, 1, 1>), grid, block, 0, st, m, e, s, action, o); break;
+        case 4: hipLaunchKernelGGL((step_kernel<1, 0, 0>), grid, block, 0, st, m, e, s, action, o); break;
+        case 5: hipLaunchKernelGGL((step_kernel<1, 0, 1>), grid, block, 0, st, m, e, s, action, o); break;
+        case 7: hipLaunchKernelGGL((step_kernel<1, 1, 1>), grid, block, 0, st, m, e, s, action, o); break;
+        default: return (int)hipErrorInvalidValue;   /* object without contacts: rejected at create */
+    }
     return (int)hipGetLastError();
 }
 
 int pgx_launch_reset(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState& s, const uint8_t* mask,
-                     const double* inject_goal, const PgxDevOut& o, void* stream) {
+                     const double* inject_goal, const double* inject_obj, const PgxDevOut& o, void* stream) {
     dim3 block(64), grid((e.n_envs + 63) / 64);
-    hipLaunchKernelGGL(reset_kernel, grid, block, 0, (hipStream_t)stream, m, e, s, mask, inject_goal, o);
+    if (e.has_object)
+        hipLaunchKernelGGL(reset_kernel<1>, grid, block, 0, (hipStream_t)stream, m, e, s, mask, inject_goal, inject_obj, o);
+    else
+        hipLaunchKernelGGL(reset_kernel<0>, grid, block, 0, (hipStream_t)stream, m, e, s, mask, inject_goal, inject_obj, o);
     return (int)hipGetLastError();
 }
 

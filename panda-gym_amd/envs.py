@@ -131,7 +131,7 @@ class PandaVecEnv:
 
     def __init__(self, env_id: str = "PandaReach-v3", num_envs: int = 4096, device: Any = "cuda:0", seed: int = 0,
                  env_id_offset: int = 0, max_episode_steps: Optional[int] = None, auto_reset: bool = True,
-                 n_substeps: int = 20, model_name: str = "panda_custom0"):
+                 n_substeps: int = 20, model_name: str = "panda_custom0", contacts: bool = True):
         if torch is None:
             raise PgxError("PandaVecEnv needs torch for device buffers")
         self.lib = load()
@@ -148,7 +148,7 @@ class PandaVecEnv:
         self._params = abi.default_sim_params(n_substeps=n_substeps)
         cfg_spec = replace(self.spec, max_episode_steps=self.spec.max_episode_steps if auto_reset else 0)
         self._cfg = abi.make_config(cfg_spec, self.num_envs, self._model, self._params, seed=seed,
-                                    env_id_offset=env_id_offset)
+                                    env_id_offset=env_id_offset, contacts=contacts)
         self.obs_dim = self.lib.pgx_obs_dim(C.byref(self._cfg))
         self.action_dim = self.lib.pgx_action_dim(C.byref(self._cfg))
         h = C.c_void_p()
@@ -200,7 +200,9 @@ class PandaVecEnv:
             pass
 
     def state(self) -> Dict[str, torch.Tensor]:
-        """Device views of the SoA state (q, qd [7,N] f32; goal [3,N] f64; elapsed, episode [N])."""
+        """Device views of the SoA state (q, qd [7,N] f32; goal [3,N] f64; object [13,N] f32 =
+        pos, quat (x,y,z,w), linvel, angvel; contacts [16,N] f32 warm-start cache; elapsed,
+        episode [N])."""
         v = abi.PgxStateView()
         check(self.lib.pgx_get_state(self._h, C.byref(v)), "pgx_get_state")
         n = self.num_envs
@@ -208,6 +210,8 @@ class PandaVecEnv:
             "q": _view(v.q, (7, n), torch.float32, self.device),
             "qd": _view(v.qd, (7, n), torch.float32, self.device),
             "goal": _view(v.goal, (3, n), torch.float64, self.device),
+            "object": _view(v.object, (13, n), torch.float32, self.device),
+            "contacts": _view(v.contacts, (2 * abi.CONTACT_SLOTS, n), torch.float32, self.device),
             "elapsed": _view(v.elapsed, (n,), torch.int32, self.device),
             "episode": _view(v.episode, (n,), torch.int32, self.device),
         }
@@ -216,22 +220,29 @@ class PandaVecEnv:
         return {"observation": self.obs, "achieved_goal": self.achieved_goal, "desired_goal": self.desired_goal}
 
     def reset_tensors(self, seed: Optional[int] = None, mask: Optional[torch.Tensor] = None,
-                      goals: Optional[np.ndarray] = None) -> Dict[str, torch.Tensor]:
-        """Reset (masked) envs on device; ``seed`` reproduces the reference's PCG64 goal draws
-        for env i with seed+i (SB3 VecEnv seeding), injected into the kernel."""
-        inj = None
+                      goals: Optional[np.ndarray] = None,
+                      objects: Optional[np.ndarray] = None) -> Dict[str, torch.Tensor]:
+        """Reset (masked) envs on device; ``seed`` reproduces the reference's PCG64 goal (and
+        object) draws for env i with seed+i (SB3 VecEnv seeding), injected into the kernel."""
+        inj, inj_obj = None, None
+        if goals is None and objects is None and seed is not None:
+            draws = [seeded_reset(self.spec, seed + i) for i in range(self.num_envs)]
+            goals = np.stack([d[0] for d in draws])
+            if self.spec.task != abi.TASK_REACH:
+                objects = np.stack([d[1] for d in draws])
         if goals is not None:
             inj = torch.as_tensor(np.asarray(goals, dtype=np.float64).reshape(self.num_envs, 3), device=self.device)
-        elif seed is not None:
-            g = np.stack([seeded_goal(self.spec, seed + i) for i in range(self.num_envs)])
-            inj = torch.as_tensor(g, device=self.device)
+        if objects is not None:
+            inj_obj = torch.as_tensor(np.asarray(objects, dtype=np.float64).reshape(self.num_envs, 3),
+                                      device=self.device)
         m = None
         if mask is not None:
             m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
         check(self.lib.pgx_reset(self._h, None if m is None else C.c_void_p(m.data_ptr()),
-                                 None if inj is None else C.c_void_p(inj.data_ptr()), None, C.byref(self._out),
+                                 None if inj is None else C.c_void_p(inj.data_ptr()),
+                                 None if inj_obj is None else C.c_void_p(inj_obj.data_ptr()), C.byref(self._out),
                                  self._stream()), "pgx_reset")
-        self._keep = (m, inj)  # keep the buffers alive until the stream consumes them
+        self._keep = (m, inj, inj_obj)  # keep the buffers alive until the stream consumes them
         return self._obs_dict()
 
     def step_tensors(self, actions: torch.Tensor):
@@ -379,8 +390,11 @@ class PandaEnv:
         self._saved_elapsed: Dict[int, int] = {}
 
     def reset(self, seed: Optional[int] = None, options: Optional[dict] = None):
-        g = seeded_goal(self.spec, seed)
-        self._vec.reset_tensors(goals=None if g is None else g[None, :])
+        r = seeded_reset(self.spec, seed)
+        if r is None:
+            self._vec.reset_tensors()
+        else:
+            self._vec.reset_tensors(goals=r[0][None, :], objects=None if r[1] is None else r[1][None, :])
         self._elapsed = 0
         obs = self._vec._numpy_obs()
         obs = {k: v[0] for k, v in obs.items()}

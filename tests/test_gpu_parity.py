@@ -32,6 +32,8 @@ def _state_to_oracle(venv, ref):
     ref.goal[:] = st["goal"].cpu().numpy().T
     ref.elapsed[:] = st["elapsed"].cpu().numpy()
     ref.episode[:] = st["episode"].cpu().numpy().view(np.uint32)
+    ref.obj[:, :13] = st["object"].double().cpu().numpy().T
+    ref.obj[:, 13:29] = st["contacts"].double().cpu().numpy().T
 
 
 def _check_step(out_gpu, out_ref, goal):

@@ -75,10 +75,13 @@ def test_host_only_calls_without_gpu():
     lib = _native.load()
     cfg = abi.make_config(abi.EnvSpec(), 8, abi.make_model(load_model("panda_custom0")), abi.default_sim_params())
     assert lib.pgx_obs_dim(C.byref(cfg)) == 6 and lib.pgx_action_dim(C.byref(cfg)) == 3
-    cfg.task = abi.TASK_PUSH
+    cfg.task = 7                                                 # Slide/Flip/Stack: out of scope
     h = C.c_void_p()
     assert lib.pgx_create(C.byref(cfg), 0, C.byref(h)) < 0      # unsupported task fails loudly
     assert b"task" in lib.pgx_last_error()
+    cfg.task, cfg.contacts = abi.TASK_PUSH, 0
+    assert lib.pgx_create(C.byref(cfg), 0, C.byref(h)) < 0      # an object needs the contact solver
+    assert b"contacts" in lib.pgx_last_error()
     assert lib.pgx_step(None, None, None, None) < 0
 
 

@@ -31,7 +31,7 @@ def _motors(oracle, q):
 
 
 def _obj(pos, vel=(0, 0, 0), w=(0, 0, 0), quat=(0, 0, 0, 1)):
-    o = np.zeros(37)
+    o = np.zeros(29)
     o[0:3], o[3:7], o[7:10], o[10:13] = pos, quat, vel, w
     o[13::2] = -1.0
     return o
