@@ -335,26 +335,26 @@ __device__ __forceinline__ void ik(MPtr mp, const float* q0, V3 target, const fl
  * deepest first, rows ordered by feature id; normal rows use ERP / speculative rhs, two
  * friction rows per point along btPlaneSpace1(n) bounded by mu * normal impulse.
  * Per-env contact data lives in LDS, lane-minor (x[...][lane]): conflict-free and
- * dynamically indexable, unlike VGPRs. */
+ * dynamically indexable, unlike VGPRs.  Solver rows are float4 records with a 16-B lane
+ * stride, so each quad is one conflict-free ds_read_b128 (MI355X_MICROARCH.md, LDS). */
 constexpr int CG = 4;
+
 constexpr int CACHE_N = 2 * PGX_CONTACT_SLOTS;
 constexpr float kTableIdLimit = 32.0f;   /* robot feature ids < 32: capsule end vs table/plane */
 
 struct ContactLds {
     /* group 0: object vertices vs table / plane (normal +z) */
-    float g0r[CG][3][64];          /* contact point - object COM */
+    float4 g0q[CG][4][64];         /* [0] = contact point - object COM; [1 + dir] = (jinv, den, rhs, lambda) */
     float g0d[CG][64], g0id[CG][64];
-    float g0row[CG][3][4][64];     /* per direction: jinv, den, rhs, lambda */
     /* group 1: robot vs table / plane / object */
     float g1p[CG][3][64];          /* point on the robot */
     float g1n[CG][3][64];          /* normal, from the other body to the robot */
     float g1rb[CG][3][64];         /* object contacts: point on the object - object COM */
     float g1d[CG][64], g1id[CG][64];
     int g1j[CG][64];               /* arm joint carrying the robot link */
-    float g1J[CG][3][PGX_NJ][64];  /* robot Jacobian row per direction */
-    float g1R[CG][3][PGX_NJ][64];  /* M^-1 J^T */
-    float g1c[CG][3][6][64];       /* object part (linear, angular) of the row; 0 vs table */
-    float g1row[CG][3][4][64];
+    /* per direction: (J0..3) (J4..6, jinv) (R0..3) (R4..6, den) (cl, rhs) (ca, lambda) with
+     * J the robot Jacobian row, R = M^-1 J^T, (cl, ca) the object part (0 against the table) */
+    float4 g1q[CG][3][6][64];
     int cnt[2][64];
     float cache[CACHE_N][64];      /* (feature id, normal impulse) x 4 per group */
     float capA[PGX_NCAP][3][64], capB[PGX_NCAP][3][64];   /* capsule end points, world */
@@ -391,11 +391,11 @@ __device__ __forceinline__ void g0_insert(ContactLds& L, int ln, float d, float 
     while (pos > 0 && d < L.g0d[pos - 1][ln]) {
         L.g0d[pos][ln] = L.g0d[pos - 1][ln];
         L.g0id[pos][ln] = L.g0id[pos - 1][ln];
-        for (int k = 0; k < 3; k++) L.g0r[pos][k][ln] = L.g0r[pos - 1][k][ln];
+        L.g0q[pos][0][ln] = L.g0q[pos - 1][0][ln];
         pos--;
     }
     L.g0d[pos][ln] = d; L.g0id[pos][ln] = id;
-    L.g0r[pos][0][ln] = r.x; L.g0r[pos][1][ln] = r.y; L.g0r[pos][2][ln] = r.z;
+    L.g0q[pos][0][ln] = make_float4(r.x, r.y, r.z, 0.0f);
 }
 __device__ __forceinline__ void g1_copy(ContactLds& L, int ln, int to, int from) {
     L.g1d[to][ln] = L.g1d[from][ln];
@@ -425,7 +425,7 @@ __device__ __forceinline__ void sort_groups(ContactLds& L, int ln) {
         for (int j = i; j > 0 && L.g0id[j][ln] < L.g0id[j - 1][ln]; j--) {
             float t = L.g0id[j][ln]; L.g0id[j][ln] = L.g0id[j - 1][ln]; L.g0id[j - 1][ln] = t;
             t = L.g0d[j][ln]; L.g0d[j][ln] = L.g0d[j - 1][ln]; L.g0d[j - 1][ln] = t;
-            for (int k = 0; k < 3; k++) { t = L.g0r[j][k][ln]; L.g0r[j][k][ln] = L.g0r[j - 1][k][ln]; L.g0r[j - 1][k][ln] = t; }
+            const float4 tq = L.g0q[j][0][ln]; L.g0q[j][0][ln] = L.g0q[j - 1][0][ln]; L.g0q[j - 1][0][ln] = tq;
         }
     const int c1 = L.cnt[1][ln];
     for (int i = 1; i < c1; i++)
@@ -734,7 +734,8 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
         const float erp_dt = m.contact_erp * m.inv_dt;
         for (int k = 0; k < CG; k++) {
             if (OBJ && k < n0) {
-                const V3 r = v3(L.g0r[k][0][ln], L.g0r[k][1][ln], L.g0r[k][2][ln]);
+                const float4 r4 = L.g0q[k][0][ln];
+                const V3 r = v3(r4.x, r4.y, r4.z);
                 const float id = L.g0id[k][ln];
                 float warm = 0.0f;
 #pragma unroll
@@ -755,10 +756,7 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
                         rhs = -rel * jinv;
                     }
                     const float lam = dir == 0 ? warm : 0.0f;
-                    L.g0row[k][dir][0][ln] = jinv;
-                    L.g0row[k][dir][1][ln] = den;
-                    L.g0row[k][dir][2][ln] = rhs;
-                    L.g0row[k][dir][3][ln] = lam;
+                    L.g0q[k][1 + dir][ln] = make_float4(jinv, den, rhs, lam);
                     if (dir == 0) { dvl = dvl + (lam * inv_m) * lin; dvw = dvw + (lam * inv_i) * ang; }
                 }
             }
@@ -809,14 +807,12 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
                         rhs = -rel * jinv;
                     }
                     const float lam = dir == 0 ? warm : 0.0f;
-#pragma unroll
-                    for (int a = 0; a < NJ; a++) { L.g1J[k][dir][a][ln] = J[a]; L.g1R[k][dir][a][ln] = Rs[a]; }
-                    L.g1c[k][dir][0][ln] = cl.x; L.g1c[k][dir][1][ln] = cl.y; L.g1c[k][dir][2][ln] = cl.z;
-                    L.g1c[k][dir][3][ln] = ca.x; L.g1c[k][dir][4][ln] = ca.y; L.g1c[k][dir][5][ln] = ca.z;
-                    L.g1row[k][dir][0][ln] = jinv;
-                    L.g1row[k][dir][1][ln] = den;
-                    L.g1row[k][dir][2][ln] = rhs;
-                    L.g1row[k][dir][3][ln] = lam;
+                    L.g1q[k][dir][0][ln] = make_float4(J[0], J[1], J[2], J[3]);
+                    L.g1q[k][dir][1][ln] = make_float4(J[4], J[5], J[6], jinv);
+                    L.g1q[k][dir][2][ln] = make_float4(Rs[0], Rs[1], Rs[2], Rs[3]);
+                    L.g1q[k][dir][3][ln] = make_float4(Rs[4], Rs[5], Rs[6], den);
+                    L.g1q[k][dir][4][ln] = make_float4(cl.x, cl.y, cl.z, rhs);
+                    L.g1q[k][dir][5][ln] = make_float4(ca.x, ca.y, ca.z, lam);
                     if (dir == 0) {
 #pragma unroll
                         for (int a = 0; a < NJ; a++) dv[a] += Rs[a] * lam;
@@ -826,6 +822,16 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
             }
         }
     }
+    /* accumulated contact impulses live in VGPRs during the sweeps, so the LDS row
+     * records stay read-only and their loads can be issued ahead of the dependent math */
+    float lam0[CG][3], lam1[CG][3];
+#pragma unroll
+    for (int k = 0; k < CG; k++)
+#pragma unroll
+        for (int dir = 0; dir < 3; dir++) {
+            lam0[k][dir] = (CONT && OBJ && k < n0) ? Lp->g0q[k][1 + dir][ln].w : 0.0f;
+            lam1[k][dir] = (CONT && k < n1) ? Lp->g1q[k][dir][5][ln].w : 0.0f;
+        }
 
     /* rows (btMultiBodyJointMotor / btMultiBodyJointLimitConstraint::createConstraintRows):
      * jinv depends only on the dof, bounds are constants, so per row only rhs and
@@ -901,29 +907,33 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
     };
     /* contact rows: normal rows of both groups, then friction rows (bounds from the
      * current normal impulse, skipped while it is 0) */
+    const bool g0_any = CONT && OBJ && __any(n0 > 0);
+    const bool g1_any = CONT && __any(n1 > 0);
     auto contact_rows = [&](float& resid) {
-        ContactLds& L = *Lp;
+        const ContactLds& L = *Lp;
 #pragma unroll
         for (int fr = 0; fr < 2; fr++) {
-            if (OBJ) {
+            if (OBJ && g0_any) {   /* wave-uniform; inside, inactive points are predicated off */
+#pragma unroll
                 for (int k = 0; k < CG; k++) {
-                    if (!__any(k < n0)) break;
-                    if (k < n0) {
-                        const V3 r = v3(L.g0r[k][0][ln], L.g0r[k][1][ln], L.g0r[k][2][ln]);
-                        const float ln_n = L.g0row[k][0][3][ln];
+                    const bool act = k < n0;   /* a resting cube has 4: predicate, no branch */
+                    {
+                        const float4 r4 = L.g0q[k][0][ln];
+                        const V3 r = v3(r4.x, r4.y, r4.z);
+                        const float ln_n = lam0[k][0];
 #pragma unroll
                         for (int dir = fr ? 1 : 0; dir < (fr ? 3 : 1); dir++) {
-                            if (fr && !(ln_n > 0.0f)) continue;
                             const V3 lin = dir == 0 ? v3(0, 0, 1) : (dir == 1 ? v3(0, -1, 0) : v3(1, 0, 0));
                             const V3 ang = dir == 0 ? v3(r.y, -r.x, 0) : (dir == 1 ? v3(r.z, 0, -r.x) : v3(0, r.z, -r.y));
-                            const float jv = L.g0row[k][dir][0][ln], dn = L.g0row[k][dir][1][ln];
-                            const float rh = L.g0row[k][dir][2][ln], lm = L.g0row[k][dir][3][ln];
+                            const float4 rw = L.g0q[k][1 + dir][ln];
+                            const float jv = rw.x, dn = rw.y, rh = rw.z, lm = lam0[k][dir];
                             const float lo = fr ? -m.friction * ln_n : 0.0f;
                             const float hi = fr ? m.friction * ln_n : 1e10f;
                             float delta = rh - (dot(lin, dvl) + dot(ang, dvw)) * jv;
                             const float nl = __builtin_amdgcn_fmed3f(lm + delta, lo, hi);
-                            delta = nl - lm;
-                            L.g0row[k][dir][3][ln] = nl;
+                            /* a friction row waits for a positive normal impulse */
+                            delta = (!act || (fr && !(ln_n > 0.0f))) ? 0.0f : nl - lm;
+                            lam0[k][dir] = lm + delta;
                             dvl = dvl + (delta * inv_m) * lin;
                             dvw = dvw + (delta * inv_i) * ang;
                             resid = fmaxf(resid, fabsf(delta * dn));
@@ -931,32 +941,36 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
                     }
                 }
             }
+            if (!g1_any) continue;
+#pragma unroll
             for (int k = 0; k < CG; k++) {
-                if (!__any(k < n1)) break;
-                if (k < n1) {
-                    const float ln_n = L.g1row[k][0][3][ln];
+                const bool act = k < n1;   /* robot points are sparse: skip idle slots */
+                if (__any(act) && act) {
+                    const float ln_n = lam1[k][0];
 #pragma unroll
                     for (int dir = fr ? 1 : 0; dir < (fr ? 3 : 1); dir++) {
-                        if (fr && !(ln_n > 0.0f)) continue;
-                        const float jv = L.g1row[k][dir][0][ln], dn = L.g1row[k][dir][1][ln];
-                        const float rh = L.g1row[k][dir][2][ln], lm = L.g1row[k][dir][3][ln];
+                        const float4 q0 = L.g1q[k][dir][0][ln], q1 = L.g1q[k][dir][1][ln];
+                        const float4 q2 = L.g1q[k][dir][2][ln], q3 = L.g1q[k][dir][3][ln];
+                        const float4 q4 = L.g1q[k][dir][4][ln], q5 = L.g1q[k][dir][5][ln];
+                        const float jv = q1.w, dn = q3.w, rh = q4.w, lm = lam1[k][dir];
                         const float lo = fr ? -m.friction * ln_n : 0.0f;
                         const float hi = fr ? m.friction * ln_n : 1e10f;
-                        float jdv = 0.0f;
-#pragma unroll
-                        for (int a = 0; a < NJ; a++) jdv += L.g1J[k][dir][a][ln] * dv[a];
+                        /* two partial sums: half the dependent-FMA chain */
+                        float ja = q0.x * dv[0] + q0.z * dv[2] + q1.x * dv[4] + q1.z * dv[6];
+                        float jb = q0.y * dv[1] + q0.w * dv[3] + q1.y * dv[5];
                         V3 cl = v3(0, 0, 0), ca = v3(0, 0, 0);
                         if (OBJ) {
-                            cl = v3(L.g1c[k][dir][0][ln], L.g1c[k][dir][1][ln], L.g1c[k][dir][2][ln]);
-                            ca = v3(L.g1c[k][dir][3][ln], L.g1c[k][dir][4][ln], L.g1c[k][dir][5][ln]);
-                            jdv += dot(cl, dvl) + dot(ca, dvw);
+                            cl = v3(q4.x, q4.y, q4.z);
+                            ca = v3(q5.x, q5.y, q5.z);
+                            jb += dot(cl, dvl) + dot(ca, dvw);
                         }
+                        const float jdv = ja + jb;
                         float delta = rh - jdv * jv;
                         const float nl = __builtin_amdgcn_fmed3f(lm + delta, lo, hi);
-                        delta = nl - lm;
-                        L.g1row[k][dir][3][ln] = nl;
-#pragma unroll
-                        for (int a = 0; a < NJ; a++) dv[a] += L.g1R[k][dir][a][ln] * delta;
+                        delta = (!act || (fr && !(ln_n > 0.0f))) ? 0.0f : nl - lm;
+                        lam1[k][dir] = lm + delta;
+                        dv[0] += q2.x * delta; dv[1] += q2.y * delta; dv[2] += q2.z * delta; dv[3] += q2.w * delta;
+                        dv[4] += q3.x * delta; dv[5] += q3.y * delta; dv[6] += q3.z * delta;
                         if (OBJ) { dvl = dvl + (delta * inv_m) * cl; dvw = dvw + (delta * inv_i) * ca; }
                         resid = fmaxf(resid, fabsf(delta * dn));
                     }
@@ -1007,9 +1021,9 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
 #pragma unroll
         for (int s = 0; s < CG; s++) {
             L.cache[2 * s][ln] = s < n0 ? L.g0id[s][ln] : -1.0f;
-            L.cache[2 * s + 1][ln] = s < n0 ? L.g0row[s][0][3][ln] : 0.0f;
+            L.cache[2 * s + 1][ln] = s < n0 ? lam0[s][0] : 0.0f;
             L.cache[8 + 2 * s][ln] = s < n1 ? L.g1id[s][ln] : -1.0f;
-            L.cache[8 + 2 * s + 1][ln] = s < n1 ? L.g1row[s][0][3][ln] : 0.0f;
+            L.cache[8 + 2 * s + 1][ln] = s < n1 ? lam1[s][0] : 0.0f;
         }
     }
     if (OBJ) {
@@ -1164,8 +1178,19 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
     const int ii = i;
     ContactLds* L = nullptr;
     if constexpr (CONT) {
-        __shared__ ContactLds lds_buf;   /* ~108 KB: one wave per CU holds its envs' contact rows */
+        __shared__ ContactLds lds_buf;   /* ~126 KB: one wave per CU holds its envs' contact rows */
         L = &lds_buf;
+        /* every row slot starts finite: the sweeps run unused slots predicated off, and an
+         * inactive slot later only holds an earlier substep's (finite) row */
+#pragma unroll
+        for (int k = 0; k < CG; k++) {
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) L->g0q[k][qq][ln] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+            for (int dir = 0; dir < 3; dir++)
+#pragma unroll
+                for (int qq = 0; qq < 6; qq++) L->g1q[k][dir][qq][ln] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
     }
     const MPtr mp = fresh((uint64_t)mdev);
     MRef m = *mp;

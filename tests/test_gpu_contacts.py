@@ -1,10 +1,13 @@
 """GPU parity of the contact scene (table / plane / cube, robot capsules) against the fp64 oracle.
 
-The contact solver is a projected Gauss-Seidel truncated by the reference's own residual exit
-(squared row residual <= 1e-7), so -- as for the joint rows (test_gpu_parity.py) -- positions are
-held to the 1e-4 observation tolerance and velocities to the solver's residual quantum.  Contact
-point selection (4 deepest per group) can pick a different but equally deep point in fp32 than
-in fp64 when two candidates tie to ~1e-7; such envs are counted, and must stay rare.
+Away from contact events the step is as well conditioned as the Reach step (errors ~1e-6).  At a
+contact event the truncated projected Gauss-Seidel (50 sweeps, residual exit 1e-7) amplifies
+rounding: the fp64 oracle itself moves the EE by up to 7e-5 in one step when its input state is
+perturbed by 1e-7 relative (tools/diag_contacts.py, DESIGN.md "Contacts"), so an fp32 step cannot
+be held to 1e-4 at every contact event and a free-running contact trajectory diverges
+chaotically.  The bar is therefore set per step, from the same state: 99th percentile <= 1e-5 and
+max <= 1e-3 of the EE and object positions; plus the physical invariants the oracle tests pin
+(test_oracle_contacts.py) checked on the device.
 """
 import numpy as np
 import pytest
@@ -55,13 +58,15 @@ def test_object_reset_and_one_step_parity(pg, oracle, env_id):
     venv.close()
 
 
-def _rollout(pg, oracle, env_id, n, steps, seed, actions=None):
+def _one_step_errors(pg, oracle, env_id, n, steps, seed, actions=None):
+    """Per step, from the device state copied into the oracle: |device - oracle| of the EE
+    position (obs 0:3) and the achieved goal (EE or object position)."""
     venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=seed)
     venv.reset_tensors(seed=seed)
     ref = oracle.OracleVecEnv(venv._cfg, n)
-    _state_to_oracle(venv, ref)
-    pos_err, vel_err, obj_err = [], [], []
+    ee_err, ag_err = [], []
     for t in range(steps):
+        _state_to_oracle(venv, ref)
         a = venv.sample_actions(t).clone() if actions is None else torch.as_tensor(
             np.repeat(np.asarray(actions[t], np.float32)[None], n, 0), device="cuda:0")
         venv.step_tensors(a)
@@ -69,34 +74,36 @@ def _rollout(pg, oracle, env_id, n, steps, seed, actions=None):
         obs, ag, dg = _obs(venv)
         assert np.array_equal(venv.truncated.cpu().numpy(), out["truncated"]), t
         if out["truncated"].any():
-            _state_to_oracle(venv, ref)   # new episode: continue from the device state
             continue
-        e = np.abs(obs - out["obs"])
-        pos_err.append(e[:, :3].max(axis=1))
-        vel_err.append(e[:, 3:6].max(axis=1))
-        if obs.shape[1] > 6:
-            obj_err.append(np.abs(ag - out["ag"]).max(axis=1))
+        ee_err.append(np.abs(obs[:, :3] - out["obs"][:, :3]).max(axis=1))
+        ag_err.append(np.abs(ag - out["ag"]).max(axis=1))
+    final = {k: v.clone() for k, v in venv.state().items()}   # views die with the handle
     venv.close()
-    return np.stack(pos_err), np.stack(vel_err), (np.stack(obj_err) if obj_err else None)
+    return np.stack(ee_err), np.stack(ag_err), final
 
 
-def test_reach_with_table_contacts_trajectory(pg, oracle):
-    """Drive the EE into the table (a = -z): the tool-bar contact holds it at z ~ 0.042 on the
-    GPU exactly as in the oracle."""
+def test_reach_with_table_contacts(pg, oracle):
+    """Drive the EE into the table (a = -z): the tool-bar contact holds it at z ~ 0.042."""
     acts = [[0.3, -0.2, -1.0]] * 30
-    pos, vel, _ = _rollout(pg, oracle, "PandaReach-v3", 64, 30, 3, acts)
-    assert pos.max() <= 5 * OBS_TOL, pos.max()
-    assert np.percentile(vel, 99) <= 10 * OBS_TOL
+    ee, ag, _ = _one_step_errors(pg, oracle, "PandaReach-v3", 64, 30, 3, acts)
+    assert np.percentile(ee, 99) <= 1e-5 and ee.max() <= 1e-3, (np.percentile(ee, 99), ee.max())
+    venv = pg.PandaVecEnv("PandaReach-v3", num_envs=64, device="cuda:0", seed=3)
+    venv.reset_tensors(seed=3)
+    for a in acts:
+        venv.step_tensors(torch.tensor([a] * 64, dtype=torch.float32, device="cuda:0"))
+    z = venv.obs[:, 2].cpu().numpy()
+    assert z.min() > 0.035, z.min()
+    venv.close()
 
 
-def test_push_random_policy_trajectory(pg, oracle):
-    """Random policy for 50 steps: EE and cube positions track the oracle; the envs whose cube
-    is struck are where contact selection ties can occur."""
-    pos, vel, obj = _rollout(pg, oracle, "PandaPush-v3", 256, 50, 21)
-    assert np.percentile(pos, 99) <= OBS_TOL, np.percentile(pos, 99)
-    assert np.percentile(obj, 99) <= OBS_TOL, np.percentile(obj, 99)
-    frac_bad = float((obj.max(axis=0) > 1e-3).mean())
-    assert frac_bad <= 0.02, frac_bad
+@pytest.mark.parametrize("env_id", ["PandaPush-v3", "PandaPickAndPlaceJoints-v3"])
+def test_random_policy_one_step_parity(pg, oracle, env_id):
+    ee, ag, final = _one_step_errors(pg, oracle, env_id, 256, 50, 21)
+    for name, e in (("ee", ee), ("object", ag)):
+        assert np.percentile(e, 99) <= 1e-5, (name, np.percentile(e, 99))
+        assert e.max() <= 1e-3, (name, e.max())
+    cube = final["object"].cpu().numpy()
+    assert cube[2].min() > -0.4
 
 
 def test_scripted_push_moves_cube_like_oracle(pg, oracle):

@@ -84,9 +84,10 @@ def test_episode_trajectory_parity(pg, oracle):
     solverResidualThreshold), so each joint velocity is only defined to sqrt(1e-7) = 3.2e-4 rad/s;
     an fp32/fp64 difference in the exit sweep moves the EE velocity by up to sum_j |J_ij| * 3.2e-4
     (~1e-3 m/s for the Panda's ~0.5 m lever arms).  Bound: max 2.5e-3, 99th percentile 3e-4
-    (DESIGN.md §5)."""
+    (DESIGN.md §5).  Without the table: a free-running trajectory through contact events is
+    chaotic at fp32 rounding (test_gpu_contacts.py holds those per step)."""
     n = 256
-    venv = pg.PandaVecEnv("PandaReach-v3", num_envs=n, device="cuda:0", seed=11)
+    venv = pg.PandaVecEnv("PandaReach-v3", num_envs=n, device="cuda:0", seed=11, contacts=False)
     venv.reset_tensors()
     ref = oracle.OracleVecEnv(venv._cfg, n)
     _state_to_oracle(venv, ref)

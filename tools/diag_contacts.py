@@ -1,0 +1,52 @@
+"""GPU diagnostics for the contact scene: per-step one-step errors (oracle re-synced to the
+device state before every step) and accumulated-trajectory errors, with the contact caches of
+the worst envs.  Usage: python tools/diag_contacts.py [env_id] [n] [steps]"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import panda_gym_amd as pg  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+from test_gpu_parity import _state_to_oracle  # noqa: E402
+
+env_id = sys.argv[1] if len(sys.argv) > 1 else "PandaPush-v3"
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+steps = int(sys.argv[3]) if len(sys.argv) > 3 else 50
+O.build()
+venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=21)
+venv.reset_tensors(seed=21)
+ref = O.OracleVecEnv(venv._cfg, n)
+np.set_printoptions(precision=5, suppress=True, linewidth=200)
+worst = []
+for t in range(steps):
+    _state_to_oracle(venv, ref)
+    pre = venv.state()
+    pre_c = pre["contacts"].cpu().numpy().T.copy()
+    a = venv.sample_actions(t).clone()
+    venv.step_tensors(a)
+    out = ref.step(a.cpu().numpy())
+    if out["truncated"].any():
+        continue
+    obs = venv.obs.cpu().numpy()
+    e = np.abs(obs - out["obs"])
+    ee = e[:, :3].max(axis=1)
+    ob = e[:, 6:9].max(axis=1) if obs.shape[1] > 6 else np.zeros(n)
+    i = int(np.argmax(np.maximum(ee, ob)))
+    st = venv.state()
+    gc = st["contacts"].cpu().numpy().T
+    print(f"t={t:2d} one-step ee max {ee.max():.2e} p99 {np.percentile(ee, 99):.2e} | obj max {ob.max():.2e} "
+          f"p99 {np.percentile(ob, 99):.2e} | worst env {i}")
+    if max(ee[i], ob[i]) > 1e-4:
+        print("   gpu obs", obs[i, :12])
+        print("   ref obs", out["obs"][i, :12])
+        print("   pre contacts", pre_c[i])
+        print("   gpu contacts", gc[i])
+        print("   ref contacts", ref.obj[i, 13:29])
+    worst.append(max(ee.max(), ob.max()))
+print("max one-step error", max(worst))
