@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--kernel-launches", type=int, default=200, help="launches for the kernel-time measurement")
     ap.add_argument("--no-her", action="store_true", help="skip the HER relabel leg (BASELINE configs[3])")
     ap.add_argument("--her-calls", type=int, default=50)
+    ap.add_argument("--no-tasks", action="store_true", help="skip the Push / PickAndPlace legs (configs[2], [3])")
+    ap.add_argument("--task-steps", type=int, default=200)
     return ap.parse_args()
 
 
@@ -165,6 +167,30 @@ def her_leg(dev, calls: int, with_cpu: bool):
     return res
 
 
+def task_leg(dev, env_id: str, n: int, steps: int, contacts: bool = True):
+    """env-steps/s of one more task config on this GPU (device random policy, in-kernel
+    auto-reset), timed like the main leg: barrier-free single GPU, HIP events bracketing."""
+    import panda_gym_amd as pg
+
+    venv = pg.PandaVecEnv(env_id, num_envs=n, device=dev, seed=1, contacts=contacts)
+    venv.reset_tensors()
+    for t in range(20):
+        venv.step_tensors(venv.sample_actions(t))
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    e0.record(stream)
+    for t in range(steps):
+        venv.step_tensors(venv.sample_actions(20 + t))
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / steps
+    venv.close()
+    return {"env_id": env_id, "envs": n, "contacts": contacts, "value": n / (ms * 1e-3), "unit": "env-steps/s",
+            "ms_per_step": ms, "steps": steps,
+            "policy": "device Philox random actions (sample_actions + step per step)"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -207,14 +233,18 @@ def main():
     total = world * E * args.steps
     value = total / elapsed
 
-    # kernel time of pgx_step alone (HIP events on the launch stream = torch's current stream)
-    acts = venv.sample_actions().clone()
+    # kernel time of pgx_step alone (HIP events on the launch stream = torch's current stream),
+    # on the same random-policy workload: the actions are drawn up front
+    K = args.kernel_launches
+    acts = torch.empty((K, E, venv.action_dim), dtype=torch.float32, device=dev)
+    for k in range(K):
+        acts[k].copy_(venv.sample_actions())
     stream = torch.cuda.current_stream(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
     ev0.record(stream)
-    for _ in range(args.kernel_launches):
-        venv.step_tensors(acts)
+    for k in range(K):
+        venv.step_tensors(acts[k])
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     kernel_ms = ev0.elapsed_time(ev1) / args.kernel_launches
@@ -241,12 +271,13 @@ def main():
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: device Philox random policy U[-1,1)^3, 50-step episodes with in-kernel auto-reset",
-            "config": {"workload": f"{args.env_id} (ee control, sparse reward), {E} envs per GPU, "
-                                   f"no contacts (BASELINE configs[1])",
+            "config": {"workload": f"{args.env_id} (ee control, sparse reward), {E} envs per GPU, the "
+                                   f"reference's scene: table / plane contacts of the robot (BASELINE configs[1])",
                        "envs_per_gpu": E, "global_envs": world * E, "parallelism": f"env-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "step_kernel<0>", "kernel_ms": kernel_ms,
+                         "kernel": "step_kernel<0, 0, 1> (ee control, no object, table contacts)",
+                         "kernel_ms": kernel_ms,
                          "alg_bytes_per_launch": alg_bytes},
             "roofline_valu": valu,
             "episode_stats_last_step": {"truncated": float(stats[0]), "success": float(stats[1]),
@@ -256,6 +287,10 @@ def main():
             line["cpu_baseline"] = cpu_baseline(venv, args.cpu_baseline_seconds)
         if world == 1 and not args.no_her:
             line["her_relabel"] = her_leg(dev, args.her_calls, not args.no_cpu_baseline)
+        if world == 1 and not args.no_tasks:
+            line["tasks"] = [task_leg(dev, "PandaPush-v3", 4096, args.task_steps),               # configs[2]
+                             task_leg(dev, "PandaPickAndPlace-v3", 16384, args.task_steps),      # configs[3]
+                             task_leg(dev, args.env_id, E, args.task_steps, contacts=False)]     # no table
         print(json.dumps(line), flush=True)
     venv.close()
     if dist is not None:
