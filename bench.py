@@ -290,6 +290,7 @@ def main():
         if world == 1 and not args.no_tasks:
             line["tasks"] = [task_leg(dev, "PandaPush-v3", 4096, args.task_steps),               # configs[2]
                              task_leg(dev, "PandaPickAndPlace-v3", 16384, args.task_steps),      # configs[3]
+                             task_leg(dev, "PandaReachAO-v3", 8192, args.task_steps),            # configs[4] / GPU
                              task_leg(dev, args.env_id, E, args.task_steps, contacts=False)]     # no table
         print(json.dumps(line), flush=True)
     venv.close()

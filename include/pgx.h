@@ -63,12 +63,19 @@ extern "C" {
 #define PGX_TASK_REACH 0
 #define PGX_TASK_PUSH 1
 #define PGX_TASK_PICK_AND_PLACE 2
+#define PGX_TASK_REACH_AO 3        /* ReachAO, scenario "reachao_rand" (reach_ao.py:587-599) */
+
+/* ReachAO "reachao_rand" scene (reach_ao.py:268-290, 573-599, 819-860): 3 spheres of
+ * radius 0.05 and 3 cuboids of half extent 0.05, 4-5 of them active per episode. */
+#define PGX_AO_OBSTACLES 6
+#define PGX_AO_LINKS 9             /* collision links: panda_link1..8, panda_ee */
 
 #define PGX_CONTROL_EE 0
 #define PGX_CONTROL_JOINTS 1
 
 #define PGX_REWARD_SPARSE 0
 #define PGX_REWARD_DENSE 1
+#define PGX_REWARD_SPARSE_AO 2   /* ReachAO relabel reward: -1 + (d < thr) (reach_ao.py:1320), collision term 0 */
 
 /* solver row kinds (pgx_model.row_kind) */
 #define PGX_ROW_MOTOR 0
@@ -178,6 +185,10 @@ typedef struct pgx_config {
     double table_center[3];       /* (-0.3, 0, -0.2) */
     double table_half[3];         /* (0.55, 0.35, 0.2) */
     double plane_z;               /* top of the plane box: -0.4 */
+    /* ReachAO (TrainConfig defaults, classes/train_config.py:24-35) */
+    int32_t terminate_on_success; /* RobotTaskEnv(terminate_on_success): 1 for ReachAO */
+    int32_t pad3;
+    double collision_reward;      /* -100: added to the sparse reward on collision */
 } pgx_config;
 
 typedef struct pgx_env* pgx_handle;
@@ -208,6 +219,7 @@ typedef struct pgx_state_view {
     double* goal;       /* [3][N] */
     float* object;      /* [13][N] pos3, quat4 (x,y,z,w), linvel3, angvel3 */
     float* contacts;    /* [2*PGX_CONTACT_SLOTS][N] warm-start cache: (id, normal impulse) per slot */
+    float* obstacles;   /* [4*PGX_AO_OBSTACLES][N] ReachAO obstacle centres (x,y,z) then active flags */
     int32_t* elapsed;   /* [N] steps in the current episode */
     uint32_t* episode;  /* [N] episodes finished (RNG counter) */
 } pgx_state_view;
@@ -223,7 +235,9 @@ int pgx_get_state(pgx_handle h, pgx_state_view* out);
 
 /* Reset envs whose mask byte is non-zero (mask NULL = all).  inject_goal
  * [N,3] f64 (host-computed PCG64 draws for seeded resets) and inject_object
- * [N,3] f64 override the device draws where given.  Writes the reset obs. */
+ * [N,3] f64 (Push/PickAndPlace object position) or [N,PGX_AO_OBSTACLES,3] f64 (ReachAO
+ * obstacle centres, parked ones at (99.9, 99.9, -99.9)) override the device draws
+ * where given.  Writes the reset obs. */
 int pgx_reset(pgx_handle h, const uint8_t* env_mask, const double* inject_goal,
               const double* inject_object, pgx_step_out* out, void* stream);
 

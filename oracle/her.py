@@ -78,6 +78,8 @@ def distance_f32(a: np.ndarray, b: np.ndarray) -> np.ndarray:
 def compute_reward_f32(ag, dg, reward_type: int, thr: float = 0.05) -> np.ndarray:
     """Reach.compute_reward (reach.py:84-89) on float32 batches."""
     d = distance_f32(ag, dg)
+    if reward_type == 2:   # ReachAO sparse, reach_ao.py:1320 (collision term 0)
+        return -1 + np.array(d < np.float32(thr), dtype=np.float32)
     if reward_type == 0:
         return -np.array(d > thr, dtype=np.float32)
     return -d.astype(np.float32)

@@ -328,7 +328,9 @@ static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x >
  * I w (k + k|w|), the base bias term m (w x v) (computeAccelerations...MultiDof:
  * "zeroAccSpatFrc[0].addLinear(m_baseMass * omega.cross(vel))"), gyroscopic w x I w
  * (zero for a cube); orientation by the exponential map (stepPositionsMultiDof). */
-#define OBJ_N 29              /* pos3 quat4 (x,y,z,w) linvel3 angvel3 + 8 x (id, impulse) */
+#define OBJ_N 53              /* pos3 quat4 (x,y,z,w) linvel3 angvel3 + 8 x (id, impulse)
+                                 + ReachAO obstacles: centres 6 x 3, active flags 6 */
+#define OBJ_AO 29
 static void quat_mul(const double* a, const double* b, double* o);
 #define NC_MAX PGX_CONTACT_SLOTS
 
@@ -402,6 +404,7 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
     }
     for (int ci = 0; ci < m->n_capsules; ci++) {
         int li = m->cap_link[ci];
+        if (m->cap_flags[ci] == 0) continue;   /* base / panda_link1: no contacts */
         double A[3], B[3];
         m3_v(k->R[li], m->cap_a[ci], A);
         m3_v(k->R[li], m->cap_b[ci], B);
@@ -727,7 +730,7 @@ void pgxo_substep(const pgx_model* m, const pgx_sim_params* p, const double base
 
 static void world_of(const pgx_config* c, world_t* W) {
     W->contacts = c->contacts;
-    W->has_object = c->task != PGX_TASK_REACH;
+    W->has_object = c->task == PGX_TASK_PUSH || c->task == PGX_TASK_PICK_AND_PLACE;
     W->half = c->object_half;
     W->mass = c->object_mass;
     W->inertia = c->object_inertia;
@@ -875,7 +878,8 @@ void pgxo_compute_reward_f32(const float* ag, const float* dg, int64_t n, int re
     for (int64_t i = 0; i < n; i++) {
         float d = pgxo_distance_f32_f32(ag + 3 * i, dg + 3 * i);
         /* numpy compares a float32 array with a Python float in float32 */
-        if (reward_type == PGX_REWARD_SPARSE) out[i] = -(d > (float)thr ? 1.0f : 0.0f);
+        if (reward_type == PGX_REWARD_SPARSE_AO) out[i] = -1.0f + (d < (float)thr ? 1.0f : 0.0f);
+        else if (reward_type == PGX_REWARD_SPARSE) out[i] = -(d > (float)thr ? 1.0f : 0.0f);
         else out[i] = -d;
     }
 }
@@ -927,6 +931,7 @@ void pgxo_sample_actions(const pgx_config* c, int64_t n, uint64_t step, float* a
 
 /* --------------------------------------------------------- env semantics */
 static int obs_dim(const pgx_config* c) {
+    if (c->task == PGX_TASK_REACH_AO) return 20 + 4 * PGX_AO_LINKS;   /* obs_type ("ee","js") + 36 */
     int robot = 6 + (c->block_gripper ? 0 : 1);
     int task = (c->task == PGX_TASK_REACH) ? 0 : 12;
     return robot + task;
@@ -948,8 +953,15 @@ static void quat_to_euler(const double* q, double* rpy) {
 /* RobotTaskEnv._get_obs (core.py:286-296): robot obs (panda.py:264-288) + task obs
  * (push.py:49-63 / pick_and_place.py:52-59: object position, euler, velocity, angular
  * velocity); achieved goal = EE position (Reach) or object position (Push/PnP). */
+static void ao_obs(const pgx_config* c, const double* q, const double* qd, const double* goal, const double* obst,
+                   float* obs, float* ag, float* dg);
+static void ao_reset_one(const pgx_config* c, int64_t e, const double* inject_goal, const double* inject_obst,
+                         double* q, double* qd, double* goal, double* obj, int32_t* elapsed, uint32_t* episode);
+static int ao_collided(const pgx_config* c, const double* q, const double* obst);
+
 static void env_obs(const pgx_config* c, const double* q, const double* qd, const double* goal, const double* obj,
                     float* obs, float* ag, float* dg) {
+    if (c->task == PGX_TASK_REACH_AO) { ao_obs(c, q, qd, goal, obj + OBJ_AO, obs, ag, dg); return; }
     const pgx_model* m = c->model;
     kin_t k;
     fk(m, c->base_pos, q, &k);
@@ -980,6 +992,10 @@ static void env_obs(const pgx_config* c, const double* q, const double* qd, cons
  * with identity orientation; its velocity is kept (resetBasePositionAndOrientation). */
 static void reset_one(const pgx_config* c, int64_t e, const double* inject_goal, const double* inject_obj, double* q,
                       double* qd, double* goal, double* obj, int32_t* elapsed, uint32_t* episode) {
+    if (c->task == PGX_TASK_REACH_AO) {
+        ao_reset_one(c, e, inject_goal, inject_obj, q, qd, goal, obj, elapsed, episode);
+        return;
+    }
     int nd = c->model->n_dofs;
     for (int d = 0; d < nd; d++) { q[d] = c->neutral_q[d]; qd[d] = 0.0; }
     uint64_t env = c->env_id_offset + (uint64_t)e;
@@ -1012,13 +1028,323 @@ int pgxo_vec_reset(const pgx_config* c, int64_t n, const uint8_t* mask, const do
     for (int64_t e = 0; e < n; e++) {
         if (mask && !mask[e]) continue;
         double* oe = obj ? obj + OBJ_N * e : NULL;
-        reset_one(c, e, inject_goal ? inject_goal + 3 * e : NULL, inject_obj ? inject_obj + 3 * e : NULL, q + nd * e,
+        const int io = c->task == PGX_TASK_REACH_AO ? 3 * PGX_AO_OBSTACLES : 3;
+        reset_one(c, e, inject_goal ? inject_goal + 3 * e : NULL, inject_obj ? inject_obj + io * e : NULL, q + nd * e,
                   qd + nd * e, goal + 3 * e, oe, elapsed + e, episode + e);
         env_obs(c, q + nd * e, qd + nd * e, goal + 3 * e, oe, obs ? obs + od * e : NULL, ag ? ag + 3 * e : NULL,
                 dg ? dg + 3 * e : NULL);
     }
     return PGX_OK;
 }
+
+/* ======================================================== ReachAO ("reachao_rand")
+ * reach_ao.py with TrainConfig defaults (classes/train_config.py): joint control,
+ * obs_type ("ee","js"), task obs "vectors+closest_per_link", truncate on collision,
+ * terminate on success, sparse reward with collision_reward -100, 20 substeps with a
+ * collision check after each (step_check_collision :182-188).  Distances restate
+ * pyb_utils' CollisionDetector (a fork, absent here) on the capsule geometry
+ * (Model.capsules, the URDF's cylinder+sphere unions) against sphere / box
+ * obstacles: signed distances (negative when penetrating), closest point pairs. */
+static const int kAoKind[PGX_AO_OBSTACLES] = {0, 0, 0, 1, 1, 1};   /* 3 spheres, then 3 cuboids */
+#define AO_SIZE 0.05          /* sphere radius / cuboid half extent (create_scenario_reachao3/_rand) */
+#define AO_DUMMY_R 0.05       /* the goal's dummy sphere (reach_ao.py:281-287) */
+#define AO_MARGIN 0.001       /* btBoxShape collision margin of createCollisionShape boxes: the
+                                 box is its inner box (h - m) swept by a sphere of radius m */
+#define AO_PI 3.14159265358979323846
+static const int kAoLinks[PGX_AO_LINKS] = {0, 1, 2, 3, 4, 5, 6, 7, 9};  /* link1..8, panda_ee */
+
+typedef struct { double d, pa[3], pb[3]; } cdist_t;
+
+/* signed distance of P to the axis-aligned box (c, h): negative inside */
+static double box_sd(const double* P, const double* c, const double* h) {
+    double o = 0.0, in = -1e300;
+    for (int i = 0; i < 3; i++) {
+        double di = fabs(P[i] - c[i]) - h[i];
+        if (di > 0) o += di * di;
+        if (di > in) in = di;
+    }
+    return sqrt(o) + (in < 0 ? in : 0.0);
+}
+
+static cdist_t capsule_sphere(const double* A, const double* B, double r, const double* C, double R) {
+    double ab[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]}, l2 = v3_dot(ab, ab), t = 0.0, P[3], v[3];
+    if (l2 > 0) t = clampd(((C[0] - A[0]) * ab[0] + (C[1] - A[1]) * ab[1] + (C[2] - A[2]) * ab[2]) / l2, 0.0, 1.0);
+    for (int i = 0; i < 3; i++) { P[i] = A[i] + t * ab[i]; v[i] = C[i] - P[i]; }
+    double len = v3_norm(v), n[3] = {0, 0, 1};
+    if (len > 0) for (int i = 0; i < 3; i++) n[i] = v[i] / len;
+    cdist_t o;
+    o.d = len - r - R;
+    for (int i = 0; i < 3; i++) { o.pa[i] = P[i] + r * n[i]; o.pb[i] = C[i] - R * n[i]; }
+    return o;
+}
+
+/* signed distance to the rounded box (c, h) with margin AO_MARGIN */
+static double rbox_sd(const double* P, const double* c, const double* h) {
+    const double hi[3] = {h[0] - AO_MARGIN, h[1] - AO_MARGIN, h[2] - AO_MARGIN};
+    return box_sd(P, c, hi) - AO_MARGIN;
+}
+
+/* capsule vs rounded axis-aligned box: the signed distance to the inner box is convex
+ * along the segment, minimised by 40 ternary-search steps ((2/3)^40 ~ 1e-7 of the
+ * segment); the margin and the capsule radius are then subtracted */
+static cdist_t capsule_box(const double* A, const double* B, double r, const double* c, const double* hfull) {
+    const double h[3] = {hfull[0] - AO_MARGIN, hfull[1] - AO_MARGIN, hfull[2] - AO_MARGIN};
+    double ab[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]}, lo = 0.0, hi = 1.0, P[3];
+    if (v3_dot(ab, ab) > 0) {
+        for (int it = 0; it < 40; it++) {
+            double m1 = lo + (hi - lo) / 3.0, m2 = hi - (hi - lo) / 3.0, P1[3], P2[3];
+            for (int i = 0; i < 3; i++) { P1[i] = A[i] + m1 * ab[i]; P2[i] = A[i] + m2 * ab[i]; }
+            if (box_sd(P1, c, h) <= box_sd(P2, c, h)) hi = m2;
+            else lo = m1;
+        }
+    }
+    double t = 0.5 * (lo + hi);
+    if (!(v3_dot(ab, ab) > 0)) t = 0.0;
+    for (int i = 0; i < 3; i++) P[i] = A[i] + t * ab[i];
+    double sd = box_sd(P, c, h), q[3], n[3];
+    if (sd > 0) {
+        for (int i = 0; i < 3; i++) q[i] = clampd(P[i], c[i] - h[i], c[i] + h[i]);
+        double v[3] = {q[0] - P[0], q[1] - P[1], q[2] - P[2]}, len = v3_norm(v);
+        for (int i = 0; i < 3; i++) n[i] = len > 0 ? v[i] / len : 0.0;
+    } else { /* inside: through the nearest face */
+        int ax = 0;
+        double best = -1e300;
+        for (int i = 0; i < 3; i++) {
+            double di = fabs(P[i] - c[i]) - h[i];
+            if (di > best) { best = di; ax = i; }
+        }
+        memcpy(q, P, sizeof q);
+        double sg = P[ax] < c[ax] ? -1.0 : 1.0;
+        q[ax] = c[ax] + sg * h[ax];
+        n[0] = n[1] = n[2] = 0.0;
+        n[ax] = -sg;   /* from the capsule axis towards the box interior */
+    }
+    cdist_t o;
+    o.d = sd - AO_MARGIN - r;
+    for (int i = 0; i < 3; i++) { o.pa[i] = P[i] + r * n[i]; o.pb[i] = q[i] - AO_MARGIN * n[i]; }
+    return o;
+}
+
+static void capsule_world(const pgx_model* m, const kin_t* k, const double* base, int ci, double* A, double* B) {
+    int li = m->cap_link[ci];
+    if (li < 0) {
+        for (int i = 0; i < 3; i++) { A[i] = base[i] + m->cap_a[ci][i]; B[i] = base[i] + m->cap_b[ci][i]; }
+        return;
+    }
+    m3_v(k->R[li], m->cap_a[ci], A);
+    m3_v(k->R[li], m->cap_b[ci], B);
+    for (int i = 0; i < 3; i++) { A[i] += k->o[li][i]; B[i] += k->o[li][i]; }
+}
+
+static cdist_t capsule_obstacle(const double* A, const double* B, double r, int kind, const double* C) {
+    if (kind == 0) return capsule_sphere(A, B, r, C, AO_SIZE);
+    const double h[3] = {AO_SIZE, AO_SIZE, AO_SIZE};
+    return capsule_box(A, B, r, C, h);
+}
+
+static void table_box(const pgx_config* c, double* tc, double* th) {
+    for (int i = 0; i < 3; i++) { tc[i] = c->table_center[i]; th[i] = c->table_half[i]; }
+}
+
+/* CollisionDetector.compute_distances_per_link: per collision link, the closest obstacle
+ * (distance, point pair); returns the table distance of links 2..ee (check_collided) */
+static double ao_link_distances(const pgx_config* c, const kin_t* k, const double* obst, double* dist,
+                                double (*pa)[3], double (*pb)[3]) {
+    const pgx_model* m = c->model;
+    double tc[3], th[3], dtable = 1e300;
+    table_box(c, tc, th);
+    for (int l = 0; l < PGX_AO_LINKS; l++) {
+        dist[l] = 1e300;
+        for (int ci = 0; ci < m->n_capsules; ci++) {
+            if (m->cap_link[ci] != kAoLinks[l]) continue;
+            double A[3], B[3];
+            capsule_world(m, k, c->base_pos, ci, A, B);
+            for (int o = 0; o < PGX_AO_OBSTACLES; o++) {
+                cdist_t cd = capsule_obstacle(A, B, m->cap_radius[ci], kAoKind[o], obst + 3 * o);
+                if (cd.d < dist[l]) {
+                    dist[l] = cd.d;
+                    memcpy(pa[l], cd.pa, sizeof cd.pa);
+                    memcpy(pb[l], cd.pb, sizeof cd.pb);
+                }
+            }
+            if (kAoLinks[l] >= 1) {   /* get_link_object_distance(table, ignore link0, link1) */
+                cdist_t ct = capsule_box(A, B, m->cap_radius[ci], tc, th);
+                if (ct.d < dtable) dtable = ct.d;
+            }
+        }
+    }
+    return dtable;
+}
+
+/* check_collided (reach_ao.py:896-900) */
+static int ao_collided(const pgx_config* c, const double* q, const double* obst) {
+    kin_t k;
+    fk(c->model, c->base_pos, q, &k);
+    double dist[PGX_AO_LINKS], pa[PGX_AO_LINKS][3], pb[PGX_AO_LINKS][3];
+    double dt = ao_link_distances(c, &k, obst, dist, pa, pb);
+    double mn = dist[0];
+    for (int l = 1; l < PGX_AO_LINKS; l++) if (dist[l] < mn) mn = dist[l];
+    return mn <= 0.0 || dt <= 0.0;
+}
+
+/* whole-robot (every capsule incl. base and hand) distance to a sphere (kind 0) / box (1) */
+static double ao_robot_distance(const pgx_config* c, const kin_t* k, int kind, const double* C, double size) {
+    const pgx_model* m = c->model;
+    double best = 1e300;
+    for (int ci = 0; ci < m->n_capsules; ci++) {
+        double A[3], B[3];
+        capsule_world(m, k, c->base_pos, ci, A, B);
+        cdist_t cd;
+        if (kind == 0) cd = capsule_sphere(A, B, m->cap_radius[ci], C, size);
+        else {
+            const double h[3] = {size, size, size};
+            cd = capsule_box(A, B, m->cap_radius[ci], C, h);
+        }
+        if (cd.d < best) best = cd.d;
+    }
+    return best;
+}
+
+/* sample_within_hollow_sphere (reach_ao.py:1188-1211): phi, theta, r = cbrt(U(rmin^3, rmax^3)) */
+typedef struct { const pgx_config* c; uint64_t env; uint32_t episode; int k; } draw_t;
+static double ao_draw(draw_t* d) { return reset_uniform(d->c, d->env, d->episode, d->k++); }
+static double ao_uniform(draw_t* d, double lo, double hi) { return lo + (hi - lo) * ao_draw(d); }
+static void hollow_sphere(draw_t* d, double rmin, double rmax, int upper_half_only, double* out) {
+    double phi = ao_uniform(d, 0.0, 2.0 * AO_PI);
+    double theta = upper_half_only ? ao_uniform(d, 0.0, 0.5 * AO_PI) : ao_uniform(d, 0.0, AO_PI);
+    double r = cbrt(ao_uniform(d, pow(rmin, 3.0), pow(rmax, 3.0)));   /* Python's radius ** 3 */
+    out[0] = r * sin(theta) * cos(phi);
+    out[1] = r * sin(theta) * sin(phi);
+    out[2] = r * cos(theta);
+}
+
+/* ReachAO.reset for "reachao_rand" (reach_ao.py:965-1033): collision-free goal
+ * (set_coll_free_goal(["table","robot"]), margin 0.1), collision-free obstacles
+ * (set_coll_free_obs(0.03), sample_obstacle_experimental), then 4 or 5 active obstacles
+ * (set_random_num_obs: integers(4, 6), shuffle, the first ones moved to (99.9,99.9,-99.9)).
+ * Device-stream draws (the host reproduces the numpy stream for seeded resets). */
+static void ao_reset_task(const pgx_config* c, int64_t e, uint32_t episode, const double* q, double* goal,
+                          double* obst, double* active) {
+    draw_t d = {c, c->env_id_offset + (uint64_t)e, episode, 0};
+    kin_t k;
+    fk(c->model, c->base_pos, q, &k);
+    double tc[3], th[3];
+    table_box(c, tc, th);
+    const double* ee = k.p[c->model->ee_link];
+    double dummy[3];   /* the dummy sphere stays at the last tested sample */
+    for (int i = 0;; i++) {
+        hollow_sphere(&d, 0.5, 0.8, 1, goal);
+        if (i > 9999) { memcpy(goal, ee, 3 * sizeof(double)); break; }   /* the 10001st draw is discarded */
+        memcpy(dummy, goal, sizeof dummy);
+        int coll = rbox_sd(goal, tc, th) - AO_DUMMY_R <= 0.1 ||
+                   ao_robot_distance(c, &k, 0, goal, AO_DUMMY_R) <= 0.1;
+        if (!coll) break;
+    }
+    for (int o = 0; o < PGX_AO_OBSTACLES; o++) {
+        double* P = obst + 3 * o;
+        for (int it = 0; it < 10000; it++) {
+            double rnd = ao_draw(&d), s[3];
+            hollow_sphere(&d, 0.1, 0.5, 0, s);
+            const double* ctr = rnd > 0.5 ? goal : ee;
+            for (int j = 0; j < 3; j++) P[j] = s[j] + ctr[j];
+            double dtab, ddum;
+            if (kAoKind[o] == 0) {
+                dtab = rbox_sd(P, tc, th) - AO_SIZE;
+                double v[3] = {P[0] - dummy[0], P[1] - dummy[1], P[2] - dummy[2]};
+                ddum = v3_norm(v) - AO_SIZE - AO_DUMMY_R;
+            } else {
+                /* rounded box vs rounded box: inner AABBs' gap minus both margins */
+                double hs[3] = {th[0] + AO_SIZE - 2 * AO_MARGIN, th[1] + AO_SIZE - 2 * AO_MARGIN,
+                                th[2] + AO_SIZE - 2 * AO_MARGIN};
+                const double h[3] = {AO_SIZE, AO_SIZE, AO_SIZE};
+                dtab = box_sd(P, tc, hs) - 2 * AO_MARGIN;
+                ddum = rbox_sd(dummy, P, h) - AO_DUMMY_R;
+            }
+            int coll = ao_robot_distance(c, &k, kAoKind[o], P, AO_SIZE) <= 0.03 || dtab <= 0.03 || ddum <= 0.03;
+            if (!coll) break;
+        }
+        active[o] = 1.0;
+    }
+    int n_active = 4 + (int)(ao_draw(&d) * 2.0);           /* integers(4, 6) */
+    int perm[PGX_AO_OBSTACLES];
+    for (int o = 0; o < PGX_AO_OBSTACLES; o++) perm[o] = o;
+    for (int j = PGX_AO_OBSTACLES - 1; j > 0; j--) {        /* Fisher-Yates */
+        int r = (int)(ao_draw(&d) * (double)(j + 1));
+        if (r > j) r = j;
+        int t = perm[j]; perm[j] = perm[r]; perm[r] = t;
+    }
+    for (int j = 0; j < PGX_AO_OBSTACLES - n_active; j++) {
+        double* P = obst + 3 * perm[j];
+        P[0] = 99.9; P[1] = 99.9; P[2] = -99.9;
+        active[perm[j]] = 0.0;
+    }
+}
+
+/* robot obs (ee pos, ee vel, q, qd) + closest distance per link (9) + unit vectors (27) */
+static void ao_obs(const pgx_config* c, const double* q, const double* qd, const double* goal, const double* obst,
+                   float* obs, float* ag, float* dg) {
+    const pgx_model* m = c->model;
+    kin_t k;
+    fk(m, c->base_pos, q, &k);
+    double v[3], w[3];
+    link_vel(m, &k, qd, m->ee_link, v, w);
+    float o[64];
+    int n = 0;
+    for (int i = 0; i < 3; i++) o[n++] = (float)k.p[m->ee_link][i];
+    for (int i = 0; i < 3; i++) o[n++] = (float)v[i];
+    for (int i = 0; i < 7; i++) o[n++] = (float)q[i];
+    for (int i = 0; i < 7; i++) o[n++] = (float)qd[i];
+    double dist[PGX_AO_LINKS], pa[PGX_AO_LINKS][3], pb[PGX_AO_LINKS][3];
+    ao_link_distances(c, &k, obst, dist, pa, pb);
+    for (int l = 0; l < PGX_AO_LINKS; l++) o[n++] = (float)dist[l];
+    for (int l = 0; l < PGX_AO_LINKS; l++) {   /* utils.unit_vector(point on link, point on obstacle) */
+        double u[3] = {pb[l][0] - pa[l][0], pb[l][1] - pa[l][1], pb[l][2] - pa[l][2]}, len = v3_norm(u);
+        for (int i = 0; i < 3; i++) o[n++] = (float)(len > 0 ? u[i] / len : 0.0);
+    }
+    if (obs) memcpy(obs, o, sizeof(float) * n);
+    if (ag) for (int i = 0; i < 3; i++) ag[i] = (float)k.p[m->ee_link][i];
+    if (dg) for (int i = 0; i < 3; i++) dg[i] = (float)goal[i];
+}
+
+static void ao_reset_one(const pgx_config* c, int64_t e, const double* inject_goal, const double* inject_obst,
+                         double* q, double* qd, double* goal, double* obj, int32_t* elapsed, uint32_t* episode) {
+    int nd = c->model->n_dofs;
+    for (int d = 0; d < nd; d++) { q[d] = c->neutral_q[d]; qd[d] = 0.0; }
+    double* obst = obj + OBJ_AO;
+    double* active = obj + OBJ_AO + 3 * PGX_AO_OBSTACLES;
+    ao_reset_task(c, e, *episode, q, goal, obst, active);
+    if (inject_goal) memcpy(goal, inject_goal, 3 * sizeof(double));
+    if (inject_obst)
+        for (int o = 0; o < PGX_AO_OBSTACLES; o++) {
+            memcpy(obst + 3 * o, inject_obst + 3 * o, 3 * sizeof(double));
+            active[o] = inject_obst[3 * o] < 50.0 ? 1.0 : 0.0;
+        }
+    for (int s = 0; s < 8; s++) { obj[13 + 2 * s] = -1.0; obj[13 + 2 * s + 1] = 0.0; }
+    *elapsed = 0;
+    *episode += 1;
+}
+
+double pgxo_ao_capsule_sphere(const double* A, const double* B, double r, const double* C, double R, double* pa,
+                              double* pb) {
+    cdist_t o = capsule_sphere(A, B, r, C, R);
+    memcpy(pa, o.pa, sizeof o.pa);
+    memcpy(pb, o.pb, sizeof o.pb);
+    return o.d;
+}
+double pgxo_ao_capsule_box(const double* A, const double* B, double r, const double* c, const double* h, double* pa,
+                           double* pb) {
+    cdist_t o = capsule_box(A, B, r, c, h);
+    memcpy(pa, o.pa, sizeof o.pa);
+    memcpy(pb, o.pb, sizeof o.pb);
+    return o.d;
+}
+double pgxo_ao_link_distances(const pgx_config* c, const double* q, const double* obst, double* dist, double* pa,
+                              double* pb) {
+    kin_t k;
+    fk(c->model, c->base_pos, q, &k);
+    return ao_link_distances(c, &k, obst, dist, (double(*)[3])pa, (double(*)[3])pb);
+}
+int pgxo_ao_collided(const pgx_config* c, const double* q, const double* obst) { return ao_collided(c, q, obst); }
 
 /* RobotTaskEnv.step (core.py:352-368) for one env + TimeLimit + VecEnv auto-reset */
 int pgxo_vec_step(const pgx_config* c, int64_t n, double* q, double* qd, double* goal, double* obj, int32_t* elapsed,
@@ -1063,16 +1389,30 @@ int pgxo_vec_step(const pgx_config* c, int64_t n, double* q, double* qd, double*
             mot[d].kd = p->motor_kd;
             mot[d].max_impulse = c->joint_forces[d] * p->dt;
         }
-        for (int s = 0; s < p->n_substeps; s++) pgxo_world_substep(c, qe, qde, oe, mot, NULL);
+        const int ao = c->task == PGX_TASK_REACH_AO;
+        int collided = 0;
+        for (int s = 0; s < p->n_substeps; s++) {
+            pgxo_world_substep(c, qe, qde, oe, mot, NULL);
+            /* ReachAO step_check_collision (reach_ao.py:182-188) */
+            if (ao && ao_collided(c, qe, oe + OBJ_AO)) { collided = 1; break; }
+        }
 
-        float o[32], agv[3], dgv[3];
+        float o[64], agv[3], dgv[3];
         env_obs(c, qe, qde, ge, oe, o, agv, dgv);
         double d = pgxo_distance_f32_f64(agv, ge);
         uint8_t succ = d < c->distance_threshold;
-        float rew = (c->reward == PGX_REWARD_SPARSE) ? -(d > c->distance_threshold ? 1.0f : 0.0f) : -(float)d;
+        float rew;
+        if (ao) {
+            /* ReachAO.compute_reward "sparse"/"reach" + collision_reward (reach_ao.py:1317-1377) */
+            rew = -1.0f + ((d + (double)collided) < c->distance_threshold ? 1.0f : 0.0f);
+            rew += (float)(collided * c->collision_reward);
+        } else {
+            rew = (c->reward == PGX_REWARD_SPARSE) ? -(d > c->distance_threshold ? 1.0f : 0.0f) : -(float)d;
+        }
         elapsed[e] += 1;
-        uint8_t trunc = (c->max_episode_steps > 0 && elapsed[e] >= c->max_episode_steps);
-        uint8_t term = 0; /* terminate_on_success=False for Reach/Push/PnP (core.py:265) */
+        uint8_t trunc = (c->max_episode_steps > 0 && elapsed[e] >= c->max_episode_steps) || collided;
+        /* terminate_on_success (core.py:359-361): False for Reach/Push/PnP, True in ReachAO's config */
+        uint8_t term = c->terminate_on_success ? succ : 0;
         if (reward) reward[e] = rew;
         if (success) success[e] = succ;
         if (terminated) terminated[e] = term;

@@ -49,7 +49,18 @@ void pgxo_substep(const pgx_model* m, const pgx_sim_params* p, const double base
  * quat4 (x,y,z,w), linvel3, angvel3, contact cache 8 x (feature id, normal impulse). */
 void pgxo_world_substep(const pgx_config* cfg, double* q, double* qd, double* obj,
                         const pgxo_motor* motors, pgxo_stats* st);
-#define PGXO_OBJ_N 29
+#define PGXO_OBJ_N 53   /* object (29) + ReachAO obstacle centres [6][3] and active flags [6] */
+
+/* ReachAO geometry (test helpers): capsule (A, B, r) vs sphere (C, R) / rounded box
+ * (c, h); per-link closest obstacle of the 9 collision links at q, returning the
+ * table distance of links 2..ee; whole-robot collision predicate. */
+double pgxo_ao_capsule_sphere(const double* A, const double* B, double r, const double* C, double R, double* pa,
+                              double* pb);
+double pgxo_ao_capsule_box(const double* A, const double* B, double r, const double* c, const double* h, double* pa,
+                           double* pb);
+double pgxo_ao_link_distances(const pgx_config* cfg, const double* q, const double* obst, double* dist, double* pa,
+                              double* pb);
+int pgxo_ao_collided(const pgx_config* cfg, const double* q, const double* obst);
 
 /* reward / success, reference utils.distance + Reach.is_success / compute_reward */
 double pgxo_distance_f32_f64(const float ag[3], const double g[3]);

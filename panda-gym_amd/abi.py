@@ -20,9 +20,11 @@ MAX_CAPSULES = 16
 CONTACT_SLOTS = 8
 CAP_VS_TABLE, CAP_VS_OBJECT = 1, 2
 
-TASK_REACH, TASK_PUSH, TASK_PICK_AND_PLACE = 0, 1, 2
+TASK_REACH, TASK_PUSH, TASK_PICK_AND_PLACE, TASK_REACH_AO = 0, 1, 2, 3
+AO_OBSTACLES, AO_LINKS = 6, 9
 CONTROL_EE, CONTROL_JOINTS = 0, 1
-REWARD_SPARSE, REWARD_DENSE = 0, 1
+REWARD_SPARSE, REWARD_DENSE, REWARD_SPARSE_AO = 0, 1, 2
+REWARD_CODES = {"sparse": REWARD_SPARSE, "dense": REWARD_DENSE, "sparse_ao": REWARD_SPARSE_AO}
 
 FLAG_CONSTRAINT_PASS_BIAS = 1
 FLAG_IK_COM = 2
@@ -79,6 +81,7 @@ class PgxConfig(C.Structure):
         ("obj_low", C.c_double * 3), ("obj_high", C.c_double * 3), ("obj_offset", C.c_double * 3),
         ("object_half", C.c_double), ("object_mass", C.c_double), ("object_inertia", C.c_double),
         ("table_center", C.c_double * 3), ("table_half", C.c_double * 3), ("plane_z", C.c_double),
+        ("terminate_on_success", C.c_int32), ("pad3", C.c_int32), ("collision_reward", C.c_double),
     ]
 
 
@@ -94,7 +97,7 @@ class PgxStepOut(C.Structure):
 class PgxStateView(C.Structure):
     _fields_ = [
         ("q", C.c_void_p), ("qd", C.c_void_p), ("goal", C.c_void_p), ("object", C.c_void_p),
-        ("contacts", C.c_void_p), ("elapsed", C.c_void_p), ("episode", C.c_void_p),
+        ("contacts", C.c_void_p), ("obstacles", C.c_void_p), ("elapsed", C.c_void_p), ("episode", C.c_void_p),
     ]
 
 
@@ -154,7 +157,7 @@ def make_model(model: Model, ee_link: int = 11) -> PgxModel:
         m.upper[d] = model.upper[d]
     for r, (k, d) in enumerate(zip(kinds, dofs)):
         m.row_kind[r], m.row_dof[r] = int(k), int(d)
-    caps = model.capsules()
+    caps = model.capsules(base_capsule=model.name == "panda_custom0")
     assert len(caps) <= MAX_CAPSULES
     m.n_capsules = len(caps)
     for i, c in enumerate(caps):
@@ -208,6 +211,16 @@ class EnvSpec:
     distance_threshold: float = 0.05                   # reach.py:15
     goal_range: float = 0.3                            # reach.py:16
 
+    @classmethod
+    def reach_ao(cls, max_episode_steps: int = 50) -> "EnvSpec":
+        """PandaReachAO-v3 with TrainConfig defaults (panda_tasks.py:132-159,
+        train_config.py:25-59): base at the origin, joint control, sparse reward,
+        terminate on success, ee_error_threshold float32(0.05) (reach_ao.py:71)."""
+        import numpy as np
+        return cls(task=TASK_REACH_AO, control=CONTROL_JOINTS, reward=REWARD_SPARSE,
+                   max_episode_steps=max_episode_steps, block_gripper=True, base_pos=(0.0, 0.0, 0.0),
+                   distance_threshold=float(np.float32(0.05)))
+
     def obj_bounds(self):
         """push.py:26-27 / pick_and_place.py:28-29: noise ranges of the object position."""
         return [-0.15, -0.15, 0.0], [0.15, 0.15, 0.0]
@@ -222,6 +235,8 @@ class EnvSpec:
 
     @property
     def obs_dim(self) -> int:
+        if self.task == TASK_REACH_AO:   # ("ee","js") 20 + vectors+closest_per_link 36
+            return 20 + 4 * AO_LINKS
         return 6 + (0 if self.block_gripper else 1) + (0 if self.task == TASK_REACH else 12)
 
     @property
@@ -263,10 +278,13 @@ def make_config(spec: EnvSpec, n_envs: int, model: PgxModel, params: PgxSimParam
     c.object_half = half
     c.object_mass = 1.0                           # push.py:37
     c.object_inertia = box_inertia(OBJECT_MASS, half)
-    for i in range(3):                            # create_table(1.1, 0.7, 0.4, x_offset=-0.3)
-        c.table_center[i] = (-0.3, 0.0, -0.2)[i]
-        c.table_half[i] = (0.55, 0.35, 0.2)[i]
+    ao = spec.task == TASK_REACH_AO
+    for i in range(3):  # create_table(1.1, 0.7, 0.4, x_offset=-0.3); ReachAO create_table(2.0, 1.3, 0.4) (reach_ao.py:272)
+        c.table_center[i] = ((0.0, 0.0, -0.2) if ao else (-0.3, 0.0, -0.2))[i]
+        c.table_half[i] = ((1.0, 0.65, 0.2) if ao else (0.55, 0.35, 0.2))[i]
     c.plane_z = -0.4                              # create_plane(z_offset=-0.4): box top
+    c.terminate_on_success = 1 if ao else 0       # core.py:265 / train_config.py:28
+    c.collision_reward = -100.0 if ao else 0.0    # train_config.py:33
     return c
 
 

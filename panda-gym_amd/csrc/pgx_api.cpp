@@ -78,6 +78,7 @@ const char* pgx_last_error(void) { return g_err.c_str(); }
 
 int pgx_obs_dim(const pgx_config* c) {
     if (!c) return PGX_E_INVALID;
+    if (c->task == PGX_TASK_REACH_AO) return 20 + 4 * PGX_AO_LINKS;   /* ("ee","js") + vectors+closest_per_link */
     return 6 + (c->block_gripper ? 0 : 1) + (c->task == PGX_TASK_REACH ? 0 : 12);
 }
 int pgx_action_dim(const pgx_config* c) {
@@ -269,11 +270,16 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     if (!cfg || !out || !cfg->model || !cfg->params) return fail(PGX_E_INVALID, "null argument");
     *out = nullptr;
     if (cfg->n_envs <= 0) return fail(PGX_E_INVALID, "n_envs must be > 0 (got %d)", cfg->n_envs);
-    if (cfg->task != PGX_TASK_REACH && cfg->task != PGX_TASK_PUSH && cfg->task != PGX_TASK_PICK_AND_PLACE)
+    if (cfg->task != PGX_TASK_REACH && cfg->task != PGX_TASK_PUSH && cfg->task != PGX_TASK_PICK_AND_PLACE &&
+        cfg->task != PGX_TASK_REACH_AO)
         return fail(PGX_E_UNSUPPORTED, "task %d is not implemented by this build", cfg->task);
-    if (cfg->task != PGX_TASK_REACH && !cfg->contacts)
+    const bool has_object = cfg->task == PGX_TASK_PUSH || cfg->task == PGX_TASK_PICK_AND_PLACE;
+    if (cfg->task == PGX_TASK_REACH_AO &&
+        (cfg->control != PGX_CONTROL_JOINTS || !cfg->block_gripper || !cfg->contacts))
+        return fail(PGX_E_UNSUPPORTED, "ReachAO is built for joint control, blocked gripper and the table scene");
+    if (has_object && !cfg->contacts)
         return fail(PGX_E_INVALID, "object tasks need contacts");
-    if (cfg->task != PGX_TASK_REACH && (cfg->object_half <= 0 || cfg->object_mass <= 0 || cfg->object_inertia <= 0))
+    if (has_object && (cfg->object_half <= 0 || cfg->object_mass <= 0 || cfg->object_inertia <= 0))
         return fail(PGX_E_INVALID, "object size, mass and inertia must be > 0");
     if (cfg->control != PGX_CONTROL_EE && cfg->control != PGX_CONTROL_JOINTS)
         return fail(PGX_E_INVALID, "control %d", cfg->control);
@@ -304,7 +310,7 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     }
     e.goal_z_zero_prob = cfg->goal_z_zero_prob;
     e.contacts = cfg->contacts ? 1 : 0;
-    e.has_object = cfg->task != PGX_TASK_REACH;
+    e.has_object = has_object;
     e.obj_half = (float)cfg->object_half;
     e.obj_inv_mass = e.has_object ? (float)(1.0 / cfg->object_mass) : 0.0f;
     e.obj_inv_inertia = e.has_object ? (float)(1.0 / cfg->object_inertia) : 0.0f;
@@ -314,6 +320,10 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     e.table_hy = (float)cfg->table_half[1];
     e.table_top = (float)(cfg->table_center[2] + cfg->table_half[2]);
     e.plane_z = (float)cfg->plane_z;
+    e.table_hz = (float)cfg->table_half[2];
+    e.ao = cfg->task == PGX_TASK_REACH_AO;
+    e.terminate_on_success = cfg->terminate_on_success ? 1 : 0;
+    e.collision_reward = cfg->collision_reward;
 
     rc = hip_check(hipSetDevice(device), "hipSetDevice");
     if (rc) { delete h; return rc; }
@@ -321,7 +331,8 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     auto align = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t off_goal = align(sizeof(PgxDevModel)), off_q = align(off_goal + 3 * N * 8), off_qd = align(off_q + PGX_NJ * N * 4),
            off_obj = align(off_qd + PGX_NJ * N * 4), off_ct = align(off_obj + 13 * N * 4),
-           off_el = align(off_ct + 2 * PGX_CONTACT_SLOTS * N * 4), off_ep = align(off_el + N * 4),
+           off_ao = align(off_ct + 2 * PGX_CONTACT_SLOTS * N * 4),
+           off_el = align(off_ao + (e.ao ? 4 * PGX_AO_OBSTACLES * N * 4 : 0)), off_ep = align(off_el + N * 4),
            total = align(off_ep + N * 4);
     rc = hip_check(hipMalloc(&h->blob, total), "hipMalloc(state)");
     if (rc) { delete h; return rc; }
@@ -332,6 +343,7 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     h->ds.qd = (float*)(b + off_qd);
     h->ds.object = (float*)(b + off_obj);
     h->ds.contacts = (float*)(b + off_ct);
+    h->ds.obstacles = e.ao ? (float*)(b + off_ao) : nullptr;
     h->ds.elapsed = (int32_t*)(b + off_el);
     h->ds.episode = (uint32_t*)(b + off_ep);
     h->dm_dev = (PgxDevModel*)b;
@@ -365,6 +377,7 @@ int pgx_get_state(pgx_handle h, pgx_state_view* out) {
     out->goal = h->ds.goal;
     out->object = h->ds.object;
     out->contacts = h->ds.contacts;
+    out->obstacles = h->ds.obstacles;
     out->elapsed = h->ds.elapsed;
     out->episode = h->ds.episode;
     return PGX_OK;
@@ -390,7 +403,8 @@ static PgxDevOut to_dev_out(const pgx_step_out* o) {
 int pgx_reset(pgx_handle h, const uint8_t* env_mask, const double* inject_goal, const double* inject_object,
               pgx_step_out* out, void* stream) {
     if (!h) return fail(PGX_E_INVALID, "null handle");
-    if (inject_object && !h->de.has_object) return fail(PGX_E_INVALID, "object injection needs an object task");
+    if (inject_object && !h->de.has_object && !h->de.ao)
+        return fail(PGX_E_INVALID, "object injection needs an object task (or ReachAO obstacles)");
     return hip_check((hipError_t)pgx_launch_reset(h->dm_dev, h->de, h->ds, env_mask, inject_goal, inject_object,
                                                   to_dev_out(out), stream),
                      "reset launch");
@@ -409,7 +423,7 @@ int pgx_sample_actions(pgx_handle h, float* action, uint64_t step, void* stream)
 int pgx_compute_reward(const float* ag, const float* dg, int64_t batch, int32_t reward_type, double thr, float* out,
                        void* stream) {
     if (batch < 0 || (batch > 0 && (!ag || !dg || !out))) return fail(PGX_E_INVALID, "bad arguments");
-    if (reward_type != PGX_REWARD_SPARSE && reward_type != PGX_REWARD_DENSE)
+    if (reward_type != PGX_REWARD_SPARSE && reward_type != PGX_REWARD_DENSE && reward_type != PGX_REWARD_SPARSE_AO)
         return fail(PGX_E_INVALID, "reward_type %d", reward_type);
     return hip_check((hipError_t)pgx_launch_compute_reward(ag, dg, batch, reward_type, thr, out, stream),
                      "compute_reward launch");

@@ -38,7 +38,9 @@ __device__ __forceinline__ float distance_f32_f32(const float* a, const float* b
 }
 #pragma clang fp contract(on)
 
-/* Task.compute_reward (reach.py:84-89): sparse -(d > thr) as f32 (-0.0 on success), dense -d */
+/* Task.compute_reward (reach.py:84-89): sparse -(d > thr) as f32 (-0.0 on success), dense -d;
+ * ReachAO sparse (reach_ao.py:1320) -1 + (d < thr) (+0.0 on success) */
 __device__ __forceinline__ float reward_f32(float d, int reward_type, float thr) {
+    if (reward_type == 2) return d < thr ? 0.0f : -1.0f;
     return reward_type == 0 ? -((d > thr) ? 1.0f : 0.0f) : -d;
 }

@@ -54,6 +54,10 @@ struct PgxDevEnv {
     int32_t contacts, has_object;
     float obj_half, obj_inv_mass, obj_inv_inertia;
     float table_cx, table_cy, table_hx, table_hy, table_top, plane_z;
+    float table_hz;
+    int32_t ao;                    /* ReachAO (obstacles, per-substep collision check) */
+    int32_t terminate_on_success;
+    double collision_reward;
 };
 
 struct PgxDevState {
@@ -62,6 +66,7 @@ struct PgxDevState {
     double* goal;      /* [3][N] */
     float* object;     /* [13][N] pos3 quat4 (x,y,z,w) linvel3 angvel3 */
     float* contacts;   /* [2*PGX_CONTACT_SLOTS][N] warm-start cache (feature id, normal impulse) */
+    float* obstacles;  /* [4*PGX_AO_OBSTACLES][N] ReachAO centres (o, xyz) then active flags */
     int32_t* elapsed;  /* [N] */
     uint32_t* episode; /* [N] */
 };

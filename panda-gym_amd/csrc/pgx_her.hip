@@ -320,7 +320,8 @@ int pgx_replay_create(const pgx_replay_config* cfg, int device, pgx_replay_handl
         return pgx_set_error(PGX_E_INVALID, "pgx_replay_create: her_ratio must be in [0, 1]");
     if ((int64_t)cfg->capacity * cfg->n_envs >= (1ll << 31))
         return pgx_set_error(PGX_E_INVALID, "pgx_replay_create: capacity * n_envs must be < 2^31");
-    if (cfg->reward_type != PGX_REWARD_SPARSE && cfg->reward_type != PGX_REWARD_DENSE)
+    if (cfg->reward_type != PGX_REWARD_SPARSE && cfg->reward_type != PGX_REWARD_DENSE &&
+        cfg->reward_type != PGX_REWARD_SPARSE_AO)
         return pgx_set_error(PGX_E_INVALID, "pgx_replay_create: unknown reward_type");
     if (cfg->strategy < PGX_HER_FUTURE || cfg->strategy > PGX_HER_EPISODE)
         return pgx_set_error(PGX_E_INVALID, "pgx_replay_create: unknown goal selection strategy");

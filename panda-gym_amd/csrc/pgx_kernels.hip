@@ -358,6 +358,9 @@ struct ContactLds {
     int cnt[2][64];
     float cache[CACHE_N][64];      /* (feature id, normal impulse) x 4 per group */
     float capA[PGX_NCAP][3][64], capB[PGX_NCAP][3][64];   /* capsule end points, world */
+    /* ReachAO: obstacle centres, per collision link the closest distance and unit vector */
+    float aoC[PGX_AO_OBSTACLES][3][64];
+    float aoD[PGX_AO_LINKS][64], aoU[PGX_AO_LINKS][3][64];
 };
 
 struct ObjState {
@@ -1168,7 +1171,312 @@ __device__ __forceinline__ void store_obj(const PgxDevState& s, int N, int i, co
     o[10 * N + i] = ob.w.x; o[11 * N + i] = ob.w.y; o[12 * N + i] = ob.w.z;
 }
 
-template <int CONTROL, int OBJ, int CONT>
+
+/* ------------------------------------------------------------- ReachAO */
+/* PandaReachAO-v3 "reachao_rand" (reach_ao.py; restated in oracle/pgx_oracle.c "ReachAO"):
+ * 3 spheres (r 0.05) then 3 cuboids (half 0.05, rounded by the 1 mm box margin) per env,
+ * centres in LDS; the robot's 9 collision links (panda_link1..8, panda_ee: every capsule
+ * but the base and the hand) against them after every substep (step_check_collision
+ * :182-188, early exit), and against the table for links 2..ee (check_collided
+ * :896-900); the observation's closest distance + unit vector per link (get_obs
+ * "vectors+closest_per_link" :902-959).  Exact distances are evaluated only for pairs a
+ * cheap bound cannot rule out: the capsule axis against the obstacle's bounding sphere. */
+constexpr int AO_N = PGX_AO_OBSTACLES;
+constexpr float kAoSize = 0.05f, kAoMargin = 0.001f, kAoDummyR = 0.05f;
+constexpr float kAoCubeBound = 0.0866025404f;   /* 0.05 * sqrt(3): cuboid circumradius */
+
+/* AO collision-link slot of each capsule (-1: base, hand) */
+__host__ __device__ constexpr int ao_slot(int c) {
+    return kCapLink[c] < 0 ? -1 : (kCapLink[c] <= 7 ? kCapLink[c] : (kCapLink[c] == 9 ? 8 : -1));
+}
+__device__ constexpr int kAoSlot[PGX_NCAP] = {ao_slot(0), ao_slot(1), ao_slot(2), ao_slot(3), ao_slot(4),
+                                              ao_slot(5), ao_slot(6), ao_slot(7), ao_slot(8), ao_slot(9),
+                                              ao_slot(10), ao_slot(11), ao_slot(12), ao_slot(13)};
+static_assert(PGX_NCAP == 14, "kAoSlot table");
+
+__device__ __forceinline__ V3 lds3(const float (*a)[64], int ln) { return v3(a[0][ln], a[1][ln], a[2][ln]); }
+
+/* signed distance to the axis-aligned box (c, h) */
+__device__ __forceinline__ float box_sd(V3 P, V3 c, V3 h) {
+    const float dx = fabsf(P.x - c.x) - h.x, dy = fabsf(P.y - c.y) - h.y, dz = fabsf(P.z - c.z) - h.z;
+    const float ox = fmaxf(dx, 0.0f), oy = fmaxf(dy, 0.0f), oz = fmaxf(dz, 0.0f);
+    return fast_sqrt(ox * ox + oy * oy + oz * oz) + fminf(fmaxf(dx, fmaxf(dy, dz)), 0.0f);
+}
+
+/* closest point of segment AB to C */
+__device__ __forceinline__ V3 seg_closest(V3 A, V3 B, V3 C) {
+    const V3 ab = B - A;
+    const float l2 = dot(ab, ab);
+    float t = l2 > 0.0f ? dot(C - A, ab) / l2 : 0.0f;
+    t = fminf(fmaxf(t, 0.0f), 1.0f);
+    return A + t * ab;
+}
+
+/* capsule (A, B, r) vs rounded box (c, full half extents hf): 40 ternary-search steps
+ * on the inner box's signed distance along the axis; the unit vector (from the
+ * capsule's closest point to the box's, utils.unit_vector) when asked for */
+template <bool VEC>
+__device__ __forceinline__ float capsule_box(V3 A, V3 B, float r, V3 c, V3 hf, V3* u) {
+    const V3 h = v3(hf.x - kAoMargin, hf.y - kAoMargin, hf.z - kAoMargin);
+    const V3 ab = B - A;
+    float lo = 0.0f, hi = 1.0f;
+    const bool seg = dot(ab, ab) > 0.0f;
+    if (seg) {
+        for (int it = 0; it < 40; it++) {
+            const float m1 = lo + (hi - lo) * (1.0f / 3.0f), m2 = hi - (hi - lo) * (1.0f / 3.0f);
+            if (box_sd(A + m1 * ab, c, h) <= box_sd(A + m2 * ab, c, h)) hi = m2;
+            else lo = m1;
+        }
+    }
+    const V3 P = A + (seg ? 0.5f * (lo + hi) : 0.0f) * ab;
+    const float sd = box_sd(P, c, h);
+    const float d = sd - kAoMargin - r;
+    if (VEC) {
+        V3 n;
+        if (sd > 0.0f) {
+            const V3 q = v3(fminf(fmaxf(P.x, c.x - h.x), c.x + h.x), fminf(fmaxf(P.y, c.y - h.y), c.y + h.y),
+                            fminf(fmaxf(P.z, c.z - h.z), c.z + h.z));
+            const V3 v = q - P;
+            const float len = norm(v);
+            n = len > 0.0f ? fast_rcp(len) * v : v3(0.0f, 0.0f, 0.0f);
+        } else {   /* inside the inner box: out through the nearest face */
+            const float bx = fabsf(P.x - c.x) - h.x, by = fabsf(P.y - c.y) - h.y, bz = fabsf(P.z - c.z) - h.z;
+            const int ax = (bx >= by && bx >= bz) ? 0 : (by >= bz ? 1 : 2);
+            const float sx = P.x < c.x ? 1.0f : -1.0f, sy = P.y < c.y ? 1.0f : -1.0f, sz = P.z < c.z ? 1.0f : -1.0f;
+            n = v3(ax == 0 ? sx : 0.0f, ax == 1 ? sy : 0.0f, ax == 2 ? sz : 0.0f);
+        }
+        /* pb - pa = d * n */
+        *u = d > 0.0f ? n : (d < 0.0f ? (-1.0f) * n : v3(0.0f, 0.0f, 0.0f));
+    }
+    return d;
+}
+
+/* world end points of every capsule at q (base capsule included) into LDS */
+template <int C = 0>
+__device__ __forceinline__ void ao_caps_walk(const Chain& k, MRef m, ContactLds& L, int ln) {
+    if constexpr (C < PGX_NCAP) {
+        V3 A, B;
+        if constexpr (kCapJ[C] < 0) {
+            const V3 b = v3(m.base[0], m.base[1], m.base[2]);
+            A = b + v3(kCapA[C][0], kCapA[C][1], kCapA[C][2]);
+            B = b + v3(kCapB[C][0], kCapB[C][1], kCapB[C][2]);
+        } else {
+            A = k.o[kCapJ[C]] + mulc(k.R[kCapJ[C]], kCapA[C]);
+            B = k.o[kCapJ[C]] + mulc(k.R[kCapJ[C]], kCapB[C]);
+        }
+        L.capA[C][0][ln] = A.x; L.capA[C][1][ln] = A.y; L.capA[C][2][ln] = A.z;
+        L.capB[C][0][ln] = B.x; L.capB[C][1][ln] = B.y; L.capB[C][2][ln] = B.z;
+        ao_caps_walk<C + 1>(k, m, L, ln);
+    }
+}
+__device__ __forceinline__ void ao_caps(MRef m, const float* q, ContactLds& L, int ln) {
+    Chain k;
+    fk_chain(m, q, k);
+    ao_caps_walk(k, m, L, ln);
+}
+
+__device__ __forceinline__ V3 ao_table_c(const PgxDevEnv& e) { return v3(e.table_cx, e.table_cy, e.table_top - e.table_hz); }
+__device__ __forceinline__ V3 ao_table_h(const PgxDevEnv& e) { return v3(e.table_hx, e.table_hy, e.table_hz); }
+
+/* check_collided: any collision link within 0 of an obstacle, or links 2..ee of the table */
+__device__ __forceinline__ bool ao_collided(const PgxDevEnv& e, ContactLds& L, int ln) {
+    const V3 tc = ao_table_c(e), th = ao_table_h(e);
+    const V3 thi = v3(th.x - kAoMargin, th.y - kAoMargin, th.z - kAoMargin);
+    const V3 hcube = v3(kAoSize, kAoSize, kAoSize);
+    bool hit = false;
+    for (int c = 0; c < PGX_NCAP && !hit; c++) {
+        const int slot = kAoSlot[c];
+        if (slot < 0) continue;
+        const V3 A = lds3(L.capA[c], ln), B = lds3(L.capB[c], ln);
+        const float r = kCapR[c];
+        for (int o = 0; o < AO_N; o++) {
+            const V3 C = lds3(L.aoC[o], ln);
+            const V3 P = seg_closest(A, B, C);
+            const float dc = norm(C - P) - r;
+            if (o < 3) hit = hit || dc - kAoSize <= 0.0f;
+            else if (dc - kAoCubeBound <= 0.0f) hit = hit || capsule_box<false>(A, B, r, C, hcube, nullptr) <= 0.0f;
+        }
+        if (slot >= 1) {
+            /* box_sd is 1-Lipschitz: min over the segment >= min(ends) - |AB| / 2 */
+            const float lb = fminf(box_sd(A, tc, thi), box_sd(B, tc, thi)) - 0.5f * norm(B - A) - kAoMargin - r;
+            if (lb <= 0.0f) hit = hit || capsule_box<false>(A, B, r, tc, th, nullptr) <= 0.0f;
+        }
+    }
+    return hit;
+}
+
+/* per collision link: the closest obstacle's distance and unit vector into LDS */
+__device__ __forceinline__ void ao_link_obs(ContactLds& L, int ln) {
+    for (int l = 0; l < PGX_AO_LINKS; l++) L.aoD[l][ln] = 3.0e38f;
+    const V3 hcube = v3(kAoSize, kAoSize, kAoSize);
+    for (int c = 0; c < PGX_NCAP; c++) {
+        const int slot = kAoSlot[c];
+        if (slot < 0) continue;
+        const V3 A = lds3(L.capA[c], ln), B = lds3(L.capB[c], ln);
+        const float r = kCapR[c];
+        float best = L.aoD[slot][ln];
+        V3 bu = v3(0.0f, 0.0f, 0.0f);
+        bool upd = false;
+        for (int o = 0; o < AO_N; o++) {
+            const V3 C = lds3(L.aoC[o], ln);
+            const V3 P = seg_closest(A, B, C);
+            const V3 v = C - P;
+            const float len = norm(v);
+            if (o < 3) {
+                const float d = len - r - kAoSize;
+                if (d < best) {
+                    best = d;
+                    const V3 n = len > 0.0f ? fast_rcp(len) * v : v3(0.0f, 0.0f, 1.0f);
+                    bu = d > 0.0f ? n : (d < 0.0f ? (-1.0f) * n : v3(0.0f, 0.0f, 0.0f));
+                    upd = true;
+                }
+            } else if (len - r - kAoCubeBound < best) {
+                V3 u;
+                const float d = capsule_box<true>(A, B, r, C, hcube, &u);
+                if (d < best) { best = d; bu = u; upd = true; }
+            }
+        }
+        if (upd) {
+            L.aoD[slot][ln] = best;
+            L.aoU[slot][0][ln] = bu.x; L.aoU[slot][1][ln] = bu.y; L.aoU[slot][2][ln] = bu.z;
+        }
+    }
+}
+
+/* robot obs ("ee","js": panda.py:264-288) + 9 distances + 9 unit vectors */
+__device__ __forceinline__ void ao_write_obs(float* dst, V3 pos, V3 vel, const float* q, const float* qd,
+                                             const ContactLds& L, int ln) {
+    dst[0] = pos.x; dst[1] = pos.y; dst[2] = pos.z;
+    dst[3] = vel.x; dst[4] = vel.y; dst[5] = vel.z;
+#pragma unroll
+    for (int j = 0; j < NJ; j++) { dst[6 + j] = q[j]; dst[13 + j] = qd[j]; }
+#pragma unroll
+    for (int l = 0; l < PGX_AO_LINKS; l++) dst[20 + l] = L.aoD[l][ln];
+#pragma unroll
+    for (int l = 0; l < PGX_AO_LINKS; l++)
+#pragma unroll
+        for (int k = 0; k < 3; k++) dst[29 + 3 * l + k] = L.aoU[l][k][ln];
+}
+
+/* whole-robot distance (every capsule) to a sphere (kind 0) / rounded cube (1) */
+__device__ __noinline__ float ao_robot_distance(ContactLds& L, int ln, int kind, V3 C, float size) {
+    float best = 3.0e38f;
+    const V3 hc = v3(size, size, size);
+    for (int c = 0; c < PGX_NCAP; c++) {
+        const V3 A = lds3(L.capA[c], ln), B = lds3(L.capB[c], ln);
+        const float r = kCapR[c];
+        const float dc = norm(C - seg_closest(A, B, C)) - r;
+        float d;
+        if (kind == 0) d = dc - size;
+        else if (dc - 1.7320508f * size >= best) continue;
+        else d = capsule_box<false>(A, B, r, C, hc, nullptr);
+        best = fminf(best, d);
+    }
+    return best;
+}
+
+struct AoDraw {
+    uint64_t env;
+    uint32_t episode;
+    int k;
+};
+__device__ __forceinline__ double ao_draw(const PgxDevEnv& e, AoDraw& d) { return reset_uniform(e, d.env, d.episode, d.k++); }
+__device__ __forceinline__ double ao_uniform(const PgxDevEnv& e, AoDraw& d, double lo, double hi) {
+    return uniform_draw(lo, hi, ao_draw(e, d));
+}
+/* sample_within_hollow_sphere (reach_ao.py:1188-1211) */
+__device__ __noinline__ void ao_hollow_sphere(const PgxDevEnv& e, AoDraw& d, double rmin, double rmax, bool upper,
+                                              double* out) {
+    const double pi = 3.14159265358979323846;
+    const double phi = ao_uniform(e, d, 0.0, 2.0 * pi);
+    const double theta = upper ? ao_uniform(e, d, 0.0, 0.5 * pi) : ao_uniform(e, d, 0.0, pi);
+    const double r = cbrt(ao_uniform(e, d, pow(rmin, 3.0), pow(rmax, 3.0)));
+    out[0] = r * sin(theta) * cos(phi);
+    out[1] = r * sin(theta) * sin(phi);
+    out[2] = r * cos(theta);
+}
+
+/* ReachAO.reset for reachao_rand (reach_ao.py:965-1082; oracle ao_reset_task): goal,
+ * obstacles by rejection against robot / table / dummy sphere, 4-5 active.  Needs the
+ * neutral-pose capsules in LDS; leaves the centres in L.aoC. */
+__device__ __noinline__ void ao_reset(const PgxDevEnv& e, ContactLds& L, int ln, uint64_t env, uint32_t episode, V3 ee,
+                                      const double* inject_goal, const double* inject_obst, double* goal) {
+    AoDraw d{env, episode, 0};
+    const V3 tc = ao_table_c(e), th = ao_table_h(e);
+    double dummy[3] = {0.0, 0.0, 0.0};
+    for (int i = 0;; i++) {
+        ao_hollow_sphere(e, d, 0.5, 0.8, true, goal);
+        if (i > 9999) { goal[0] = ee.x; goal[1] = ee.y; goal[2] = ee.z; break; }
+        dummy[0] = goal[0]; dummy[1] = goal[1]; dummy[2] = goal[2];
+        const V3 g = v3((float)goal[0], (float)goal[1], (float)goal[2]);
+        const bool coll = box_sd(g, tc, v3(th.x - kAoMargin, th.y - kAoMargin, th.z - kAoMargin)) - kAoMargin -
+                                  kAoDummyR <= 0.1f ||
+                          ao_robot_distance(L, ln, 0, g, kAoDummyR) <= 0.1f;
+        if (!coll) break;
+    }
+    const V3 dm = v3((float)dummy[0], (float)dummy[1], (float)dummy[2]);
+    for (int o = 0; o < AO_N; o++) {
+        double P[3];
+        for (int it = 0; it < 10000; it++) {
+            const double rnd = ao_draw(e, d);
+            double sm[3];
+            ao_hollow_sphere(e, d, 0.1, 0.5, false, sm);
+            if (rnd > 0.5) { P[0] = sm[0] + goal[0]; P[1] = sm[1] + goal[1]; P[2] = sm[2] + goal[2]; }
+            else { P[0] = (double)ee.x + sm[0]; P[1] = (double)ee.y + sm[1]; P[2] = (double)ee.z + sm[2]; }
+            const V3 Pf = v3((float)P[0], (float)P[1], (float)P[2]);
+            float dtab, ddum;
+            if (o < 3) {
+                dtab = box_sd(Pf, tc, v3(th.x - kAoMargin, th.y - kAoMargin, th.z - kAoMargin)) - kAoMargin - kAoSize;
+                ddum = norm(Pf - dm) - kAoSize - kAoDummyR;
+            } else {
+                const float g2 = kAoSize - 2.0f * kAoMargin;
+                dtab = box_sd(Pf, tc, v3(th.x + g2, th.y + g2, th.z + g2)) - 2.0f * kAoMargin;
+                ddum = box_sd(dm, Pf, v3(kAoSize - kAoMargin, kAoSize - kAoMargin, kAoSize - kAoMargin)) - kAoMargin -
+                       kAoDummyR;
+            }
+            const bool coll = dtab <= 0.03f || ddum <= 0.03f || ao_robot_distance(L, ln, o < 3 ? 0 : 1, Pf, kAoSize) <= 0.03f;
+            if (!coll) break;
+        }
+        L.aoC[o][0][ln] = (float)P[0]; L.aoC[o][1][ln] = (float)P[1]; L.aoC[o][2][ln] = (float)P[2];
+    }
+    const int n_active = 4 + (int)(ao_draw(e, d) * 2.0);
+    int perm[AO_N] = {0, 1, 2, 3, 4, 5};
+    for (int j = AO_N - 1; j > 0; j--) {   /* Fisher-Yates, unrolled so perm stays in VGPRs */
+        int r = (int)(ao_draw(e, d) * (double)(j + 1));
+        r = r > j ? j : r;
+        int pj = 0, pr = 0;
+#pragma unroll
+        for (int t = 0; t < AO_N; t++) { pj = t == j ? perm[t] : pj; pr = t == r ? perm[t] : pr; }
+#pragma unroll
+        for (int t = 0; t < AO_N; t++) perm[t] = t == j ? pr : (t == r ? pj : perm[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < AO_N; t++) {
+        int pt = perm[t];
+        if (t < AO_N - n_active) { L.aoC[pt][0][ln] = 99.9f; L.aoC[pt][1][ln] = 99.9f; L.aoC[pt][2][ln] = -99.9f; }
+    }
+    if (inject_goal) { goal[0] = inject_goal[0]; goal[1] = inject_goal[1]; goal[2] = inject_goal[2]; }
+    if (inject_obst)
+        for (int o = 0; o < AO_N; o++)
+            for (int k = 0; k < 3; k++) L.aoC[o][k][ln] = (float)inject_obst[3 * o + k];
+}
+
+__device__ __forceinline__ void ao_load(const PgxDevState& s, int N, int i, ContactLds& L, int ln) {
+#pragma unroll
+    for (int o = 0; o < AO_N; o++)
+#pragma unroll
+        for (int k = 0; k < 3; k++) L.aoC[o][k][ln] = s.obstacles[(3 * o + k) * N + i];
+}
+__device__ __forceinline__ void ao_store(const PgxDevState& s, int N, int i, const ContactLds& L, int ln) {
+#pragma unroll
+    for (int o = 0; o < AO_N; o++) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) s.obstacles[(3 * o + k) * N + i] = L.aoC[o][k][ln];
+        s.obstacles[(3 * AO_N + o) * N + i] = L.aoC[o][0][ln] < 50.0f ? 1.0f : 0.0f;
+    }
+}
+
+template <int CONTROL, int OBJ, int CONT, int AO>
 __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict__ mdev, PgxDevEnv e, PgxDevState s,
                                                   const float* __restrict__ action, PgxDevOut o) {
     const int ln = threadIdx.x;
@@ -1209,6 +1517,7 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
 #pragma unroll
         for (int k = 0; k < CACHE_N; k++) L->cache[k][ln] = s.contacts[k * N + ii];
     }
+    if constexpr (AO) ao_load(s, N, ii, *L, ln);
 
     /* Panda.set_action: clip to Box(-1,1) in float32 */
     const int A = e.action_dim;
@@ -1232,7 +1541,14 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
     }
 
     const int n_substeps = m.n_substeps;
-    for (int st = 0; st < n_substeps; st++) substep<OBJ, CONT>(mp, e, q, qd, tq, ob, L, ln);
+    bool collided = false;
+    for (int st = 0; st < n_substeps; st++) {
+        substep<OBJ, CONT>(mp, e, q, qd, tq, ob, L, ln);
+        if constexpr (AO) {   /* ReachAO step_check_collision: check after every substep, stop on contact */
+            ao_caps(*fresh(mp), q, *L, ln);
+            if (ao_collided(e, *L, ln)) { collided = true; break; }
+        }
+    }
 
     V3 pos, vel;
     ee_state(*fresh(mp), q, qd, pos, vel);
@@ -1240,16 +1556,28 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
     const V3 ag = OBJ ? ob.p : pos;
     double d = distance_f32_f64(ag, goal);
     bool succ = d < e.distance_threshold;
-    float rew = e.reward == 0 ? -((d > e.distance_threshold) ? 1.0f : 0.0f) : -(float)d;
+    float rew;
+    if (AO) {   /* ReachAO.compute_reward sparse + collision_reward (reach_ao.py:1317-1320, 1376-1377) */
+        rew = -1.0f + ((d + (collided ? 1.0 : 0.0)) < e.distance_threshold ? 1.0f : 0.0f);
+        if (collided) rew += (float)e.collision_reward;
+    } else {
+        rew = e.reward == 0 ? -((d > e.distance_threshold) ? 1.0f : 0.0f) : -(float)d;
+    }
     int el = s.elapsed[i] + 1;
     uint32_t episode = s.episode[i];
-    bool trunc = e.max_episode_steps > 0 && el >= e.max_episode_steps;
+    /* TimeLimit, ReachAO.is_truncated (collision); terminate_on_success (core.py:359-361) */
+    const bool trunc = (e.max_episode_steps > 0 && el >= e.max_episode_steps) || collided;
+    const bool term = e.terminate_on_success && succ;
     if (o.reward) o.reward[i] = rew;
     if (o.success) o.success[i] = succ;
-    if (o.terminated) o.terminated[i] = 0;
+    if (o.terminated) o.terminated[i] = term;
     if (o.truncated) o.truncated[i] = trunc;
-    if (trunc) {
-        if (o.terminal_obs) write_obs<OBJ>(e, o.terminal_obs + (size_t)i * od, pos, vel, ob);
+    if constexpr (AO) ao_link_obs(*L, ln);
+    if (trunc || term) {
+        if (o.terminal_obs) {
+            if constexpr (AO) ao_write_obs(o.terminal_obs + (size_t)i * od, pos, vel, q, qd, *L, ln);
+            else write_obs<OBJ>(e, o.terminal_obs + (size_t)i * od, pos, vel, ob);
+        }
         if (o.terminal_ag) {
             o.terminal_ag[3 * (size_t)i] = ag.x; o.terminal_ag[3 * (size_t)i + 1] = ag.y;
             o.terminal_ag[3 * (size_t)i + 2] = ag.z;
@@ -1258,16 +1586,30 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
             o.terminal_dg[3 * (size_t)i] = (float)goal[0]; o.terminal_dg[3 * (size_t)i + 1] = (float)goal[1];
             o.terminal_dg[3 * (size_t)i + 2] = (float)goal[2];
         }
-        reset_env<OBJ>(m, e, i, episode, nullptr, nullptr, q, qd, goal, ob);
+        if constexpr (AO) {
+            MRef mr = *fresh(mp);
+#pragma unroll
+            for (int j = 0; j < NJ; j++) { q[j] = mr.neutral_q[j]; qd[j] = 0.0f; }
+            ee_state(mr, q, qd, pos, vel);
+            ao_caps(mr, q, *L, ln);
+            ao_reset(e, *L, ln, e.env_id_offset + (uint64_t)i, episode, pos, nullptr, nullptr, goal);
+            episode += 1;
+            ao_link_obs(*L, ln);
+        } else {
+            reset_env<OBJ>(m, e, i, episode, nullptr, nullptr, q, qd, goal, ob);
+            ee_state(m, q, qd, pos, vel);
+        }
         el = 0;
-        ee_state(m, q, qd, pos, vel);
         if (CONT) {
 #pragma unroll
             for (int k = 0; k < CACHE_N; k++) L->cache[k][ln] = (k & 1) ? 0.0f : -1.0f;
         }
     }
     const V3 ag2 = OBJ ? ob.p : pos;
-    if (o.obs) write_obs<OBJ>(e, o.obs + (size_t)i * od, pos, vel, ob);
+    if (o.obs) {
+        if constexpr (AO) ao_write_obs(o.obs + (size_t)i * od, pos, vel, q, qd, *L, ln);
+        else write_obs<OBJ>(e, o.obs + (size_t)i * od, pos, vel, ob);
+    }
     if (o.ag) { o.ag[3 * (size_t)i] = ag2.x; o.ag[3 * (size_t)i + 1] = ag2.y; o.ag[3 * (size_t)i + 2] = ag2.z; }
     if (o.dg) {
         o.dg[3 * (size_t)i] = (float)goal[0]; o.dg[3 * (size_t)i + 1] = (float)goal[1];
@@ -1281,6 +1623,7 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
 #pragma unroll
     for (int c = 0; c < 3; c++) s.goal[c * N + i] = goal[c];
     if (OBJ) store_obj(s, N, i, ob);
+    if constexpr (AO) ao_store(s, N, i, *L, ln);
     if (CONT) {
 #pragma unroll
         for (int k = 0; k < CACHE_N; k++) s.contacts[k * N + i] = L->cache[k][ln];
@@ -1289,13 +1632,19 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
     s.episode[i] = episode;
 }
 
-template <int OBJ>
+template <int OBJ, int AO>
 __global__ __launch_bounds__(64) void reset_kernel(const PgxDevModel* __restrict__ mdev, PgxDevEnv e, PgxDevState s,
                                                    const uint8_t* mask, const double* inject_goal,
                                                    const double* inject_obj, PgxDevOut o) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ln = threadIdx.x;
+    const int i = blockIdx.x * blockDim.x + ln;
     const int N = e.n_envs;
     if (i >= N) return;
+    ContactLds* L = nullptr;
+    if constexpr (AO) {
+        __shared__ ContactLds lds_buf;
+        L = &lds_buf;
+    }
     MRef m = *fresh((uint64_t)mdev);
     if (mask && !mask[i]) return;
     float q[NJ], qd[NJ];
@@ -1303,12 +1652,27 @@ __global__ __launch_bounds__(64) void reset_kernel(const PgxDevModel* __restrict
     ObjState ob;
     if (OBJ) load_obj(s, N, i, ob);
     uint32_t episode = s.episode[i];
-    reset_env<OBJ>(m, e, i, episode, inject_goal ? inject_goal + 3 * (size_t)i : nullptr,
-                   inject_obj ? inject_obj + 3 * (size_t)i : nullptr, q, qd, goal, ob);
     V3 pos, vel;
-    ee_state(m, q, qd, pos, vel);
+    if constexpr (AO) {
+#pragma unroll
+        for (int j = 0; j < NJ; j++) { q[j] = m.neutral_q[j]; qd[j] = 0.0f; }
+        ee_state(m, q, qd, pos, vel);
+        ao_caps(m, q, *L, ln);
+        ao_reset(e, *L, ln, e.env_id_offset + (uint64_t)i, episode, pos,
+                 inject_goal ? inject_goal + 3 * (size_t)i : nullptr,
+                 inject_obj ? inject_obj + 3 * AO_N * (size_t)i : nullptr, goal);
+        episode += 1;
+        ao_link_obs(*L, ln);
+    } else {
+        reset_env<OBJ>(m, e, i, episode, inject_goal ? inject_goal + 3 * (size_t)i : nullptr,
+                       inject_obj ? inject_obj + 3 * (size_t)i : nullptr, q, qd, goal, ob);
+        ee_state(m, q, qd, pos, vel);
+    }
     const V3 ag = OBJ ? ob.p : pos;
-    if (o.obs) write_obs<OBJ>(e, o.obs + (size_t)i * e.obs_dim, pos, vel, ob);
+    if (o.obs) {
+        if constexpr (AO) ao_write_obs(o.obs + (size_t)i * e.obs_dim, pos, vel, q, qd, *L, ln);
+        else write_obs<OBJ>(e, o.obs + (size_t)i * e.obs_dim, pos, vel, ob);
+    }
     if (o.ag) { o.ag[3 * (size_t)i] = ag.x; o.ag[3 * (size_t)i + 1] = ag.y; o.ag[3 * (size_t)i + 2] = ag.z; }
     if (o.dg) {
         o.dg[3 * (size_t)i] = (float)goal[0]; o.dg[3 * (size_t)i + 1] = (float)goal[1];
@@ -1323,6 +1687,7 @@ __global__ __launch_bounds__(64) void reset_kernel(const PgxDevModel* __restrict
 #pragma unroll
     for (int c = 0; c < 3; c++) s.goal[c * N + i] = goal[c];
     if (OBJ) store_obj(s, N, i, ob);
+    if constexpr (AO) ao_store(s, N, i, *L, ln);
 #pragma unroll
     for (int k = 0; k < CACHE_N; k++) s.contacts[k * N + i] = (k & 1) ? 0.0f : -1.0f;
     s.elapsed[i] = 0;
@@ -1359,14 +1724,15 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
                     const PgxDevOut& o, void* stream) {
     dim3 block(64), grid((e.n_envs + 63) / 64);
     hipStream_t st = (hipStream_t)stream;
-    const int variant = e.control * 4 + (e.has_object ? 2 : 0) + (e.contacts ? 1 : 0);
+    const int variant = e.ao ? 13 : e.control * 4 + (e.has_object ? 2 : 0) + (e.contacts ? 1 : 0);
     switch (variant) {
-        case 0: hipLaunchKernelGGL((step_kernel<0, 0, 0>), grid, block, 0, st, m, e, s, action, o); break;
-        case 1: hipLaunchKernelGGL((step_kernel<0, 0, 1>), grid, block, 0, st, m, e, s, action, o); break;
-        case 3: hipLaunchKernelGGL((step_kernel<0, 1, 1>), grid, block, 0, st, m, e, s, action, o); break;
-        case 4: hipLaunchKernelGGL((step_kernel<1, 0, 0>), grid, block, 0, st, m, e, s, action, o); break;
-        case 5: hipLaunchKernelGGL((step_kernel<1, 0, 1>), grid, block, 0, st, m, e, s, action, o); break;
-        case 7: hipLaunchKernelGGL((step_kernel<1, 1, 1>), grid, block, 0, st, m, e, s, action, o); break;
+        case 0: hipLaunchKernelGGL((step_kernel<0, 0, 0, 0>), grid, block, 0, st, m, e, s, action, o); break;
+        case 1: hipLaunchKernelGGL((step_kernel<0, 0, 1, 0>), grid, block, 0, st, m, e, s, action, o); break;
+        case 3: hipLaunchKernelGGL((step_kernel<0, 1, 1, 0>), grid, block, 0, st, m, e, s, action, o); break;
+        case 4: hipLaunchKernelGGL((step_kernel<1, 0, 0, 0>), grid, block, 0, st, m, e, s, action, o); break;
+        case 5: hipLaunchKernelGGL((step_kernel<1, 0, 1, 0>), grid, block, 0, st, m, e, s, action, o); break;
+        case 7: hipLaunchKernelGGL((step_kernel<1, 1, 1, 0>), grid, block, 0, st, m, e, s, action, o); break;
+        case 13: hipLaunchKernelGGL((step_kernel<1, 0, 1, 1>), grid, block, 0, st, m, e, s, action, o); break;
         default: return (int)hipErrorInvalidValue;   /* object without contacts: rejected at create */
     }
     return (int)hipGetLastError();
@@ -1375,10 +1741,12 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
 int pgx_launch_reset(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState& s, const uint8_t* mask,
                      const double* inject_goal, const double* inject_obj, const PgxDevOut& o, void* stream) {
     dim3 block(64), grid((e.n_envs + 63) / 64);
-    if (e.has_object)
-        hipLaunchKernelGGL(reset_kernel<1>, grid, block, 0, (hipStream_t)stream, m, e, s, mask, inject_goal, inject_obj, o);
+    if (e.ao)
+        hipLaunchKernelGGL((reset_kernel<0, 1>), grid, block, 0, (hipStream_t)stream, m, e, s, mask, inject_goal, inject_obj, o);
+    else if (e.has_object)
+        hipLaunchKernelGGL((reset_kernel<1, 0>), grid, block, 0, (hipStream_t)stream, m, e, s, mask, inject_goal, inject_obj, o);
     else
-        hipLaunchKernelGGL(reset_kernel<0>, grid, block, 0, (hipStream_t)stream, m, e, s, mask, inject_goal, inject_obj, o);
+        hipLaunchKernelGGL((reset_kernel<0, 0>), grid, block, 0, (hipStream_t)stream, m, e, s, mask, inject_goal, inject_obj, o);
     return (int)hipGetLastError();
 }
 

@@ -24,7 +24,7 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from . import abi
+from . import abi, reach_ao
 from ._native import PgxError, check, load
 from .model import load_model
 
@@ -82,6 +82,9 @@ def register_envs(max_ep_steps: int = 50) -> None:
             _REGISTRY[f"PandaPickAndPlace{cs}{rs}-v3"] = abi.EnvSpec(
                 task=abi.TASK_PICK_AND_PLACE, control=control, reward=reward, max_episode_steps=max_ep_steps,
                 block_gripper=False)
+    # panda_gym/__init__.py:15-20, 51-56; PandaReachAOEnv (panda_tasks.py:132-159) with TrainConfig
+    # defaults and scenario "reachao_rand" (the config this build runs)
+    _REGISTRY["PandaReachAO-v3"] = abi.EnvSpec.reach_ao(max_episode_steps=max_ep_steps)
 
 
 def registered_ids() -> List[str]:
@@ -102,6 +105,15 @@ def seeded_goal(env_spec: abi.EnvSpec, seed: Optional[int]) -> Optional[np.ndarr
     return None if r is None else r[0]
 
 
+_AO_GEOM: Dict[tuple, "reach_ao.RobotGeometry"] = {}
+
+
+def _ao_geometry(base_pos: tuple) -> "reach_ao.RobotGeometry":
+    if base_pos not in _AO_GEOM:
+        _AO_GEOM[base_pos] = reach_ao.RobotGeometry(load_model("panda_custom0"), base_pos)
+    return _AO_GEOM[base_pos]
+
+
 def seeded_reset(env_spec: abi.EnvSpec, seed: Optional[int]) -> Optional[Tuple[np.ndarray, Optional[np.ndarray]]]:
     """(goal, object position) of RobotTaskEnv.reset(seed): a fresh PCG64(SeedSequence(seed))
     (core.py:302), then the task's draws in its own order -- Reach reach.py:75-78; Push
@@ -109,6 +121,8 @@ def seeded_reset(env_spec: abi.EnvSpec, seed: Optional[int]) -> Optional[Tuple[n
     PickAndPlace pick_and_place.py:258-272 (goal noise, random() < 0.3 zeroes its z, object)."""
     if seed is None:
         return None
+    if env_spec.task == abi.TASK_REACH_AO:   # (goal, obstacle centres [6, 3])
+        return reach_ao.seeded_reset(seed, _ao_geometry(tuple(env_spec.base_pos)))
     rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed)))
     lo, hi = env_spec.goal_bounds()
     if env_spec.task == abi.TASK_REACH:
@@ -177,7 +191,10 @@ class PandaVecEnv:
                                            achieved_goal=Box(-10.0, 10.0, (3,)))
         self.action_space = Box(-1.0, 1.0, (self.action_dim,))
         self.distance_threshold = self.spec.distance_threshold
-        self.reward_type = "dense" if self.spec.reward == abi.REWARD_DENSE else "sparse"
+        if self.spec.task == abi.TASK_REACH_AO:
+            self.reward_type = "sparse_ao"   # ReachAO.compute_reward sparse/reach (reach_ao.py:1317-1320)
+        else:
+            self.reward_type = "dense" if self.spec.reward == abi.REWARD_DENSE else "sparse"
         self._snapshots: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
         self._next_snap = 0
         self._pending: Optional[torch.Tensor] = None
@@ -212,6 +229,8 @@ class PandaVecEnv:
             "goal": _view(v.goal, (3, n), torch.float64, self.device),
             "object": _view(v.object, (13, n), torch.float32, self.device),
             "contacts": _view(v.contacts, (2 * abi.CONTACT_SLOTS, n), torch.float32, self.device),
+            **({"obstacles": _view(v.obstacles, (4 * abi.AO_OBSTACLES, n), torch.float32, self.device)}
+               if v.obstacles else {}),
             "elapsed": _view(v.elapsed, (n,), torch.int32, self.device),
             "episode": _view(v.episode, (n,), torch.int32, self.device),
         }
@@ -232,8 +251,9 @@ class PandaVecEnv:
                 objects = np.stack([d[1] for d in draws])
         if goals is not None:
             inj = torch.as_tensor(np.asarray(goals, dtype=np.float64).reshape(self.num_envs, 3), device=self.device)
-        if objects is not None:
-            inj_obj = torch.as_tensor(np.asarray(objects, dtype=np.float64).reshape(self.num_envs, 3),
+        if objects is not None:   # object position [N,3] or ReachAO obstacle centres [N,6,3]
+            w = 3 * abi.AO_OBSTACLES if self.spec.task == abi.TASK_REACH_AO else 3
+            inj_obj = torch.as_tensor(np.asarray(objects, dtype=np.float64).reshape(self.num_envs, w),
                                       device=self.device)
         m = None
         if mask is not None:
@@ -318,7 +338,7 @@ class PandaVecEnv:
         ag = ag.to(self.device, torch.float32).reshape(-1, 3).contiguous()
         dg = dg.to(self.device, torch.float32).reshape(-1, 3).contiguous()
         out = torch.empty(ag.shape[0], dtype=torch.float32, device=self.device)
-        rt = abi.REWARD_DENSE if self.reward_type == "dense" else abi.REWARD_SPARSE
+        rt = abi.REWARD_CODES[self.reward_type]
         check(self.lib.pgx_compute_reward(C.c_void_p(ag.data_ptr()), C.c_void_p(dg.data_ptr()),
                                           C.c_int64(ag.shape[0]), rt, C.c_double(self.distance_threshold),
                                           C.c_void_p(out.data_ptr()), self._stream()), "pgx_compute_reward")

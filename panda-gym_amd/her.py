@@ -91,7 +91,7 @@ class HerReplayBuffer:
         cfg = abi.PgxReplayConfig()
         cfg.n_envs, cfg.capacity = self.n_envs, self.buffer_size
         cfg.obs_dim, cfg.action_dim = self.obs_dim, self.action_dim
-        cfg.reward_type = abi.REWARD_DENSE if self.reward_type == "dense" else abi.REWARD_SPARSE
+        cfg.reward_type = abi.REWARD_CODES[self.reward_type]
         cfg.strategy = STRATEGIES[goal_selection_strategy]
         cfg.distance_threshold, cfg.her_ratio, cfg.seed = self.distance_threshold, self.her_ratio, int(seed)
         self._cfg = cfg

@@ -118,7 +118,7 @@ class Model:
                 dofs.append(dof)
         return np.array(kinds, dtype=np.int32), np.array(dofs, dtype=np.int32)
 
-    def capsules(self, table_from_link: int = 1, object_from_link: int = 4) -> List[dict]:
+    def capsules(self, table_from_link: int = 1, object_from_link: int = 4, base_capsule: bool = False) -> List[dict]:
         """Contact geometry: every <collision> cylinder with the spheres capping its ends
         fused into a capsule, spheres not contained in a capsule as zero-length capsules.
 
@@ -154,9 +154,15 @@ class Model:
                     break
             if not inside:
                 caps.append(dict(link=s["link"], a=s["c"].copy(), b=s["c"].copy(), r=s["r"]))
+        if base_capsule:
+            # panda_link0's cylinder (r 0.06, length 0.03 along x) capped by its two spheres
+            # (panda.urdf:21-36), in the base frame; it only takes part in whole-robot distance
+            # queries (ReachAO's collision-free sampling), never in contacts
+            caps.append(dict(link=-1, a=np.array([-0.09, 0.0, 0.06]), b=np.array([-0.06, 0.0, 0.06]), r=0.06))
         out = []
         for c in sorted(caps, key=lambda c: c["link"]):
-            flags = (1 if c["link"] >= table_from_link else 0) | (2 if c["link"] >= object_from_link else 0)
+            flags = 0 if c["link"] < 0 else ((1 if c["link"] >= table_from_link else 0) |
+                                             (2 if c["link"] >= object_from_link else 0))
             out.append(dict(link=int(c["link"]), a=[float(x) for x in c["a"]], b=[float(x) for x in c["b"]],
                             r=float(c["r"]), flags=flags))
         return out

@@ -34,6 +34,8 @@ def _state_to_oracle(venv, ref):
     ref.episode[:] = st["episode"].cpu().numpy().view(np.uint32)
     ref.obj[:, :13] = st["object"].double().cpu().numpy().T
     ref.obj[:, 13:29] = st["contacts"].double().cpu().numpy().T
+    if "obstacles" in st:
+        ref.obj[:, 29:53] = st["obstacles"].double().cpu().numpy().T
 
 
 def _check_step(out_gpu, out_ref, goal):

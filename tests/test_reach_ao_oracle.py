@@ -1,0 +1,220 @@
+"""ReachAO (config 5) on the CPU: geometry, seeded reset, step semantics.
+
+The reference's distances come from pybullet getClosestPoints through the pyb_utils
+fork (absent here), so the restatement is pinned analytically: capsule/sphere and
+capsule/rounded-box distances against brute-force sampling, the host numpy geometry
+against the oracle's C geometry, the reset's rejection constraints, and the step's
+reward / termination / truncation rules of reach_ao.py and core.py.
+"""
+import numpy as np
+import pytest
+
+from panda_gym_amd import abi, reach_ao
+from panda_gym_amd.model import load_model
+
+KEEP = []
+
+
+def _cfg(n=1, seed=0):
+    model = abi.make_model(load_model("panda_custom0"), ee_link=11)
+    params = abi.default_sim_params()
+    cfg = abi.make_config(abi.EnvSpec.reach_ao(), n, model, params, seed=seed)
+    KEEP.append((model, params, cfg))
+    return cfg
+
+
+def _brute_capsule_box(A, B, r, c, h, m=reach_ao.MARGIN, n=20001):
+    t = np.linspace(0.0, 1.0, n)[:, None]
+    P = A + t * (B - A)
+    return float(np.min(reach_ao.box_sd(P, c, np.asarray(h) - m))) - m - r
+
+
+def test_capsule_sphere_matches_closed_form(oracle):
+    from oracle import oracle as O
+
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        A, B, C = rng.uniform(-0.3, 0.3, (3, 3))
+        r, R = rng.uniform(0.01, 0.06), 0.05
+        d, pa, pb = O.ao_capsule_sphere(A, B, r, C, R)
+        t = np.linspace(0, 1, 20001)[:, None]
+        brute = np.min(np.linalg.norm(A + t * (B - A) - C, axis=1)) - r - R
+        assert abs(d - brute) < 1e-6
+        assert abs(np.linalg.norm(pb - pa) - abs(d)) < 1e-9       # the point pair spans the distance
+        host = reach_ao.capsule_sphere_dist(A[None], B[None], np.array([r]), C, R)[0]
+        assert abs(host - d) < 1e-12
+
+
+def test_capsule_box_matches_brute_force(oracle):
+    from oracle import oracle as O
+
+    rng = np.random.default_rng(1)
+    h = np.array([0.05, 0.05, 0.05])
+    for k in range(300):
+        c = rng.uniform(-0.2, 0.2, 3)
+        A = c + rng.uniform(-0.25, 0.25, 3)
+        B = A + rng.uniform(-0.2, 0.2, 3) * (k % 5 != 0)         # every 5th a sphere (A == B)
+        r = rng.uniform(0.01, 0.06)
+        d, pa, pb = O.ao_capsule_box(A, B, r, c, h)
+        brute = _brute_capsule_box(A, B, r, c, h)
+        step = np.linalg.norm(B - A) / 20000                    # the sampling's resolution (1-Lipschitz)
+        assert brute - step - 1e-9 <= d <= brute + 1e-7        # ternary search: (2/3)^40 of |AB|
+        assert abs(np.linalg.norm(pb - pa) - abs(d)) < 1e-7
+        host = reach_ao.capsule_box_dist(A[None], B[None], np.array([r]), c, h)[0]
+        assert abs(host - d) < 1e-12
+
+
+def test_rounded_box_edges():
+    """The 1 mm box margin rounds the cuboid's edges: at a corner the distance is that of
+    the inner box's corner sphere, on a face it is the plain box distance."""
+    c, h = np.zeros(3), np.array([0.05, 0.05, 0.05])
+    face = np.array([0.2, 0.0, 0.0])
+    corner = np.array([0.2, 0.2, 0.2])
+    assert abs(reach_ao.rbox_sd(face, c, h) - 0.15) < 1e-15
+    want = np.linalg.norm(corner - (h - reach_ao.MARGIN)) - reach_ao.MARGIN
+    assert abs(reach_ao.rbox_sd(corner, c, h) - want) < 1e-15
+    assert reach_ao.rbox_sd(corner, c, h) > np.linalg.norm(corner - h)
+
+
+def test_link_distances_pick_the_closest_obstacle(oracle):
+    from oracle import oracle as O
+
+    cfg = _cfg()
+    q = np.array(abi.NEUTRAL_Q[:7])
+    geom = reach_ao.RobotGeometry(load_model("panda_custom0"))
+    obst = np.array([[0.3, 0.0, 0.5], [99.9, 99.9, -99.9], [0.0, 0.4, 0.3], [0.5, 0.1, 0.2],
+                     [99.9, 99.9, -99.9], [-0.3, -0.3, 0.4]])
+    dist, pa, pb, dtab = O.ao_link_distances(cfg, q, obst)
+    # brute force over the same capsules of each link (geometry from the host module)
+    links = [c["link"] for c in load_model("panda_custom0").capsules(base_capsule=True)]
+    for slot, link in enumerate([0, 1, 2, 3, 4, 5, 6, 7, 9]):
+        sel = [i for i, l in enumerate(links) if l == link]
+        best = np.inf
+        for o in range(6):
+            A, B, r = geom.A[sel], geom.B[sel], geom.r[sel]
+            if o < 3:
+                dd = reach_ao.capsule_sphere_dist(A, B, r, obst[o], 0.05)
+            else:
+                dd = reach_ao.capsule_box_dist(A, B, r, obst[o], (0.05,) * 3)
+            best = min(best, float(np.min(dd)))
+        assert abs(dist[slot] - best) < 1e-9, (slot, dist[slot], best)
+    assert dtab > 0.0
+
+
+def test_seeded_reset_constraints():
+    geom = reach_ao.RobotGeometry(load_model("panda_custom0"))
+    for seed in range(40):
+        goal, obst = reach_ao.seeded_reset(seed, geom)
+        g2, o2 = reach_ao.seeded_reset(seed, geom)
+        assert np.array_equal(goal, g2) and np.array_equal(obst, o2)
+        r = np.linalg.norm(goal)
+        assert 0.5 - 1e-12 <= r <= 0.8 + 1e-12 and goal[2] >= 0.0
+        assert reach_ao.rbox_sd(goal, reach_ao.TABLE_CENTER, reach_ao.TABLE_HALF) - 0.05 > 0.1
+        assert geom.distance(0, goal, 0.05) > 0.1
+        parked = np.all(obst == np.array(reach_ao.PARKED), axis=1)
+        assert parked.sum() in (1, 2)                        # integers(4, 6) active
+        for o in np.flatnonzero(~parked):
+            kind = reach_ao.AO_KIND[o]
+            assert geom.distance(kind, obst[o], 0.05) > 0.03
+            near = min(np.linalg.norm(obst[o] - goal), np.linalg.norm(obst[o] - geom.ee))
+            assert 0.1 - 1e-9 <= near                          # hollow sphere r >= 0.1 around a centre
+
+
+def test_seeded_reset_draw_order():
+    """The reset consumes the numpy stream in the reference's order: the draws of the
+    first accepted goal are the first three uniforms of the seeded Generator."""
+    geom = reach_ao.RobotGeometry(load_model("panda_custom0"))
+    for seed in range(20):
+        goal, _ = reach_ao.seeded_reset(seed, geom)
+        rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed)))
+        cand = []
+        for _ in range(50):
+            phi, theta = rng.uniform(0, 2 * np.pi), rng.uniform(0, 0.5 * np.pi)
+            r = np.cbrt(rng.uniform(0.5 ** 3, 0.8 ** 3))
+            cand.append([r * np.sin(theta) * np.cos(phi), r * np.sin(theta) * np.sin(phi), r * np.cos(theta)])
+        assert any(np.array_equal(goal, c) for c in cand)
+
+
+def test_oracle_reset_and_obs_layout(oracle):
+    from oracle import oracle as O
+
+    cfg = _cfg(n=8, seed=5)
+    env = O.OracleVecEnv(cfg, 8)
+    b = env.reset()
+    assert b["obs"].shape == (8, 56)
+    assert np.allclose(b["obs"][:, 6:13], np.array(abi.NEUTRAL_Q[:7], np.float32))
+    assert np.all(b["obs"][:, 13:20] == 0)
+    assert np.array_equal(b["ag"], b["obs"][:, 0:3])
+    n_act = env.active.sum(1)
+    assert set(n_act.tolist()) <= {4.0, 5.0}
+    for e in range(8):
+        dist, _, _, _ = O.ao_link_distances(cfg, env.q[e], env.obstacles[e])
+        assert np.allclose(b["obs"][e, 20:29], dist.astype(np.float32))
+        u = b["obs"][e, 29:56].reshape(9, 3)
+        assert np.allclose(np.linalg.norm(u, axis=1), 1.0, atol=1e-6)
+        assert dist.min() > 0.03 - 1e-9                       # collision-free reset
+
+
+def test_oracle_injected_reset(oracle):
+    from oracle import oracle as O
+
+    cfg = _cfg(n=2)
+    env = O.OracleVecEnv(cfg, 2)
+    goal = np.array([[0.4, 0.2, 0.4], [0.3, -0.3, 0.5]])
+    obst = np.tile(np.array([[0.5, 0.0, 0.6], [99.9, 99.9, -99.9], [0.2, 0.4, 0.3], [0.6, 0.2, 0.2],
+                             [-0.3, 0.3, 0.3], [99.9, 99.9, -99.9]]), (2, 1, 1))
+    env.reset(inject_goal=goal, inject_obj=obst)
+    assert np.array_equal(env.goal, goal)
+    assert np.array_equal(env.obstacles, obst)
+    assert np.array_equal(env.active[0], [1, 0, 1, 1, 1, 0])
+
+
+def test_collision_truncates_with_penalty(oracle):
+    """An obstacle right in front of the moving link: the substep loop stops at the first
+    contact, the step is truncated with reward -1 - 100 and the env auto-resets."""
+    from oracle import oracle as O
+
+    cfg = _cfg(n=1)
+    env = O.OracleVecEnv(cfg, 1)
+    q0 = np.array(abi.NEUTRAL_Q[:7])
+    from oracle.oracle import fk
+    com, rot, org = fk(cfg.model.contents, q0)
+    ee = com[11]
+    obst = np.array([[ee[0], ee[1] + 0.14, ee[2]]] + [[99.9, 99.9, -99.9]] * 5)
+    env.reset(inject_goal=np.array([[0.5, 0.3, 0.3]]), inject_obj=obst[None])
+    first = None
+    for k in range(10):
+        b = env.step(np.array([[1.0, 0, 0, 0, 0, 0, 0]], np.float32))   # swing joint 1 towards +y
+        if b["truncated"][0]:
+            first = k
+            break
+    assert first is not None
+    assert b["reward"][0] == -101.0 and not b["terminated"][0]
+    assert b["terminal_obs"][0, 20:29].min() <= 1e-3          # the terminal obs touches the obstacle
+    assert np.all(b["obs"][0, 13:20] == 0)                     # auto-reset: neutral pose at rest
+
+
+def test_success_terminates(oracle):
+    from oracle import oracle as O
+    from oracle.oracle import fk
+
+    cfg = _cfg(n=1)
+    env = O.OracleVecEnv(cfg, 1)
+    com, _, _ = fk(cfg.model.contents, np.array(abi.NEUTRAL_Q[:7]))
+    far = np.array([[99.9, 99.9, -99.9]] * 6)
+    env.reset(inject_goal=com[11][None] + 0.01, inject_obj=far[None])
+    b = env.step(np.zeros((1, 7), np.float32))
+    assert b["success"][0] and b["terminated"][0] and not b["truncated"][0]
+    assert b["reward"][0] == 0.0 and not np.signbit(b["reward"][0])     # -1 + 1 = +0.0
+
+
+def test_reach_ao_compute_reward(oracle):
+    from oracle.her import compute_reward_f32 as her_reward
+    from oracle.oracle import compute_reward_f32
+
+    ag = np.array([[0.0, 0.0, 0.0], [0.0, 0.0, 0.1], [0.03, 0.0, 0.0]], np.float32)
+    dg = np.zeros((3, 3), np.float32)
+    thr = float(np.float32(0.05))
+    r = compute_reward_f32(ag, dg, abi.REWARD_SPARSE_AO, thr)
+    assert r.tolist() == [0.0, -1.0, 0.0] and not np.signbit(r[0])
+    assert np.array_equal(her_reward(ag, dg, 2, thr), r)
