@@ -1103,6 +1103,16 @@ static cdist_t capsule_box(const double* A, const double* B, double r, const dou
     for (int i = 0; i < 3; i++) P[i] = A[i] + t * ab[i];
     double sd = box_sd(P, c, h), q[3], n[3];
     if (sd > 0) {
+        /* two alternating projections (box -> segment): the search cannot resolve t where
+         * the distance is flat to second order (a segment passing an edge or a corner);
+         * each projection can only shorten the pair (|P' - q| <= |P - q|) and pins it */
+        for (int it = 0; it < 2 && v3_dot(ab, ab) > 0; it++) {
+            for (int i = 0; i < 3; i++) q[i] = clampd(P[i], c[i] - h[i], c[i] + h[i]);
+            double tq = clampd(((q[0] - A[0]) * ab[0] + (q[1] - A[1]) * ab[1] + (q[2] - A[2]) * ab[2]) / v3_dot(ab, ab),
+                               0.0, 1.0);
+            for (int i = 0; i < 3; i++) P[i] = A[i] + tq * ab[i];
+        }
+        sd = box_sd(P, c, h);
         for (int i = 0; i < 3; i++) q[i] = clampd(P[i], c[i] - h[i], c[i] + h[i]);
         double v[3] = {q[0] - P[0], q[1] - P[1], q[2] - P[2]}, len = v3_norm(v);
         for (int i = 0; i < 3; i++) n[i] = len > 0 ? v[i] / len : 0.0;

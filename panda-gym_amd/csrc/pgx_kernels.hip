@@ -1228,8 +1228,19 @@ __device__ __forceinline__ float capsule_box(V3 A, V3 B, float r, V3 c, V3 hf, V
             else lo = m1;
         }
     }
-    const V3 P = A + (seg ? 0.5f * (lo + hi) : 0.0f) * ab;
-    const float sd = box_sd(P, c, h);
+    V3 P = A + (seg ? 0.5f * (lo + hi) : 0.0f) * ab;
+    float sd = box_sd(P, c, h);
+    if (seg && sd > 0.0f) {
+        /* two alternating projections (box -> segment): the search cannot resolve t where
+         * the distance is flat to second order (a segment passing an edge or a corner);
+         * each can only shorten the pair and pins it */
+        for (int it = 0; it < 2; it++) {
+            const V3 q = v3(fminf(fmaxf(P.x, c.x - h.x), c.x + h.x), fminf(fmaxf(P.y, c.y - h.y), c.y + h.y),
+                            fminf(fmaxf(P.z, c.z - h.z), c.z + h.z));
+            P = seg_closest(A, B, q);
+        }
+        sd = box_sd(P, c, h);
+    }
     const float d = sd - kAoMargin - r;
     if (VEC) {
         V3 n;

@@ -81,7 +81,16 @@ def capsule_box_dist(A: np.ndarray, B: np.ndarray, r: np.ndarray, c: np.ndarray,
         hi = np.where(left, m2, hi)
         lo = np.where(left, lo, m1)
     t = np.where(nz, 0.5 * (lo + hi), 0.0)
-    return box_sd(A + t[:, None] * ab, c, hi_box) - MARGIN - r
+    P = A + t[:, None] * ab
+    outside = (box_sd(P, c, hi_box) > 0) & nz
+    # two alternating projections (box -> segment) where the distance is flat to second order
+    l2 = np.sum(ab * ab, axis=-1)
+    for _ in range(2):
+        q = np.clip(P, c - hi_box, c + hi_box)
+        num = (q[:, 0] - A[:, 0]) * ab[:, 0] + (q[:, 1] - A[:, 1]) * ab[:, 1] + (q[:, 2] - A[:, 2]) * ab[:, 2]
+        tq = np.clip(num / np.where(nz, l2, 1.0), 0.0, 1.0)
+        P = np.where(outside[:, None], A + tq[:, None] * ab, P)
+    return box_sd(P, c, hi_box) - MARGIN - r
 
 
 class RobotGeometry:
