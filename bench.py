@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--her-calls", type=int, default=50)
     ap.add_argument("--no-tasks", action="store_true", help="skip the Push / PickAndPlace legs (configs[2], [3])")
     ap.add_argument("--task-steps", type=int, default=200)
+    ap.add_argument("--no-ao", action="store_true", help="skip the sharded ReachAO leg (configs[4])")
+    ap.add_argument("--ao-envs", type=int, default=8192, help="ReachAO envs per GPU (65536 over 8 GPUs)")
     return ap.parse_args()
 
 
@@ -191,6 +193,37 @@ def task_leg(dev, env_id: str, n: int, steps: int, contacts: bool = True):
             "policy": "device Philox random actions (sample_actions + step per step)"}
 
 
+def sharded_leg(dev, env_id: str, n: int, steps: int, warmup: int, dist, rank: int, world: int):
+    """Every rank steps its own shard of ``n`` envs (global ids [rank*n, (rank+1)*n)); the timed
+    region is barrier-bracketed and the max over ranks is taken, like the headline leg.  Used for
+    BASELINE configs[4] (ReachAO, 65536 envs as 8192 per GPU on 8 GPUs)."""
+    import panda_gym_amd as pg
+    from panda_gym_amd.shard import max_over_ranks, shard_offset
+
+    venv = pg.PandaVecEnv(env_id, num_envs=n, device=dev, seed=1, env_id_offset=shard_offset(rank, n))
+    venv.reset_tensors()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(warmup):
+        venv.step_tensors(venv.sample_actions())
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        venv.step_tensors(venv.sample_actions())
+    torch.cuda.synchronize(dev)
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, dist, dev)
+    venv.close()
+    return {"env_id": env_id, "envs_per_gpu": n, "global_envs": world * n, "n_gpus": world,
+            "value": world * n * steps / elapsed, "unit": "env-steps/s", "ms_per_step": elapsed / steps * 1e3,
+            "steps": steps, "warmup": warmup, "scaling": "weak",
+            "policy": "device Philox random actions, in-kernel collision / success / TimeLimit auto-reset"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -248,6 +281,9 @@ def main():
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     kernel_ms = ev0.elapsed_time(ev1) / args.kernel_launches
+    # configs[4]: ReachAO sharded over every rank (collective timing: all ranks take part)
+    ao = None if args.no_ao else sharded_leg(dev, "PandaReachAO-v3", args.ao_envs, args.task_steps, 20, dist, rank,
+                                            world)
 
     if rank == 0:
         alg_bytes = ALG_BYTES_PER_ENV_STEP * E
@@ -283,6 +319,8 @@ def main():
             "episode_stats_last_step": {"truncated": float(stats[0]), "success": float(stats[1]),
                                         "reward_sum": float(stats[2])},
         }
+        if ao is not None:
+            line["reach_ao"] = ao
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(venv, args.cpu_baseline_seconds)
         if world == 1 and not args.no_her:
@@ -290,7 +328,6 @@ def main():
         if world == 1 and not args.no_tasks:
             line["tasks"] = [task_leg(dev, "PandaPush-v3", 4096, args.task_steps),               # configs[2]
                              task_leg(dev, "PandaPickAndPlace-v3", 16384, args.task_steps),      # configs[3]
-                             task_leg(dev, "PandaReachAO-v3", 8192, args.task_steps),            # configs[4] / GPU
                              task_leg(dev, args.env_id, E, args.task_steps, contacts=False)]     # no table
         print(json.dumps(line), flush=True)
     venv.close()

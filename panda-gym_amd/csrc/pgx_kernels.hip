@@ -982,32 +982,36 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
         }
     };
     const bool any_contact = CONT && __any(n0 > 0 || n1 > 0);
+    /* Sweeps alternate direction (Bullet reverses the row order on even iterations); the
+     * loop body holds one even (reverse) and one odd (forward) sweep, so no value has to
+     * be merged from two branch arms (that cost ~35 v_mov per sweep). */
+    const int n_it = m.num_iterations;
     if (__all(far)) {
-        for (int it = 0; it < m.num_iterations; it++) {
+        for (int it = 0; it < n_it; it += 2) {
             float resid = 0.0f;
-            if (it & 1) {
 #pragma unroll
-                for (int r = 0; r < PGX_N_ROWS; r++)
-                    if ((kPgxRowCode[r] >> 4) == 0) row(r, resid);
-            } else {
+            for (int r = PGX_N_ROWS - 1; r >= 0; r--)
+                if ((kPgxRowCode[r] >> 4) == 0) row(r, resid);
+            if (CONT && any_contact) contact_rows(resid);
+            if (resid * resid <= m.residual_thr || it + 1 >= n_it) break;
+            resid = 0.0f;
 #pragma unroll
-                for (int r = PGX_N_ROWS - 1; r >= 0; r--)
-                    if ((kPgxRowCode[r] >> 4) == 0) row(r, resid);
-            }
+            for (int r = 0; r < PGX_N_ROWS; r++)
+                if ((kPgxRowCode[r] >> 4) == 0) row(r, resid);
             if (CONT && any_contact) contact_rows(resid);
             if (resid * resid <= m.residual_thr) break;
         }
     } else {
         init_limit_rows();
-        for (int it = 0; it < m.num_iterations; it++) {
+        for (int it = 0; it < n_it; it += 2) {
             float resid = 0.0f;
-            if (it & 1) {
 #pragma unroll
-                for (int r = 0; r < PGX_N_ROWS; r++) row(r, resid);
-            } else {
+            for (int r = PGX_N_ROWS - 1; r >= 0; r--) row(r, resid);
+            if (CONT && any_contact) contact_rows(resid);
+            if (resid * resid <= m.residual_thr || it + 1 >= n_it) break;
+            resid = 0.0f;
 #pragma unroll
-                for (int r = PGX_N_ROWS - 1; r >= 0; r--) row(r, resid);
-            }
+            for (int r = 0; r < PGX_N_ROWS; r++) row(r, resid);
             if (CONT && any_contact) contact_rows(resid);
             if (resid * resid <= m.residual_thr) break;
         }
