@@ -22,6 +22,13 @@
 #define D PGX_MAX_DOFS
 
 /* ----------------------------------------------------------------- small vec */
+/* diagnostics (tools/diag_iterations.py): histograms of PGS sweeps [0,64), contact
+ * points per substep [64,80) and IK iterations [80,112); not part of the restatement */
+int64_t pgxo_diag_hist[112];
+void pgxo_diag_read(int64_t* out, int clear) {
+    for (int i = 0; i < 112; i++) { out[i] = pgxo_diag_hist[i]; if (clear) pgxo_diag_hist[i] = 0; }
+}
+
 static void v3_cross(const double* a, const double* b, double* o) {
     double x = a[1] * b[2] - a[2] * b[1];
     double y = a[2] * b[0] - a[0] * b[2];
@@ -678,6 +685,8 @@ static void substep_impl(const pgx_model* m, const pgx_sim_params* p, const doub
         if (!(p->flags & PGX_FLAG_NO_RESIDUAL_EXIT) && resid <= p->residual_threshold) break;
     }
     if (st) st->solver_iterations = it_used;
+    pgxo_diag_hist[it_used < 63 ? it_used : 63]++;
+    pgxo_diag_hist[64 + (ncon < 15 ? ncon : 15)]++;
     double vn[D];
     for (int d = 0; d < nd; d++) vn[d] = clampd(vu[d] + dv[d], -p->max_coord_vel, p->max_coord_vel);
     if (p->flags & PGX_FLAG_CONSTRAINT_PASS_BIAS) {
@@ -853,6 +862,7 @@ int pgxo_ik(const pgx_model* m, const pgx_sim_params* p, const double base[3], c
     }
     if (it == 0) memcpy(q_out, q_start, sizeof(double) * nd);
     if (st) { st->ik_iterations = it; st->ik_residual = diff; }
+    pgxo_diag_hist[80 + (it < 31 ? it : 31)]++;
     return it;
 }
 

@@ -58,6 +58,7 @@ struct PgxDevEnv {
     int32_t ao;                    /* ReachAO (obstacles, per-substep collision check) */
     int32_t terminate_on_success;
     double collision_reward;
+    int32_t lanes_per_env;         /* step layout: 1 (env per lane) or 16 (env per DPP row) */
 };
 
 struct PgxDevState {

@@ -29,6 +29,17 @@
 #include "pgx_model_consts.h"
 #include "pgx_rows.h"
 
+#ifdef PGX_PROF
+__device__ unsigned long long pgx_prof_counters[16];
+extern "C" int pgx_prof_read(unsigned long long* out, int clear) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(pgx_prof_counters), sizeof(unsigned long long) * 16);
+    if (e == hipSuccess && clear) {
+        unsigned long long z[16] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(pgx_prof_counters), z, sizeof z);
+    }
+    return (int)e;
+}
+#endif
 namespace {
 
 constexpr int NJ = PGX_NJ;
@@ -47,6 +58,24 @@ __device__ __forceinline__ MPtr fresh(uint64_t addr) {
     return (MPtr)addr;
 }
 __device__ __forceinline__ MPtr fresh(MPtr p) { return fresh((uint64_t)p); }
+
+/* Phase profile (build with -DPGX_PROF, tools/prof_phases.py): per-wave s_memtime
+ * deltas accumulated in LDS by phase, summed over waves into pgx_prof_counters at the
+ * end of the launch.  Compiled out of the product library. */
+#ifdef PGX_PROF
+__shared__ unsigned long long g_prof[16];
+__shared__ unsigned long long g_prof_t;
+__device__ __forceinline__ void prof_mark(int k) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    g_prof[k] += t - g_prof_t;
+    g_prof_t = t;
+}
+#define PGX_PROF_MARK(k) prof_mark(k)
+#define PGX_PROF_COUNT(k, v) (g_prof[k] += (unsigned long long)(v))
+#else
+#define PGX_PROF_MARK(k) ((void)0)
+#define PGX_PROF_COUNT(k, v) ((void)0)
+#endif
 
 struct V3 {
     float x, y, z;
@@ -342,26 +371,28 @@ constexpr int CG = 4;
 constexpr int CACHE_N = 2 * PGX_CONTACT_SLOTS;
 constexpr float kTableIdLimit = 32.0f;   /* robot feature ids < 32: capsule end vs table/plane */
 
-struct ContactLds {
+template <int W>
+struct ContactLdsT {
     /* group 0: object vertices vs table / plane (normal +z) */
-    float4 g0q[CG][4][64];         /* [0] = contact point - object COM; [1 + dir] = (jinv, den, rhs, lambda) */
-    float g0d[CG][64], g0id[CG][64];
+    float4 g0q[CG][4][W];         /* [0] = contact point - object COM; [1 + dir] = (jinv, den, rhs, lambda) */
+    float g0d[CG][W], g0id[CG][W];
     /* group 1: robot vs table / plane / object */
-    float g1p[CG][3][64];          /* point on the robot */
-    float g1n[CG][3][64];          /* normal, from the other body to the robot */
-    float g1rb[CG][3][64];         /* object contacts: point on the object - object COM */
-    float g1d[CG][64], g1id[CG][64];
-    int g1j[CG][64];               /* arm joint carrying the robot link */
+    float g1p[CG][3][W];          /* point on the robot */
+    float g1n[CG][3][W];          /* normal, from the other body to the robot */
+    float g1rb[CG][3][W];         /* object contacts: point on the object - object COM */
+    float g1d[CG][W], g1id[CG][W];
+    int g1j[CG][W];               /* arm joint carrying the robot link */
     /* per direction: (J0..3) (J4..6, jinv) (R0..3) (R4..6, den) (cl, rhs) (ca, lambda) with
      * J the robot Jacobian row, R = M^-1 J^T, (cl, ca) the object part (0 against the table) */
-    float4 g1q[CG][3][6][64];
-    int cnt[2][64];
-    float cache[CACHE_N][64];      /* (feature id, normal impulse) x 4 per group */
-    float capA[PGX_NCAP][3][64], capB[PGX_NCAP][3][64];   /* capsule end points, world */
+    float4 g1q[CG][3][6][W];
+    int cnt[2][W];
+    float cache[CACHE_N][W];      /* (feature id, normal impulse) x 4 per group */
+    float capA[PGX_NCAP][3][W], capB[PGX_NCAP][3][W];   /* capsule end points, world */
     /* ReachAO: obstacle centres, per collision link the closest distance and unit vector */
-    float aoC[PGX_AO_OBSTACLES][3][64];
-    float aoD[PGX_AO_LINKS][64], aoU[PGX_AO_LINKS][3][64];
+    float aoC[PGX_AO_OBSTACLES][3][W];
+    float aoD[PGX_AO_LINKS][W], aoU[PGX_AO_LINKS][3][W];
 };
+using ContactLds = ContactLdsT<64>;   /* one env per lane */
 
 struct ObjState {
     V3 p, v, w;
@@ -386,7 +417,8 @@ __device__ __forceinline__ float ground_z(const PgxDevEnv& e, float x, float y) 
 }
 
 /* keep the CG deepest candidates of group 0 (stable: an equal depth does not displace) */
-__device__ __forceinline__ void g0_insert(ContactLds& L, int ln, float d, float id, V3 r) {
+template <class LT>
+__device__ __forceinline__ void g0_insert(LT& L, int ln, float d, float id, V3 r) {
     int c = L.cnt[0][ln], pos;
     if (c < CG) { pos = c; L.cnt[0][ln] = c + 1; }
     else if (d < L.g0d[CG - 1][ln]) pos = CG - 1;
@@ -400,7 +432,8 @@ __device__ __forceinline__ void g0_insert(ContactLds& L, int ln, float d, float 
     L.g0d[pos][ln] = d; L.g0id[pos][ln] = id;
     L.g0q[pos][0][ln] = make_float4(r.x, r.y, r.z, 0.0f);
 }
-__device__ __forceinline__ void g1_copy(ContactLds& L, int ln, int to, int from) {
+template <class LT>
+__device__ __forceinline__ void g1_copy(LT& L, int ln, int to, int from) {
     L.g1d[to][ln] = L.g1d[from][ln];
     L.g1id[to][ln] = L.g1id[from][ln];
     L.g1j[to][ln] = L.g1j[from][ln];
@@ -410,7 +443,8 @@ __device__ __forceinline__ void g1_copy(ContactLds& L, int ln, int to, int from)
         L.g1rb[to][k][ln] = L.g1rb[from][k][ln];
     }
 }
-__device__ __forceinline__ void g1_insert(ContactLds& L, int ln, float d, float id, int j, V3 p, V3 n, V3 rb) {
+template <class LT>
+__device__ __forceinline__ void g1_insert(LT& L, int ln, float d, float id, int j, V3 p, V3 n, V3 rb) {
     int c = L.cnt[1][ln], pos;
     if (c < CG) { pos = c; L.cnt[1][ln] = c + 1; }
     else if (d < L.g1d[CG - 1][ln]) pos = CG - 1;
@@ -422,7 +456,8 @@ __device__ __forceinline__ void g1_insert(ContactLds& L, int ln, float d, float 
     L.g1rb[pos][0][ln] = rb.x; L.g1rb[pos][1][ln] = rb.y; L.g1rb[pos][2][ln] = rb.z;
 }
 /* rows are ordered by feature id (insertion sort of <= 4 entries, via a spare slot-free swap) */
-__device__ __forceinline__ void sort_groups(ContactLds& L, int ln) {
+template <class LT>
+__device__ __forceinline__ void sort_groups(LT& L, int ln) {
     const int c0 = L.cnt[0][ln];
     for (int i = 1; i < c0; i++)
         for (int j = i; j > 0 && L.g0id[j][ln] < L.g0id[j - 1][ln]; j--) {
@@ -458,8 +493,8 @@ __device__ __forceinline__ V3 mul_t(const M3& A, V3 v) {
 /* Robot capsules against the table/plane (end spheres) and the object (spheres sampled
  * along the axis), from the world end points the FK pass left in LDS.  A runtime loop
  * over the capsule table (wave-uniform index: scalar loads) keeps the code compact. */
-template <int OBJ>
-__device__ __forceinline__ void robot_contacts(const PgxDevEnv& e, float tau, ContactLds& L, int ln, const ObjState& ob,
+template <int OBJ, class LT>
+__device__ __forceinline__ void robot_contacts(const PgxDevEnv& e, float tau, LT& L, int ln, const ObjState& ob,
                                             const M3& Rc) {
     for (int c = 0; c < PGX_NCAP; c++) {
         const V3 A = v3(L.capA[c][0][ln], L.capA[c][1][ln], L.capA[c][2][ln]);
@@ -523,15 +558,15 @@ __device__ __forceinline__ void robot_contacts(const PgxDevEnv& e, float tau, Co
 }
 
 /* world end points of the capsules carried by arm joint j (compile-time walk) */
-template <int C = 0>
-__device__ __forceinline__ void link_capsules(int j, ContactLds& L, int ln, const M3& R, V3 oj) {
+template <int C = 0, class LT>
+__device__ __forceinline__ void link_capsules(int j, LT& L, int ln, const M3& R, V3 oj) {
     if constexpr (C < PGX_NCAP) {
         if (kCapJ[C] == j) {
             const V3 A = oj + mulc(R, kCapA[C]), B = oj + mulc(R, kCapB[C]);
             L.capA[C][0][ln] = A.x; L.capA[C][1][ln] = A.y; L.capA[C][2][ln] = A.z;
             L.capB[C][0][ln] = B.x; L.capB[C][1][ln] = B.y; L.capB[C][2][ln] = B.z;
         }
-        link_capsules<C + 1>(j, L, ln, R, oj);
+        link_capsules<C + 1, LT>(j, L, ln, R, oj);
     }
 }
 
@@ -545,10 +580,20 @@ __device__ __forceinline__ void link_capsules(int j, ContactLds& L, int ln, cons
  *   qd = clamp(qd_u + M^-1 J^T lambda); q += dt*qd   (constraint pass, stepPositions)
  *   object: p += dt v, orientation by the exponential map of w dt
  * M by composite-rigid-body, b by Newton-Euler with Bullet's link damping. */
-template <int OBJ, int CONT>
-__device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, float* qd, const float* tq,
-                                        ObjState& ob, ContactLds* Lp, int ln) {
-    MRef m = *fresh(mp);
+/* Per-substep dynamics shared by both solver layouts: contact detection at the current
+ * poses (CONT), FK fused with the per-link terms, Newton-Euler bias, CRBA mass matrix,
+ * Cholesky, the unconstrained velocities vu = clamp(qd + dt M^-1 (-b)) and M^-1 (lower
+ * triangle); the object's unconstrained velocities (OBJ). */
+struct Dyn {
+    V3 z[NJ], o[NJ];
+    float Mi[NJ][NJ];
+    float vu[NJ];
+    V3 vcu, wcu;
+};
+
+template <int OBJ, int CONT, class LT>
+__device__ __forceinline__ void substep_dyn(MRef m, const PgxDevEnv& e, const float* q, const float* qd,
+                                            const ObjState& ob, LT* Lp, int ln, Dyn& D) {
     M3 Rc;
     if (OBJ) Rc = quat_mat(ob);
     if (CONT) { Lp->cnt[0][ln] = 0; Lp->cnt[1][ln] = 0; }
@@ -564,7 +609,9 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
     }
     /* FK fused with the per-link quantities the dynamics need, so the 3x3
      * rotations die immediately (only panda_link7's survives for its group). */
-    V3 z[NJ], o[NJ], c[NJ];
+    V3 (&z)[NJ] = D.z;
+    V3 (&o)[NJ] = D.o;
+    V3 c[NJ];
     S3 Iw[NJ];
     M3 R6;
     {
@@ -596,6 +643,7 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
         robot_contacts<OBJ>(e, m.contact_dist, *Lp, ln, ob, Rc);
         sort_groups(*Lp, ln);
     }
+    PGX_PROF_MARK(1);
     const V3 g = v3(m.gravity[0], m.gravity[1], m.gravity[2]);
 
     /* forward Newton-Euler (qdd = 0) fused with the link wrenches at the COM
@@ -680,7 +728,7 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
         }
     }
     chol7(Mt);
-    float vu[NJ];
+    float (&vu)[NJ] = D.vu;
     {
         float qdd[NJ];
         chol7_solve(Mt, nb, qdd);
@@ -689,7 +737,7 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
     }
 
     /* M^-1 = L^-T L^-1 (symmetric, lower triangle kept) */
-    float Mi[NJ][NJ];
+    float (&Mi)[NJ][NJ] = D.Mi;
     {
         float X[NJ][NJ];
 #pragma unroll
@@ -713,15 +761,54 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
                 Mi[i][jj] = s;
             }
     }
-#define MINV(a, b) ((a) >= (b) ? Mi[a][b] : Mi[b][a])
 
     /* object: unconstrained velocities (btMultiBody floating base) */
-    V3 vcu = v3(0, 0, 0), wcu = v3(0, 0, 0);
+    V3& vcu = D.vcu;
+    V3& wcu = D.wcu;
+    vcu = v3(0, 0, 0);
+    wcu = v3(0, 0, 0);
     if (OBJ) {
         const float vn = norm(ob.v), wn = norm(ob.w);
         vcu = ob.v + m.dt * (g - (m.lin_damp + m.lin_damp * vn) * ob.v - cross(ob.w, ob.v));
         wcu = ob.w - (m.dt * (m.ang_damp + m.ang_damp * wn)) * ob.w;
     }
+}
+
+/* floating-base object: v, w after the constraint pass; p += dt v, orientation by the
+ * exponential map (btMultiBody::stepPositionsMultiDof) */
+__device__ __forceinline__ void object_integrate(MRef m, ObjState& ob, V3 v, V3 w) {
+    ob.v = v;
+    ob.w = w;
+    ob.p = ob.p + m.dt * ob.v;
+    /* btMultiBody::stepPositionsMultiDof, base: exponential map of w dt */
+    float ang = norm(ob.w);
+    if (ang * m.dt > 0.39269908f) ang = 0.39269908f * m.inv_dt;
+    const float hdt = 0.5f * m.dt;
+    const float f = ang < 0.001f ? (hdt - m.dt * m.dt * m.dt * 0.020833333333f * ang * ang)
+                                 : __sinf(ang * hdt) * fast_rcp(ang);
+    const float ax = ob.w.x * f, ay = ob.w.y * f, az = ob.w.z * f, aw = __cosf(ang * hdt);
+    /* dq * q (Hamilton, (x,y,z,w)) */
+    const float nx = aw * ob.qx + ax * ob.qw + ay * ob.qz - az * ob.qy;
+    const float ny = aw * ob.qy + ay * ob.qw + az * ob.qx - ax * ob.qz;
+    const float nz = aw * ob.qz + az * ob.qw + ax * ob.qy - ay * ob.qx;
+    const float nw = aw * ob.qw - ax * ob.qx - ay * ob.qy - az * ob.qz;
+    const float inn = __builtin_amdgcn_rsqf(nx * nx + ny * ny + nz * nz + nw * nw);
+    ob.qx = nx * inn; ob.qy = ny * inn; ob.qz = nz * inn; ob.qw = nw * inn;
+}
+
+template <int OBJ, int CONT>
+__device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, float* qd, const float* tq,
+                                        ObjState& ob, ContactLds* Lp, int ln) {
+    MRef m = *fresh(mp);
+    Dyn D;
+    substep_dyn<OBJ, CONT>(m, e, q, qd, ob, Lp, ln, D);
+    const V3 (&z)[NJ] = D.z;
+    const V3 (&o)[NJ] = D.o;
+    const float (&Mi)[NJ][NJ] = D.Mi;
+    const float (&vu)[NJ] = D.vu;
+    const V3 vcu = D.vcu, wcu = D.wcu;
+#define MINV(a, b) ((a) >= (b) ? Mi[a][b] : Mi[b][a])
+    PGX_PROF_MARK(2);
     float dv[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; j++) dv[j] = 0.0f;
@@ -986,6 +1073,8 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
      * loop body holds one even (reverse) and one odd (forward) sweep, so no value has to
      * be merged from two branch arms (that cost ~35 v_mov per sweep). */
     const int n_it = m.num_iterations;
+    PGX_PROF_MARK(3);
+    PGX_PROF_COUNT(9, 1);
     if (__all(far)) {
         for (int it = 0; it < n_it; it += 2) {
             float resid = 0.0f;
@@ -993,30 +1082,37 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
             for (int r = PGX_N_ROWS - 1; r >= 0; r--)
                 if ((kPgxRowCode[r] >> 4) == 0) row(r, resid);
             if (CONT && any_contact) contact_rows(resid);
+            PGX_PROF_COUNT(8, 1);
             if (resid * resid <= m.residual_thr || it + 1 >= n_it) break;
             resid = 0.0f;
 #pragma unroll
             for (int r = 0; r < PGX_N_ROWS; r++)
                 if ((kPgxRowCode[r] >> 4) == 0) row(r, resid);
             if (CONT && any_contact) contact_rows(resid);
+            PGX_PROF_COUNT(8, 1);
             if (resid * resid <= m.residual_thr) break;
         }
     } else {
+        PGX_PROF_COUNT(10, 1);
         init_limit_rows();
         for (int it = 0; it < n_it; it += 2) {
             float resid = 0.0f;
 #pragma unroll
             for (int r = PGX_N_ROWS - 1; r >= 0; r--) row(r, resid);
             if (CONT && any_contact) contact_rows(resid);
+            PGX_PROF_COUNT(8, 1);
             if (resid * resid <= m.residual_thr || it + 1 >= n_it) break;
             resid = 0.0f;
 #pragma unroll
             for (int r = 0; r < PGX_N_ROWS; r++) row(r, resid);
             if (CONT && any_contact) contact_rows(resid);
+            PGX_PROF_COUNT(8, 1);
             if (resid * resid <= m.residual_thr) break;
         }
     }
 #undef MINV
+    PGX_PROF_MARK(4);
+    PGX_PROF_COUNT(11, any_contact ? 1 : 0);
 #pragma unroll
     for (int j = 0; j < NJ; j++) {
         float vn = fminf(fmaxf(vu[j] + dv[j], -m.max_vel), m.max_vel);
@@ -1033,25 +1129,412 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
             L.cache[8 + 2 * s + 1][ln] = s < n1 ? lam1[s][0] : 0.0f;
         }
     }
-    if (OBJ) {
-        ob.v = vcu + dvl;
-        ob.w = wcu + dvw;
-        ob.p = ob.p + m.dt * ob.v;
-        /* btMultiBody::stepPositionsMultiDof, base: exponential map of w dt */
-        float ang = norm(ob.w);
-        if (ang * m.dt > 0.39269908f) ang = 0.39269908f * m.inv_dt;
-        const float hdt = 0.5f * m.dt;
-        const float f = ang < 0.001f ? (hdt - m.dt * m.dt * m.dt * 0.020833333333f * ang * ang)
-                                     : __sinf(ang * hdt) * fast_rcp(ang);
-        const float ax = ob.w.x * f, ay = ob.w.y * f, az = ob.w.z * f, aw = __cosf(ang * hdt);
-        /* dq * q (Hamilton, (x,y,z,w)) */
-        const float nx = aw * ob.qx + ax * ob.qw + ay * ob.qz - az * ob.qy;
-        const float ny = aw * ob.qy + ay * ob.qw + az * ob.qx - ax * ob.qz;
-        const float nz = aw * ob.qz + az * ob.qw + ax * ob.qy - ay * ob.qx;
-        const float nw = aw * ob.qw - ax * ob.qx - ay * ob.qy - az * ob.qz;
-        const float inn = __builtin_amdgcn_rsqf(nx * nx + ny * ny + nz * nz + nw * nw);
-        ob.qx = nx * inn; ob.qy = ny * inn; ob.qz = nz * inn; ob.qw = nw * inn;
+    if (OBJ) object_integrate(m, ob, vcu + dvl, wcu + dvw);
+    PGX_PROF_MARK(5);
+}
+
+/* ======================================================= wide layout: 16 lanes per env */
+/* At the headline batch (4096 envs = 64 waves in the one-lane layout, 6 % of the chip's
+ * 1024 SIMDs) the step is bound by one wave's dependent instruction stream, 77 % of it
+ * the PGS sweeps (tools/prof_phases.py).  The wide layout gives each env one 16-lane DPP
+ * row and splits the solver's coordinates over it: lanes 0-6 own the arm dofs'
+ * velocity deltas, lanes 7-9 / 10-12 the object's linear / angular ones.  A motor row
+ * broadcasts its dof's delta (row_newbcast), a contact row reduces J.dv with a 4-step
+ * DPP butterfly, and every lane applies the impulse to its own coordinate, so a row
+ * costs ~8 instructions on the critical path instead of ~13 + 14 for the 7-wide column
+ * updates and dot products.  Everything else (FK, dynamics, detection, IK, epilogue)
+ * runs redundantly and bit-identically on the 16 lanes, so all lanes of an env take the
+ * same branches; only the lead lane stores. */
+constexpr int GW = 16;          /* lanes per env: one DPP row */
+constexpr int EPW = 64 / GW;    /* envs per wave */
+using ContactLdsG = ContactLdsT<EPW>;
+
+template <int V>
+struct IC {
+    static constexpr int value = V;
+};
+/* compile-time loop (DPP controls must be constants) */
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+    if constexpr (B < E) {
+        f(IC<B>{});
+        sfor<B + 1, E>(f);
     }
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
+}
+/* lane SRC of this lane's 16-lane row (DPP row_newbcast, gfx90a+) */
+template <int SRC>
+__device__ __forceinline__ float bcast16(float x) {
+    return dpp<0x150 + SRC>(x);
+}
+/* t + bcast16<SRC>(g) * k as one v_fmac_f32_dpp (the compiler does not fold the DPP move
+ * into an FMAC).  A DPP read needs 2 wait states after the last VALU write of its source:
+ * the s_nop 1 covers that whatever precedes the asm. */
+#define PGX_FMAC_BCAST(N)                                                                                  \
+    if constexpr (SRC == N)                                                                                \
+        asm("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:" #N " row_mask:0xf bank_mask:0xf bound_ctrl:1" \
+            : "+v"(t) : "v"(g), "v"(k));
+template <int SRC>
+__device__ __forceinline__ float fmac_bcast(float t, float g, float k) {
+    PGX_FMAC_BCAST(0) PGX_FMAC_BCAST(1) PGX_FMAC_BCAST(2) PGX_FMAC_BCAST(3) PGX_FMAC_BCAST(4) PGX_FMAC_BCAST(5)
+    PGX_FMAC_BCAST(6) PGX_FMAC_BCAST(7) PGX_FMAC_BCAST(8) PGX_FMAC_BCAST(9) PGX_FMAC_BCAST(10) PGX_FMAC_BCAST(11)
+    PGX_FMAC_BCAST(12) PGX_FMAC_BCAST(13) PGX_FMAC_BCAST(14) PGX_FMAC_BCAST(15)
+    return t;
+}
+#undef PGX_FMAC_BCAST
+/* sum over the 16-lane row, the same bits in every lane: each butterfly step adds two
+ * partner sums that are already equal within their halves, and fl(a+b) = fl(b+a) */
+__device__ __forceinline__ float sum16(float x) {
+    x += dpp<0xB1>(x);    /* quad_perm [1,0,3,2] */
+    x += dpp<0x4E>(x);    /* quad_perm [2,3,0,1] */
+    x += dpp<0x141>(x);   /* row_half_mirror */
+    x += dpp<0x140>(x);   /* row_mirror */
+    return x;
+}
+/* Per-lane selection by row position K as one v_cndmask with a constant lane mask.  Plain
+ * `c == k ? a[k] : v` chains get rewritten by the compiler into a dynamically indexed
+ * stack array (scratch memory); the asm keeps them as selects. */
+template <int K>
+__device__ __forceinline__ float lane_sel(float a, float other) {   /* lanes with c == K take a */
+    constexpr uint64_t mask = 0x0001000100010001ull << K;
+    float r;
+    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(other), "v"(a), "s"(mask));
+    return r;
+}
+/* object coordinate of (lin, ang) for this lane: 7-9 linear, 10-12 angular, else 0 */
+__device__ __forceinline__ float pick_obj(V3 lin, V3 ang) {
+    float v = 0.0f;
+    v = lane_sel<7>(lin.x, v); v = lane_sel<8>(lin.y, v); v = lane_sel<9>(lin.z, v);
+    v = lane_sel<10>(ang.x, v); v = lane_sel<11>(ang.y, v); v = lane_sel<12>(ang.z, v);
+    return v;
+}
+/* this lane's arm entry a[c] (c < 7), else `other` */
+__device__ __forceinline__ float pick_arm(const float* a, float other) {
+    float v = other;
+    sfor<0, NJ>([&](auto kc) __attribute__((always_inline)) { v = lane_sel<decltype(kc)::value>(a[decltype(kc)::value], v); });
+    return v;
+}
+/* generalized coordinate of (arm[7], lin, ang) for this lane: arm dof c < 7, object 7-12, else 0 */
+__device__ __forceinline__ float pick_gen(const float* arm, V3 lin, V3 ang) { return pick_arm(arm, pick_obj(lin, ang)); }
+__device__ __forceinline__ V3 pick_v3(const V3* a) {
+    float x[NJ], y[NJ], zz[NJ];
+#pragma unroll
+    for (int k = 0; k < NJ; k++) { x[k] = a[k].x; y[k] = a[k].y; zz[k] = a[k].z; }
+    return v3(pick_arm(x, 0.0f), pick_arm(y, 0.0f), pick_arm(zz, 0.0f));
+}
+
+/* One stepSimulation() in the wide layout: the same restatement as substep() (dynamics
+ * shared through substep_dyn), rows solved in the same order with the same exit rule. */
+template <int OBJ, int CONT>
+__device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q, float* qd, const float* tq,
+                                          ObjState& ob, ContactLdsG* Lp, int es, int c) {
+    MRef m = *fresh(mp);
+    Dyn D;
+    substep_dyn<OBJ, CONT>(m, e, q, qd, ob, Lp, es, D);
+    const V3 (&z)[NJ] = D.z;
+    const V3 (&o)[NJ] = D.o;
+    const float (&Mi)[NJ][NJ] = D.Mi;
+    const float (&vu)[NJ] = D.vu;
+    const V3 vcu = D.vcu, wcu = D.wcu;
+#define MINV(a, b) ((a) >= (b) ? Mi[a][b] : Mi[b][a])
+    PGX_PROF_MARK(2);
+    const bool arm = c < NJ;
+    const float inv_m = e.obj_inv_mass, inv_i = e.obj_inv_inertia;
+    /* this lane's coordinate: M^-1 row (arm), object inverse mass / inertia, velocity */
+    float mcol[NJ];
+#pragma unroll
+    for (int d = 0; d < NJ; d++) {
+        float col[NJ];
+#pragma unroll
+        for (int k = 0; k < NJ; k++) col[k] = MINV(k, d);
+        mcol[d] = pick_arm(col, 0.0f);
+    }
+    const float kobj = OBJ ? ((c >= 7 && c < 10) ? inv_m : ((c >= 10 && c < 13) ? inv_i : 0.0f)) : 0.0f;
+    const float vu_c = pick_gen(vu, vcu, wcu);
+    float gv = 0.0f;   /* this lane's velocity delta */
+
+    /* ---- contact rows: per lane J_c and (M^-1 J^T)_c, per row rhs / jinv / den / lambda */
+    constexpr int P0 = OBJ ? CG : 0;            /* group-1 rows follow group 0's */
+    constexpr int NP = P0 + (CONT ? CG : 0);
+    float cJ[NP > 0 ? NP : 1][3], cR[NP > 0 ? NP : 1][3], crhs[NP > 0 ? NP : 1][3], cjinv[NP > 0 ? NP : 1][3];
+    float cden[NP > 0 ? NP : 1][3], clam[NP > 0 ? NP : 1][3];
+    bool act[NP > 0 ? NP : 1];
+    int n0 = 0, n1 = 0;
+    if (CONT) {
+        ContactLdsG& L = *Lp;
+        n0 = L.cnt[0][es];
+        n1 = L.cnt[1][es];
+        const float erp_dt = m.contact_erp * m.inv_dt;
+#pragma unroll
+        for (int k = 0; k < P0; k++) { /* object vertices vs the box top: object coordinates only */
+            act[k] = k < n0;
+            const float4 r4 = L.g0q[k][0][es];
+            const V3 r = v3(r4.x, r4.y, r4.z);
+            const float id = L.g0id[k][es];
+            float warm = 0.0f;
+#pragma unroll
+            for (int s = 0; s < CG; s++) if (L.cache[2 * s][es] == id) warm = m.warmstart * L.cache[2 * s + 1][es];
+#pragma unroll
+            for (int dir = 0; dir < 3; dir++) {
+                const V3 lin = dir == 0 ? v3(0, 0, 1) : (dir == 1 ? v3(0, -1, 0) : v3(1, 0, 0));
+                const V3 ang = dir == 0 ? v3(r.y, -r.x, 0) : (dir == 1 ? v3(r.z, 0, -r.x) : v3(0, r.z, -r.y));
+                const float den = inv_m + dot(ang, ang) * inv_i;
+                const float jinv = den > 2.220446e-16f ? fast_rcp(den) : 0.0f;
+                const float rel = dot(lin, vcu) + dot(ang, wcu);
+                float rhs;
+                if (dir == 0) {
+                    const float pen = L.g0d[k][es];
+                    rhs = (pen > 0.0f ? (-rel - pen * m.inv_dt) : (-pen * erp_dt - rel)) * jinv;
+                } else {
+                    rhs = -rel * jinv;
+                }
+                const float J = pick_obj(lin, ang);
+                cJ[k][dir] = act[k] ? J : 0.0f;
+                cR[k][dir] = act[k] ? J * kobj : 0.0f;
+                crhs[k][dir] = act[k] ? rhs : 0.0f;
+                cjinv[k][dir] = act[k] ? jinv : 0.0f;
+                cden[k][dir] = act[k] ? den : 0.0f;
+                clam[k][dir] = (act[k] && dir == 0) ? warm : 0.0f;
+                gv += cR[k][dir] * clam[k][dir];
+            }
+        }
+        /* robot vs table / plane / object: this lane's joint axis and pivot */
+        const V3 zc = pick_v3(z), oc = pick_v3(o);
+#pragma unroll
+        for (int k = 0; k < (CONT ? CG : 0); k++) {
+            const int p = P0 + k;
+            act[p] = k < n1;
+#pragma unroll
+            for (int dir = 0; dir < 3; dir++) {
+                cJ[p][dir] = 0.0f; cR[p][dir] = 0.0f; crhs[p][dir] = 0.0f;
+                cjinv[p][dir] = 0.0f; cden[p][dir] = 0.0f; clam[p][dir] = 0.0f;
+            }
+            if (__any(act[p])) {   /* wave-uniform; robot points are sparse */
+                const V3 P = v3(L.g1p[k][0][es], L.g1p[k][1][es], L.g1p[k][2][es]);
+                const V3 n = v3(L.g1n[k][0][es], L.g1n[k][1][es], L.g1n[k][2][es]);
+                const V3 rb = v3(L.g1rb[k][0][es], L.g1rb[k][1][es], L.g1rb[k][2][es]);
+                const int jl = L.g1j[k][es];
+                const float id = L.g1id[k][es];
+                const bool vs_obj = OBJ && id >= kTableIdLimit;
+                float warm = 0.0f;
+#pragma unroll
+                for (int s = 0; s < CG; s++)
+                    if (L.cache[8 + 2 * s][es] == id) warm = m.warmstart * L.cache[8 + 2 * s + 1][es];
+                V3 t1, t2;
+                plane_space(n, t1, t2);
+                const V3 Jv = (arm && c <= jl) ? cross(zc, P - oc) : v3(0, 0, 0);
+#pragma unroll
+                for (int dir = 0; dir < 3; dir++) {
+                    const V3 u = dir == 0 ? n : (dir == 1 ? t1 : t2);
+                    float J = dot(u, Jv);
+                    if (OBJ) {
+                        const V3 ca = cross(rb, u);
+                        const float oj = pick_obj(-1.0f * u, -1.0f * ca);
+                        J = (!arm && vs_obj) ? oj : J;
+                    }
+                    float R = kobj * J;
+                    sfor<0, NJ>([&](auto bc) __attribute__((always_inline)) {
+                        constexpr int b = decltype(bc)::value;
+                        R += mcol[b] * bcast16<b>(J);
+                    });
+                    const float den = sum16(J * R);
+                    const float rel = sum16(J * vu_c);
+                    const float jinv = den > 2.220446e-16f ? fast_rcp(den) : 0.0f;
+                    float rhs;
+                    if (dir == 0) {
+                        const float pen = L.g1d[k][es];
+                        rhs = (pen > 0.0f ? (-rel - pen * m.inv_dt) : (-pen * erp_dt - rel)) * jinv;
+                    } else {
+                        rhs = -rel * jinv;
+                    }
+                    cJ[p][dir] = act[p] ? J : 0.0f;
+                    cR[p][dir] = act[p] ? R : 0.0f;
+                    crhs[p][dir] = act[p] ? rhs : 0.0f;
+                    cjinv[p][dir] = act[p] ? jinv : 0.0f;
+                    cden[p][dir] = act[p] ? den : 0.0f;
+                    clam[p][dir] = (act[p] && dir == 0) ? warm : 0.0f;
+                    gv += cR[p][dir] * clam[p][dir];
+                }
+            }
+        }
+    }
+
+    /* ---- motor / limit rows (as substep()): per row rhs and lambda, per dof jinv / den */
+    float den[NJ], jinv[NJ];
+#pragma unroll
+    for (int d = 0; d < NJ; d++) {
+        den[d] = Mi[d][d];
+        jinv[d] = den[d] > 2.220446e-16f ? fast_rcp(den[d]) : 0.0f;
+    }
+    float rhs[PGX_N_ROWS], lam[PGX_N_ROWS];
+#pragma unroll
+    for (int r = 0; r < PGX_N_ROWS; r++) {
+        const int kind = kPgxRowCode[r] >> 4, d = kPgxRowCode[r] & 15;
+        lam[r] = 0.0f;
+        rhs[r] = 0.0f;
+        if (kind == 0) {
+            const float pos_term = (tq[d] - q[d]) * m.inv_dt;
+            const float desired = m.kp * pos_term + vu[d] + m.kd * (0.0f - vu[d]);
+            rhs[r] = (desired - vu[d]) * jinv[d];
+        }
+    }
+    auto init_limit_rows = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < PGX_N_ROWS; r++) {
+            const int kind = kPgxRowCode[r] >> 4, d = kPgxRowCode[r] & 15;
+            if (kind == 0) continue;
+            const float rel = kind == 2 ? -vu[d] : vu[d];
+            const float pen = kind == 1 ? (q[d] - kLower[d]) : (kUpper[d] - q[d]);
+            float verr = -rel, perr = 0.0f;
+            if (pen > 0.0f) verr -= pen * m.inv_dt;
+            else perr = -pen * m.erp * m.inv_dt;
+            rhs[r] = (perr + verr) * jinv[d];
+        }
+    };
+    /* exact limit-row skip (see substep()) */
+    bool far = n1 == 0;
+#pragma unroll
+    for (int d = 0; d < NJ; d++) {
+        float B = 0.0f;
+#pragma unroll
+        for (int k = 0; k < NJ; k++) B += fabsf(MINV(d, k)) * m.max_impulse[k];
+        B = B * 1.001f + 1e-6f;
+        const float penl = q[d] - kLower[d], penu = kUpper[d] - q[d];
+        far = far && penl > 0.0f && penu > 0.0f && (vu[d] - B) > -penl * m.inv_dt && (vu[d] + B) < penu * m.inv_dt;
+    }
+    /* delta = rhs - s dv_d jinv (s = -1 on upper-limit rows) as one v_fmac_f32_dpp; the
+     * chain per row is fmac_dpp -> add lam -> med3 -> sub -> fmac (the next broadcast's
+     * source).  Adding lam last keeps the rounding of the reference order: (lam + rhs)
+     * first cancels against large rhs and the residual exit then comes ~50 % later. */
+    float nsj[NJ], psj[NJ];
+#pragma unroll
+    for (int d = 0; d < NJ; d++) {
+        nsj[d] = -jinv[d];
+        psj[d] = jinv[d];
+        asm("" : "+v"(nsj[d]));   /* keep both signs in registers (no v_xor per row) */
+    }
+    auto mrow = [&](auto rc, float& resid) __attribute__((always_inline)) {
+        constexpr int r = decltype(rc)::value;
+        constexpr int kind = kPgxRowCode[r] >> 4, d = kPgxRowCode[r] & 15;
+        const float lo = kind == 0 ? -m.max_impulse[d] : 0.0f;
+        const float hi = kind == 0 ? m.max_impulse[d] : m.limit_max_imp;
+        const float x = fmac_bcast<d>(rhs[r], gv, kind == 2 ? psj[d] : nsj[d]);
+        const float nl = __builtin_amdgcn_fmed3f(lam[r] + x, lo, hi);
+        const float delta = nl - lam[r];
+        lam[r] = nl;
+        gv += mcol[d] * (kind == 2 ? -delta : delta);
+        resid = fmaxf(resid, fabsf(delta * den[d]));
+    };
+    /* an idle row (inactive point, or a friction row while the normal impulse is 0) gets
+     * the bounds [lam, lam]: delta = 0 without a select on the dependent chain */
+    auto crow = [&](const int p, const int dir, const bool fr, float& resid) __attribute__((always_inline)) {
+        const float ln_n = clam[p][0], lm = clam[p][dir];
+        const bool idle = !act[p] || (fr && !(ln_n > 0.0f));
+        const float lo = idle ? lm : (fr ? -m.friction * ln_n : 0.0f);
+        const float hi = idle ? lm : (fr ? m.friction * ln_n : 1e10f);
+        const float jdv = sum16(cJ[p][dir] * gv);
+        const float nl = __builtin_amdgcn_fmed3f(lm + fmaf(jdv, -cjinv[p][dir], crhs[p][dir]), lo, hi);
+        const float delta = nl - lm;
+        clam[p][dir] = nl;
+        gv += cR[p][dir] * delta;
+        resid = fmaxf(resid, fabsf(delta * cden[p][dir]));
+    };
+    const bool g0_any = CONT && OBJ && __any(n0 > 0);
+    const bool g1_any = CONT && __any(n1 > 0);
+    bool g1k_any[CG];
+#pragma unroll
+    for (int k = 0; k < CG; k++) g1k_any[k] = CONT && __any(k < n1);
+    auto contact_rows = [&](float& resid) __attribute__((always_inline)) {
+#pragma unroll
+        for (int fr = 0; fr < 2; fr++) {
+            if (OBJ && g0_any) {
+#pragma unroll
+                for (int k = 0; k < P0; k++)
+#pragma unroll
+                    for (int dir = fr ? 1 : 0; dir < (fr ? 3 : 1); dir++) crow(k, dir, fr, resid);
+            }
+            if (!g1_any) continue;
+#pragma unroll
+            for (int k = 0; k < (CONT ? CG : 0); k++) {
+                if (g1k_any[k]) {
+#pragma unroll
+                    for (int dir = fr ? 1 : 0; dir < (fr ? 3 : 1); dir++) crow(P0 + k, dir, fr, resid);
+                }
+            }
+        }
+    };
+    const bool any_contact = CONT && __any(n0 > 0 || n1 > 0);
+    const int n_it = m.num_iterations;
+    PGX_PROF_MARK(3);
+    PGX_PROF_COUNT(9, 1);
+    if (__all(far)) {
+        for (int it = 0; it < n_it; it += 2) {
+            float resid = 0.0f;
+            sfor<0, PGX_N_ROWS>([&](auto i) __attribute__((always_inline)) {
+                constexpr int r = PGX_N_ROWS - 1 - decltype(i)::value;
+                if constexpr ((kPgxRowCode[r] >> 4) == 0) mrow(IC<r>{}, resid);
+            });
+            if (CONT && any_contact) contact_rows(resid);
+            PGX_PROF_COUNT(8, 1);
+            if (resid * resid <= m.residual_thr || it + 1 >= n_it) break;
+            resid = 0.0f;
+            sfor<0, PGX_N_ROWS>([&](auto i) __attribute__((always_inline)) {
+                constexpr int r = decltype(i)::value;
+                if constexpr ((kPgxRowCode[r] >> 4) == 0) mrow(IC<r>{}, resid);
+            });
+            if (CONT && any_contact) contact_rows(resid);
+            PGX_PROF_COUNT(8, 1);
+            if (resid * resid <= m.residual_thr) break;
+        }
+    } else {
+        PGX_PROF_COUNT(10, 1);
+        init_limit_rows();
+        for (int it = 0; it < n_it; it += 2) {
+            float resid = 0.0f;
+            sfor<0, PGX_N_ROWS>([&](auto i) __attribute__((always_inline)) { mrow(IC<PGX_N_ROWS - 1 - decltype(i)::value>{}, resid); });
+            if (CONT && any_contact) contact_rows(resid);
+            PGX_PROF_COUNT(8, 1);
+            if (resid * resid <= m.residual_thr || it + 1 >= n_it) break;
+            resid = 0.0f;
+            sfor<0, PGX_N_ROWS>([&](auto i) __attribute__((always_inline)) { mrow(i, resid); });
+            if (CONT && any_contact) contact_rows(resid);
+            PGX_PROF_COUNT(8, 1);
+            if (resid * resid <= m.residual_thr) break;
+        }
+    }
+#undef MINV
+    PGX_PROF_MARK(4);
+    PGX_PROF_COUNT(11, any_contact ? 1 : 0);
+    sfor<0, NJ>([&](auto jc) __attribute__((always_inline)) {
+        constexpr int j = decltype(jc)::value;
+        const float vn = fminf(fmaxf(vu[j] + bcast16<j>(gv), -m.max_vel), m.max_vel);
+        qd[j] = vn;
+        q[j] += m.dt * vn;
+    });
+    if (CONT) { /* contact cache: this step's features and normal impulses */
+        ContactLdsG& L = *Lp;
+#pragma unroll
+        for (int s = 0; s < CG; s++) {
+            if (OBJ) {
+                L.cache[2 * s][es] = s < n0 ? L.g0id[s][es] : -1.0f;
+                L.cache[2 * s + 1][es] = s < n0 ? clam[s][0] : 0.0f;
+            } else {
+                L.cache[2 * s][es] = -1.0f;
+                L.cache[2 * s + 1][es] = 0.0f;
+            }
+            L.cache[8 + 2 * s][es] = s < n1 ? L.g1id[s][es] : -1.0f;
+            L.cache[8 + 2 * s + 1][es] = s < n1 ? clam[P0 + s][0] : 0.0f;
+        }
+    }
+    if (OBJ) {
+        const V3 dvl = v3(bcast16<7>(gv), bcast16<8>(gv), bcast16<9>(gv));
+        const V3 dvw = v3(bcast16<10>(gv), bcast16<11>(gv), bcast16<12>(gv));
+        object_integrate(m, ob, vcu + dvl, wcu + dvw);
+    }
+    PGX_PROF_MARK(5);
 }
 
 /* EE (link 11) COM position and velocity: getLinkState(11)[0] and [6] */
@@ -1491,22 +1974,28 @@ __device__ __forceinline__ void ao_store(const PgxDevState& s, int N, int i, con
     }
 }
 
-template <int CONTROL, int OBJ, int CONT, int AO>
+/* WIDE = 0: one env per lane (64 per wave); WIDE = 1: 16 lanes per env (4 per wave,
+ * substep_g), the redundant lanes compute the same values and only the lead lane stores. */
+template <int CONTROL, int OBJ, int CONT, int AO, int WIDE>
 __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict__ mdev, PgxDevEnv e, PgxDevState s,
                                                   const float* __restrict__ action, PgxDevOut o) {
-    const int ln = threadIdx.x;
-    const int i = blockIdx.x * blockDim.x + ln;
+    static_assert(!(AO && WIDE), "ReachAO runs in the one-lane layout");
+    using LT = ContactLdsT<WIDE ? EPW : 64>;
+    const int ln = WIDE ? (int)threadIdx.x / GW : (int)threadIdx.x;   /* env slot in the wave (LDS index) */
+    const int c = WIDE ? (int)threadIdx.x % GW : 0;                   /* lane within the env's row */
+    const bool lead = c == 0;
+    const int i = blockIdx.x * (WIDE ? EPW : 64) + ln;
     const int N = e.n_envs;
     if (i >= N) return;
     const int ii = i;
-    ContactLds* L = nullptr;
+    LT* L = nullptr;
     if constexpr (CONT) {
-        __shared__ ContactLds lds_buf;   /* ~126 KB: one wave per CU holds its envs' contact rows */
+        __shared__ LT lds_buf;   /* one-lane: ~126 KB, one wave per CU; wide: ~9 KB */
         L = &lds_buf;
         /* every row slot starts finite: the sweeps run unused slots predicated off, and an
          * inactive slot later only holds an earlier substep's (finite) row */
 #pragma unroll
-        for (int k = 0; k < CG; k++) {
+        for (int k = 0; k < (WIDE ? 0 : CG); k++) {
 #pragma unroll
             for (int qq = 0; qq < 4; qq++) L->g0q[k][qq][ln] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
@@ -1515,6 +2004,10 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
                 for (int qq = 0; qq < 6; qq++) L->g1q[k][dir][qq][ln] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         }
     }
+#ifdef PGX_PROF
+    if (threadIdx.x < 16) g_prof[threadIdx.x] = 0;
+    g_prof_t = __builtin_amdgcn_s_memtime();
+#endif
     const MPtr mp = fresh((uint64_t)mdev);
     MRef m = *mp;
     float q[NJ], qd[NJ], tq[NJ];
@@ -1555,10 +2048,12 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
         }
     }
 
+    PGX_PROF_MARK(0);
     const int n_substeps = m.n_substeps;
     bool collided = false;
     for (int st = 0; st < n_substeps; st++) {
-        substep<OBJ, CONT>(mp, e, q, qd, tq, ob, L, ln);
+        if constexpr (WIDE) substep_g<OBJ, CONT>(mp, e, q, qd, tq, ob, L, ln, c);
+        else substep<OBJ, CONT>(mp, e, q, qd, tq, ob, L, ln);
         if constexpr (AO) {   /* ReachAO step_check_collision: check after every substep, stop on contact */
             ao_caps(*fresh(mp), q, *L, ln);
             if (ao_collided(e, *L, ln)) { collided = true; break; }
@@ -1583,21 +2078,23 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
     /* TimeLimit, ReachAO.is_truncated (collision); terminate_on_success (core.py:359-361) */
     const bool trunc = (e.max_episode_steps > 0 && el >= e.max_episode_steps) || collided;
     const bool term = e.terminate_on_success && succ;
-    if (o.reward) o.reward[i] = rew;
-    if (o.success) o.success[i] = succ;
-    if (o.terminated) o.terminated[i] = term;
-    if (o.truncated) o.truncated[i] = trunc;
+    if (lead) {
+        if (o.reward) o.reward[i] = rew;
+        if (o.success) o.success[i] = succ;
+        if (o.terminated) o.terminated[i] = term;
+        if (o.truncated) o.truncated[i] = trunc;
+    }
     if constexpr (AO) ao_link_obs(*L, ln);
     if (trunc || term) {
-        if (o.terminal_obs) {
+        if (o.terminal_obs && lead) {
             if constexpr (AO) ao_write_obs(o.terminal_obs + (size_t)i * od, pos, vel, q, qd, *L, ln);
             else write_obs<OBJ>(e, o.terminal_obs + (size_t)i * od, pos, vel, ob);
         }
-        if (o.terminal_ag) {
+        if (o.terminal_ag && lead) {
             o.terminal_ag[3 * (size_t)i] = ag.x; o.terminal_ag[3 * (size_t)i + 1] = ag.y;
             o.terminal_ag[3 * (size_t)i + 2] = ag.z;
         }
-        if (o.terminal_dg) {
+        if (o.terminal_dg && lead) {
             o.terminal_dg[3 * (size_t)i] = (float)goal[0]; o.terminal_dg[3 * (size_t)i + 1] = (float)goal[1];
             o.terminal_dg[3 * (size_t)i + 2] = (float)goal[2];
         }
@@ -1621,6 +2118,7 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
         }
     }
     const V3 ag2 = OBJ ? ob.p : pos;
+    if (!lead) return;
     if (o.obs) {
         if constexpr (AO) ao_write_obs(o.obs + (size_t)i * od, pos, vel, q, qd, *L, ln);
         else write_obs<OBJ>(e, o.obs + (size_t)i * od, pos, vel, ob);
@@ -1645,6 +2143,11 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
     }
     s.elapsed[i] = el;
     s.episode[i] = episode;
+#ifdef PGX_PROF
+    PGX_PROF_MARK(6);
+    if (threadIdx.x == 0)
+        for (int k = 0; k < 16; k++) atomicAdd(&pgx_prof_counters[k], g_prof[k]);
+#endif
 }
 
 template <int OBJ, int AO>
@@ -1737,19 +2240,29 @@ __global__ __launch_bounds__(256) void compute_reward_kernel(const float* __rest
 
 int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState& s, const float* action,
                     const PgxDevOut& o, void* stream) {
-    dim3 block(64), grid((e.n_envs + 63) / 64);
     hipStream_t st = (hipStream_t)stream;
+    const int wide = !e.ao && e.lanes_per_env == GW;
+    const int per_block = wide ? EPW : 64;
+    dim3 block(64), grid((e.n_envs + per_block - 1) / per_block);
     const int variant = e.ao ? 13 : e.control * 4 + (e.has_object ? 2 : 0) + (e.contacts ? 1 : 0);
-    switch (variant) {
-        case 0: hipLaunchKernelGGL((step_kernel<0, 0, 0, 0>), grid, block, 0, st, m, e, s, action, o); break;
-        case 1: hipLaunchKernelGGL((step_kernel<0, 0, 1, 0>), grid, block, 0, st, m, e, s, action, o); break;
-        case 3: hipLaunchKernelGGL((step_kernel<0, 1, 1, 0>), grid, block, 0, st, m, e, s, action, o); break;
-        case 4: hipLaunchKernelGGL((step_kernel<1, 0, 0, 0>), grid, block, 0, st, m, e, s, action, o); break;
-        case 5: hipLaunchKernelGGL((step_kernel<1, 0, 1, 0>), grid, block, 0, st, m, e, s, action, o); break;
-        case 7: hipLaunchKernelGGL((step_kernel<1, 1, 1, 0>), grid, block, 0, st, m, e, s, action, o); break;
-        case 13: hipLaunchKernelGGL((step_kernel<1, 0, 1, 1>), grid, block, 0, st, m, e, s, action, o); break;
+#define PGX_STEP(C, O, K, A, W) hipLaunchKernelGGL((step_kernel<C, O, K, A, W>), grid, block, 0, st, m, e, s, action, o)
+    switch (variant * 2 + wide) {
+        case 0: PGX_STEP(0, 0, 0, 0, 0); break;
+        case 1: PGX_STEP(0, 0, 0, 0, 1); break;
+        case 2: PGX_STEP(0, 0, 1, 0, 0); break;
+        case 3: PGX_STEP(0, 0, 1, 0, 1); break;
+        case 6: PGX_STEP(0, 1, 1, 0, 0); break;
+        case 7: PGX_STEP(0, 1, 1, 0, 1); break;
+        case 8: PGX_STEP(1, 0, 0, 0, 0); break;
+        case 9: PGX_STEP(1, 0, 0, 0, 1); break;
+        case 10: PGX_STEP(1, 0, 1, 0, 0); break;
+        case 11: PGX_STEP(1, 0, 1, 0, 1); break;
+        case 14: PGX_STEP(1, 1, 1, 0, 0); break;
+        case 15: PGX_STEP(1, 1, 1, 0, 1); break;
+        case 26: PGX_STEP(1, 0, 1, 1, 0); break;
         default: return (int)hipErrorInvalidValue;   /* object without contacts: rejected at create */
     }
+#undef PGX_STEP
     return (int)hipGetLastError();
 }
 

@@ -1,0 +1,59 @@
+"""Phase breakdown of the step kernel (s_memtime per wave, libpgx_prof.so = make -C
+panda-gym_amd/csrc prof).  Prints mean cycles per wave per env step by phase and the
+PGS sweeps per substep the waves ran.
+Usage: PGX_LIB=panda-gym_amd/libpgx_prof.so python tools/prof_phases.py [env_id] [n] [contacts]"""
+import ctypes as C
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import panda_gym_amd as pg  # noqa: E402
+from panda_gym_amd import _native  # noqa: E402
+
+NAMES = ["prologue+IK", "FK+detect", "dynamics", "row setup", "PGS sweeps", "integrate", "epilogue"]
+
+
+def run(env_id, n, contacts, launches=100, warm=50):
+    lib = _native.load()
+    buf = (C.c_ulonglong * 16)()
+    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=0, contacts=contacts)
+    venv.reset_tensors()
+    for t in range(warm):
+        venv.step_tensors(venv.sample_actions(t))
+    torch.cuda.synchronize()
+    lib.pgx_prof_read(buf, 1)
+    acts = [venv.sample_actions(warm + t).clone() for t in range(launches)]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for a in acts:
+        venv.step_tensors(a)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / launches
+    lib.pgx_prof_read(buf, 1)
+    waves = n // 64
+    per = [buf[k] / (waves * launches) for k in range(16)]
+    tot = sum(per[:7])
+    out = {"env_id": env_id, "n": n, "contacts": contacts, "ms_per_step": ms,
+           "cycles_per_wave_step": tot, "clock_ghz_est": tot / (ms * 1e6),
+           "phases": {NAMES[k]: round(per[k]) for k in range(7)},
+           "share": {NAMES[k]: round(per[k] / tot, 3) for k in range(7)},
+           "sweeps_per_substep": per[8] / max(per[9], 1e-9), "nonfar_frac": per[10] / max(per[9], 1e-9),
+           "contact_substep_frac": per[11] / max(per[9], 1e-9),
+           "cycles_per_sweep": per[4] / max(per[8], 1e-9)}
+    venv.close()
+    return out
+
+
+if __name__ == "__main__":
+    cases = [("PandaReach-v3", 4096, True), ("PandaReach-v3", 4096, False), ("PandaPush-v3", 4096, True),
+             ("PandaPickAndPlace-v3", 16384, True), ("PandaReachAO-v3", 8192, True)]
+    if len(sys.argv) > 1:
+        cases = [(sys.argv[1], int(sys.argv[2]), bool(int(sys.argv[3])))]
+    for c in cases:
+        print(json.dumps(run(*c)), flush=True)
