@@ -325,10 +325,12 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     e.ao = cfg->task == PGX_TASK_REACH_AO;
     e.terminate_on_success = cfg->terminate_on_success ? 1 : 0;
     e.collision_reward = cfg->collision_reward;
-    /* Step layout (pgx_kernels.hip): 16 lanes per env while the batch leaves SIMDs idle in
-     * the one-lane layout (<= 32768 envs = 512 one-lane waves on 1024 SIMDs), one lane per
-     * env beyond; PGX_LANES_PER_ENV=1|16 overrides.  ReachAO always runs one lane per env. */
-    e.lanes_per_env = cfg->n_envs <= 32768 ? 16 : 1;
+    /* Step layout (pgx_kernels.hip): 16 lanes per env up to 4096 envs (at most one wide wave
+     * per SIMD: 4096 x 16 lanes = 1024 waves), one lane per env beyond, where the one-lane
+     * waves already fill enough SIMDs (tools/time_layouts.py: Reach at 8192 envs 1.37 ms
+     * one-lane vs 1.66 ms wide).  PGX_LANES_PER_ENV=1|16 overrides.  ReachAO runs one lane
+     * per env. */
+    e.lanes_per_env = cfg->n_envs <= 4096 ? 16 : 1;
     if (const char* lpe = std::getenv("PGX_LANES_PER_ENV")) {
         const int v = std::atoi(lpe);
         if (v != 1 && v != 16) { delete h; return fail(PGX_E_INVALID, "PGX_LANES_PER_ENV must be 1 or 16, got %s", lpe); }

@@ -63,8 +63,8 @@ __device__ __forceinline__ MPtr fresh(MPtr p) { return fresh((uint64_t)p); }
  * deltas accumulated in LDS by phase, summed over waves into pgx_prof_counters at the
  * end of the launch.  Compiled out of the product library. */
 #ifdef PGX_PROF
-__shared__ unsigned long long g_prof[16];
-__shared__ unsigned long long g_prof_t;
+__shared__ volatile unsigned long long g_prof[16];   /* volatile: never kept in per-lane registers */
+__shared__ volatile unsigned long long g_prof_t;
 __device__ __forceinline__ void prof_mark(int k) {
     const unsigned long long t = __builtin_amdgcn_s_memtime();
     g_prof[k] += t - g_prof_t;
@@ -72,9 +72,22 @@ __device__ __forceinline__ void prof_mark(int k) {
 }
 #define PGX_PROF_MARK(k) prof_mark(k)
 #define PGX_PROF_COUNT(k, v) (g_prof[k] += (unsigned long long)(v))
+/* sweeps: counted per lane in a register, the wave's maximum (the loop's trip count) added
+ * once per substep, so the counting adds nothing to the sweep loop's LDS traffic */
+#define PGX_PROF_SWEEP() (++prof_sweeps)
+#define PGX_PROF_SWEEPS_DONE()                                                       \
+    do {                                                                             \
+        int v_ = prof_sweeps;                                                        \
+        for (int o_ = 32; o_ >= 1; o_ >>= 1) v_ = max(v_, __shfl_xor(v_, o_));      \
+        g_prof[8] += (unsigned long long)v_;                                         \
+    } while (0)
+#define PGX_PROF_SWEEPS_DECL int prof_sweeps = 0
 #else
 #define PGX_PROF_MARK(k) ((void)0)
 #define PGX_PROF_COUNT(k, v) ((void)0)
+#define PGX_PROF_SWEEP() ((void)0)
+#define PGX_PROF_SWEEPS_DONE() ((void)0)
+#define PGX_PROF_SWEEPS_DECL ((void)0)
 #endif
 
 struct V3 {
@@ -981,7 +994,7 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
         const float lo = kind == 0 ? -m.max_impulse[d] : 0.0f;
         const float hi = kind == 0 ? m.max_impulse[d] : m.limit_max_imp;
         const float vd = kind == 2 ? -dv[d] : dv[d];
-        float delta = rhs[r] - vd * jinv[d];
+        float delta = fmaf(-vd, jinv[d], rhs[r]);
         /* v_med3 with the bounds straight from SGPRs (lo <= hi always holds) */
         const float nl = __builtin_amdgcn_fmed3f(lam[r] + delta, lo, hi);
         delta = nl - lam[r];
@@ -997,6 +1010,10 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
     };
     /* contact rows: normal rows of both groups, then friction rows (bounds from the
      * current normal impulse, skipped while it is 0) */
+    /* friction coefficient in a register: a model load inside the bound selects makes the
+     * compiler branch around it (a scalar load + wait per friction row) */
+    float mu = m.friction;
+    asm("" : "+s"(mu));
     const bool g0_any = CONT && OBJ && __any(n0 > 0);
     const bool g1_any = CONT && __any(n1 > 0);
     auto contact_rows = [&](float& resid) {
@@ -1017,8 +1034,8 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
                             const V3 ang = dir == 0 ? v3(r.y, -r.x, 0) : (dir == 1 ? v3(r.z, 0, -r.x) : v3(0, r.z, -r.y));
                             const float4 rw = L.g0q[k][1 + dir][ln];
                             const float jv = rw.x, dn = rw.y, rh = rw.z, lm = lam0[k][dir];
-                            const float lo = fr ? -m.friction * ln_n : 0.0f;
-                            const float hi = fr ? m.friction * ln_n : 1e10f;
+                            const float lo = fr ? -mu * ln_n : 0.0f;
+                            const float hi = fr ? mu * ln_n : 1e10f;
                             float delta = rh - (dot(lin, dvl) + dot(ang, dvw)) * jv;
                             const float nl = __builtin_amdgcn_fmed3f(lm + delta, lo, hi);
                             /* a friction row waits for a positive normal impulse */
@@ -1043,8 +1060,8 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
                         const float4 q2 = L.g1q[k][dir][2][ln], q3 = L.g1q[k][dir][3][ln];
                         const float4 q4 = L.g1q[k][dir][4][ln], q5 = L.g1q[k][dir][5][ln];
                         const float jv = q1.w, dn = q3.w, rh = q4.w, lm = lam1[k][dir];
-                        const float lo = fr ? -m.friction * ln_n : 0.0f;
-                        const float hi = fr ? m.friction * ln_n : 1e10f;
+                        const float lo = fr ? -mu * ln_n : 0.0f;
+                        const float hi = fr ? mu * ln_n : 1e10f;
                         /* two partial sums: half the dependent-FMA chain */
                         float ja = q0.x * dv[0] + q0.z * dv[2] + q1.x * dv[4] + q1.z * dv[6];
                         float jb = q0.y * dv[1] + q0.w * dv[3] + q1.y * dv[5];
@@ -1075,6 +1092,7 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
     const int n_it = m.num_iterations;
     PGX_PROF_MARK(3);
     PGX_PROF_COUNT(9, 1);
+    PGX_PROF_SWEEPS_DECL;
     if (__all(far)) {
         for (int it = 0; it < n_it; it += 2) {
             float resid = 0.0f;
@@ -1082,14 +1100,14 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
             for (int r = PGX_N_ROWS - 1; r >= 0; r--)
                 if ((kPgxRowCode[r] >> 4) == 0) row(r, resid);
             if (CONT && any_contact) contact_rows(resid);
-            PGX_PROF_COUNT(8, 1);
+            PGX_PROF_SWEEP();
             if (resid * resid <= m.residual_thr || it + 1 >= n_it) break;
             resid = 0.0f;
 #pragma unroll
             for (int r = 0; r < PGX_N_ROWS; r++)
                 if ((kPgxRowCode[r] >> 4) == 0) row(r, resid);
             if (CONT && any_contact) contact_rows(resid);
-            PGX_PROF_COUNT(8, 1);
+            PGX_PROF_SWEEP();
             if (resid * resid <= m.residual_thr) break;
         }
     } else {
@@ -1100,17 +1118,18 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
 #pragma unroll
             for (int r = PGX_N_ROWS - 1; r >= 0; r--) row(r, resid);
             if (CONT && any_contact) contact_rows(resid);
-            PGX_PROF_COUNT(8, 1);
+            PGX_PROF_SWEEP();
             if (resid * resid <= m.residual_thr || it + 1 >= n_it) break;
             resid = 0.0f;
 #pragma unroll
             for (int r = 0; r < PGX_N_ROWS; r++) row(r, resid);
             if (CONT && any_contact) contact_rows(resid);
-            PGX_PROF_COUNT(8, 1);
+            PGX_PROF_SWEEP();
             if (resid * resid <= m.residual_thr) break;
         }
     }
 #undef MINV
+    PGX_PROF_SWEEPS_DONE();
     PGX_PROF_MARK(4);
     PGX_PROF_COUNT(11, any_contact ? 1 : 0);
 #pragma unroll
@@ -1170,21 +1189,6 @@ template <int SRC>
 __device__ __forceinline__ float bcast16(float x) {
     return dpp<0x150 + SRC>(x);
 }
-/* t + bcast16<SRC>(g) * k as one v_fmac_f32_dpp (the compiler does not fold the DPP move
- * into an FMAC).  A DPP read needs 2 wait states after the last VALU write of its source:
- * the s_nop 1 covers that whatever precedes the asm. */
-#define PGX_FMAC_BCAST(N)                                                                                  \
-    if constexpr (SRC == N)                                                                                \
-        asm("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:" #N " row_mask:0xf bank_mask:0xf bound_ctrl:1" \
-            : "+v"(t) : "v"(g), "v"(k));
-template <int SRC>
-__device__ __forceinline__ float fmac_bcast(float t, float g, float k) {
-    PGX_FMAC_BCAST(0) PGX_FMAC_BCAST(1) PGX_FMAC_BCAST(2) PGX_FMAC_BCAST(3) PGX_FMAC_BCAST(4) PGX_FMAC_BCAST(5)
-    PGX_FMAC_BCAST(6) PGX_FMAC_BCAST(7) PGX_FMAC_BCAST(8) PGX_FMAC_BCAST(9) PGX_FMAC_BCAST(10) PGX_FMAC_BCAST(11)
-    PGX_FMAC_BCAST(12) PGX_FMAC_BCAST(13) PGX_FMAC_BCAST(14) PGX_FMAC_BCAST(15)
-    return t;
-}
-#undef PGX_FMAC_BCAST
 /* sum over the 16-lane row, the same bits in every lane: each butterfly step adds two
  * partner sums that are already equal within their halves, and fl(a+b) = fl(b+a) */
 __device__ __forceinline__ float sum16(float x) {
@@ -1362,6 +1366,42 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         }
     }
 
+    /* ---- Reach: contact-row velocities in lanes.  Lane q = 3 point + dir holds w_q = J_q.dv
+     * (register gw) and the Delassus entries W[q][s] = J_q M^-1 J_s^T of every row s (Wm:
+     * motor / limit rows of dof d, = (M^-1 J_q^T)_d; Wc: contact rows), so a contact row
+     * reads its velocity with one broadcast, like a motor row, instead of a 16-lane
+     * reduction; every row's impulse also updates gw (one more off-chain fma). */
+    constexpr bool WROWS = CONT && !OBJ;
+    constexpr int NQ = WROWS ? 3 * CG : 1;
+    bool g1k_any[CG];
+#pragma unroll
+    for (int k = 0; k < CG; k++) g1k_any[k] = CONT && __any(k < n1);
+    float gw = 0.0f, Wm[NJ], Wc[NQ];
+#pragma unroll
+    for (int d = 0; d < NJ; d++) Wm[d] = 0.0f;
+#pragma unroll
+    for (int s2 = 0; s2 < NQ; s2++) Wc[s2] = 0.0f;
+    if constexpr (WROWS) {
+        sfor<0, NQ>([&](auto qc) __attribute__((always_inline)) {
+            constexpr int q = decltype(qc)::value, pq = q / 3, dq = q % 3;
+            if (g1k_any[pq]) {
+                sfor<0, NJ>([&](auto dc) __attribute__((always_inline)) {
+                    constexpr int d = decltype(dc)::value;
+                    Wm[d] = lane_sel<q>(bcast16<d>(cR[pq][dq]), Wm[d]);
+                });
+                sfor<0, q + 1>([&](auto sc) __attribute__((always_inline)) {
+                    constexpr int s2 = decltype(sc)::value;
+                    if (g1k_any[s2 / 3]) {
+                        const float w = sum16(cJ[pq][dq] * cR[s2 / 3][s2 % 3]);
+                        Wc[s2] = lane_sel<q>(w, Wc[s2]);
+                        if constexpr (s2 != q) Wc[q] = lane_sel<s2>(w, Wc[q]);
+                    }
+                });
+                gw = lane_sel<q>(sum16(cJ[pq][dq] * gv), gw);
+            }
+        });
+    }
+
     /* ---- motor / limit rows (as substep()): per row rhs and lambda, per dof jinv / den */
     float den[NJ], jinv[NJ];
 #pragma unroll
@@ -1405,10 +1445,10 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         const float penl = q[d] - kLower[d], penu = kUpper[d] - q[d];
         far = far && penl > 0.0f && penu > 0.0f && (vu[d] - B) > -penl * m.inv_dt && (vu[d] + B) < penu * m.inv_dt;
     }
-    /* delta = rhs - s dv_d jinv (s = -1 on upper-limit rows) as one v_fmac_f32_dpp; the
-     * chain per row is fmac_dpp -> add lam -> med3 -> sub -> fmac (the next broadcast's
-     * source).  Adding lam last keeps the rounding of the reference order: (lam + rhs)
-     * first cancels against large rhs and the residual exit then comes ~50 % later. */
+    /* delta = rhs - s dv_d jinv (s = -1 on upper-limit rows): the dof's delta broadcast from
+     * its lane (row_newbcast) and one fma with the signed jinv kept in registers; the chain
+     * per row is dpp move -> fma -> add lam -> med3 -> sub -> fmac (the next broadcast's
+     * source), lam added last as in the reference's order. */
     float nsj[NJ], psj[NJ];
 #pragma unroll
     for (int d = 0; d < NJ; d++) {
@@ -1421,55 +1461,63 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         constexpr int kind = kPgxRowCode[r] >> 4, d = kPgxRowCode[r] & 15;
         const float lo = kind == 0 ? -m.max_impulse[d] : 0.0f;
         const float hi = kind == 0 ? m.max_impulse[d] : m.limit_max_imp;
-        const float x = fmac_bcast<d>(rhs[r], gv, kind == 2 ? psj[d] : nsj[d]);
+        const float x = fmaf(bcast16<d>(gv), kind == 2 ? psj[d] : nsj[d], rhs[r]);
         const float nl = __builtin_amdgcn_fmed3f(lam[r] + x, lo, hi);
         const float delta = nl - lam[r];
         lam[r] = nl;
-        gv += mcol[d] * (kind == 2 ? -delta : delta);
+        const float sd = kind == 2 ? -delta : delta;
+        gv += mcol[d] * sd;
+        if constexpr (WROWS) gw += Wm[d] * sd;
         resid = fmaxf(resid, fabsf(delta * den[d]));
     };
+    /* friction coefficient in a register: a model load inside the bound selects makes the
+     * compiler branch around it (a scalar load + wait per friction row) */
+    float mu = m.friction;
+    asm("" : "+s"(mu));
     /* an idle row (inactive point, or a friction row while the normal impulse is 0) gets
      * the bounds [lam, lam]: delta = 0 without a select on the dependent chain */
-    auto crow = [&](const int p, const int dir, const bool fr, float& resid) __attribute__((always_inline)) {
+    auto crow = [&](auto pc, auto dc, const bool fr, float& resid) __attribute__((always_inline)) {
+        constexpr int p = decltype(pc)::value, dir = decltype(dc)::value;
         const float ln_n = clam[p][0], lm = clam[p][dir];
         const bool idle = !act[p] || (fr && !(ln_n > 0.0f));
-        const float lo = idle ? lm : (fr ? -m.friction * ln_n : 0.0f);
-        const float hi = idle ? lm : (fr ? m.friction * ln_n : 1e10f);
-        const float jdv = sum16(cJ[p][dir] * gv);
+        const float lo = idle ? lm : (fr ? -mu * ln_n : 0.0f);
+        const float hi = idle ? lm : (fr ? mu * ln_n : 1e10f);
+        float jdv;
+        if constexpr (WROWS) jdv = bcast16<3 * p + dir>(gw);
+        else jdv = sum16(cJ[p][dir] * gv);
         const float nl = __builtin_amdgcn_fmed3f(lm + fmaf(jdv, -cjinv[p][dir], crhs[p][dir]), lo, hi);
         const float delta = nl - lm;
         clam[p][dir] = nl;
         gv += cR[p][dir] * delta;
+        if constexpr (WROWS) gw += Wc[3 * p + dir] * delta;
         resid = fmaxf(resid, fabsf(delta * cden[p][dir]));
     };
     const bool g0_any = CONT && OBJ && __any(n0 > 0);
     const bool g1_any = CONT && __any(n1 > 0);
-    bool g1k_any[CG];
-#pragma unroll
-    for (int k = 0; k < CG; k++) g1k_any[k] = CONT && __any(k < n1);
     auto contact_rows = [&](float& resid) __attribute__((always_inline)) {
 #pragma unroll
         for (int fr = 0; fr < 2; fr++) {
             if (OBJ && g0_any) {
-#pragma unroll
-                for (int k = 0; k < P0; k++)
-#pragma unroll
-                    for (int dir = fr ? 1 : 0; dir < (fr ? 3 : 1); dir++) crow(k, dir, fr, resid);
+                sfor<0, P0>([&](auto kc) __attribute__((always_inline)) {
+                    if (fr) { crow(kc, IC<1>{}, true, resid); crow(kc, IC<2>{}, true, resid); }
+                    else crow(kc, IC<0>{}, false, resid);
+                });
             }
             if (!g1_any) continue;
-#pragma unroll
-            for (int k = 0; k < (CONT ? CG : 0); k++) {
+            sfor<0, (CONT ? CG : 0)>([&](auto kc) __attribute__((always_inline)) {
+                constexpr int k = decltype(kc)::value;
                 if (g1k_any[k]) {
-#pragma unroll
-                    for (int dir = fr ? 1 : 0; dir < (fr ? 3 : 1); dir++) crow(P0 + k, dir, fr, resid);
+                    if (fr) { crow(IC<P0 + k>{}, IC<1>{}, true, resid); crow(IC<P0 + k>{}, IC<2>{}, true, resid); }
+                    else crow(IC<P0 + k>{}, IC<0>{}, false, resid);
                 }
-            }
+            });
         }
     };
     const bool any_contact = CONT && __any(n0 > 0 || n1 > 0);
     const int n_it = m.num_iterations;
     PGX_PROF_MARK(3);
     PGX_PROF_COUNT(9, 1);
+    PGX_PROF_SWEEPS_DECL;
     if (__all(far)) {
         for (int it = 0; it < n_it; it += 2) {
             float resid = 0.0f;
@@ -1478,7 +1526,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 if constexpr ((kPgxRowCode[r] >> 4) == 0) mrow(IC<r>{}, resid);
             });
             if (CONT && any_contact) contact_rows(resid);
-            PGX_PROF_COUNT(8, 1);
+            PGX_PROF_SWEEP();
             if (resid * resid <= m.residual_thr || it + 1 >= n_it) break;
             resid = 0.0f;
             sfor<0, PGX_N_ROWS>([&](auto i) __attribute__((always_inline)) {
@@ -1486,7 +1534,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 if constexpr ((kPgxRowCode[r] >> 4) == 0) mrow(IC<r>{}, resid);
             });
             if (CONT && any_contact) contact_rows(resid);
-            PGX_PROF_COUNT(8, 1);
+            PGX_PROF_SWEEP();
             if (resid * resid <= m.residual_thr) break;
         }
     } else {
@@ -1496,16 +1544,17 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             float resid = 0.0f;
             sfor<0, PGX_N_ROWS>([&](auto i) __attribute__((always_inline)) { mrow(IC<PGX_N_ROWS - 1 - decltype(i)::value>{}, resid); });
             if (CONT && any_contact) contact_rows(resid);
-            PGX_PROF_COUNT(8, 1);
+            PGX_PROF_SWEEP();
             if (resid * resid <= m.residual_thr || it + 1 >= n_it) break;
             resid = 0.0f;
             sfor<0, PGX_N_ROWS>([&](auto i) __attribute__((always_inline)) { mrow(i, resid); });
             if (CONT && any_contact) contact_rows(resid);
-            PGX_PROF_COUNT(8, 1);
+            PGX_PROF_SWEEP();
             if (resid * resid <= m.residual_thr) break;
         }
     }
 #undef MINV
+    PGX_PROF_SWEEPS_DONE();
     PGX_PROF_MARK(4);
     PGX_PROF_COUNT(11, any_contact ? 1 : 0);
     sfor<0, NJ>([&](auto jc) __attribute__((always_inline)) {
