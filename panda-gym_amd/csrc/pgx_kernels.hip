@@ -1418,7 +1418,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         if (kind == 0) {
             const float pos_term = (tq[d] - q[d]) * m.inv_dt;
             const float desired = m.kp * pos_term + vu[d] + m.kd * (0.0f - vu[d]);
-            rhs[r] = (desired - vu[d]) * jinv[d];
+            rhs[r] = desired - vu[d];   /* scaled units: rhs * den */
         }
     }
     auto init_limit_rows = [&]() __attribute__((always_inline)) {
@@ -1431,7 +1431,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             float verr = -rel, perr = 0.0f;
             if (pen > 0.0f) verr -= pen * m.inv_dt;
             else perr = -pen * m.erp * m.inv_dt;
-            rhs[r] = (perr + verr) * jinv[d];
+            rhs[r] = perr + verr;   /* scaled units */
         }
     };
     /* exact limit-row skip (see substep()) */
@@ -1445,52 +1445,74 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         const float penl = q[d] - kLower[d], penu = kUpper[d] - q[d];
         far = far && penl > 0.0f && penu > 0.0f && (vu[d] - B) > -penl * m.inv_dt && (vu[d] + B) < penu * m.inv_dt;
     }
-    /* delta = rhs - s dv_d jinv (s = -1 on upper-limit rows): the dof's delta broadcast from
-     * its lane (row_newbcast) and one fma with the signed jinv kept in registers; the chain
-     * per row is dpp move -> fma -> add lam -> med3 -> sub -> fmac (the next broadcast's
-     * source), lam added last as in the reference's order. */
-    float nsj[NJ], psj[NJ];
+    /* Rows in scaled units: each row equation multiplied by its den (= J M^-1 J^T), so
+     * lambda' = lambda den, rhs' = rhs den and the unclamped update is
+     *   lambda' + delta' = (lambda' + rhs') - s v_d        (jinv den = 1)
+     * with v_d the row's velocity: one DPP-sourced v_sub/v_add of the broadcast delta-v off
+     * a sum formed off the chain; delta' = delta den is the residual Bullet tracks, and the
+     * coordinate updates take the columns pre-multiplied by jinv.  Chain per row:
+     * v_sub_dpp -> med3 -> sub -> fmac (the next broadcast's source). */
+    float mcs[NJ], wms[NJ], mhi[NJ], lhi[NJ];
 #pragma unroll
     for (int d = 0; d < NJ; d++) {
-        nsj[d] = -jinv[d];
-        psj[d] = jinv[d];
-        asm("" : "+v"(nsj[d]));   /* keep both signs in registers (no v_xor per row) */
+        mcs[d] = mcol[d] * jinv[d];
+        wms[d] = Wm[d] * jinv[d];
+        mhi[d] = m.max_impulse[d] * den[d];
+        lhi[d] = m.limit_max_imp * den[d];
     }
     auto mrow = [&](auto rc, float& resid) __attribute__((always_inline)) {
         constexpr int r = decltype(rc)::value;
         constexpr int kind = kPgxRowCode[r] >> 4, d = kPgxRowCode[r] & 15;
-        const float lo = kind == 0 ? -m.max_impulse[d] : 0.0f;
-        const float hi = kind == 0 ? m.max_impulse[d] : m.limit_max_imp;
-        const float x = fmaf(bcast16<d>(gv), kind == 2 ? psj[d] : nsj[d], rhs[r]);
-        const float nl = __builtin_amdgcn_fmed3f(lam[r] + x, lo, hi);
+        const float t = lam[r] + rhs[r];
+        const float x = kind == 2 ? t + bcast16<d>(gv) : t - bcast16<d>(gv);
+        const float nl = kind == 0 ? __builtin_amdgcn_fmed3f(x, -mhi[d], mhi[d]) : __builtin_amdgcn_fmed3f(x, 0.0f, lhi[d]);
         const float delta = nl - lam[r];
         lam[r] = nl;
         const float sd = kind == 2 ? -delta : delta;
-        gv += mcol[d] * sd;
-        if constexpr (WROWS) gw += Wm[d] * sd;
-        resid = fmaxf(resid, fabsf(delta * den[d]));
+        gv += mcs[d] * sd;
+        if constexpr (WROWS) gw += wms[d] * sd;
+        resid = fmaxf(resid, fabsf(delta));
     };
     /* friction coefficient in a register: a model load inside the bound selects makes the
      * compiler branch around it (a scalar load + wait per friction row) */
     float mu = m.friction;
     asm("" : "+s"(mu));
-    /* an idle row (inactive point, or a friction row while the normal impulse is 0) gets
-     * the bounds [lam, lam]: delta = 0 without a select on the dependent chain */
+    /* contact rows in scaled units too: lambda' = lambda den, friction bounds
+     * +-mu lambda_n den_f = +-lambda'_n (mu jinv_n den_f); an idle row (inactive point, no
+     * usable den, or a friction row while the normal impulse is 0) gets the bounds
+     * [lambda', lambda']: delta' = 0 without a select on the chain */
+    constexpr int NPP = NP > 0 ? NP : 1;
+    float fk[NPP][3];
+    bool rok[NPP][3];   /* row usable: den above SIMD_EPSILON (else jinv = 0 and the row is inert) */
+#pragma unroll
+    for (int p = 0; p < NP; p++)
+#pragma unroll
+        for (int dir = 0; dir < 3; dir++) {
+            rok[p][dir] = act[p] && cjinv[p][dir] != 0.0f;
+            fk[p][dir] = mu * cjinv[p][0] * cden[p][dir];
+            crhs[p][dir] *= cden[p][dir];
+            clam[p][dir] *= cden[p][dir];
+            cR[p][dir] *= cjinv[p][dir];
+        }
+    if constexpr (WROWS) {
+#pragma unroll
+        for (int q = 0; q < NQ; q++) Wc[q] *= cjinv[q / 3][q % 3];
+    }
     auto crow = [&](auto pc, auto dc, const bool fr, float& resid) __attribute__((always_inline)) {
         constexpr int p = decltype(pc)::value, dir = decltype(dc)::value;
         const float ln_n = clam[p][0], lm = clam[p][dir];
-        const bool idle = !act[p] || (fr && !(ln_n > 0.0f));
-        const float lo = idle ? lm : (fr ? -mu * ln_n : 0.0f);
-        const float hi = idle ? lm : (fr ? mu * ln_n : 1e10f);
+        const bool idle = !rok[p][dir] || (fr && !(ln_n > 0.0f));
+        const float lo = idle ? lm : (fr ? -fk[p][dir] * ln_n : 0.0f);
+        const float hi = idle ? lm : (fr ? fk[p][dir] * ln_n : 3.0e38f);
         float jdv;
         if constexpr (WROWS) jdv = bcast16<3 * p + dir>(gw);
         else jdv = sum16(cJ[p][dir] * gv);
-        const float nl = __builtin_amdgcn_fmed3f(lm + fmaf(jdv, -cjinv[p][dir], crhs[p][dir]), lo, hi);
+        const float nl = __builtin_amdgcn_fmed3f((lm + crhs[p][dir]) - jdv, lo, hi);
         const float delta = nl - lm;
         clam[p][dir] = nl;
         gv += cR[p][dir] * delta;
         if constexpr (WROWS) gw += Wc[3 * p + dir] * delta;
-        resid = fmaxf(resid, fabsf(delta * cden[p][dir]));
+        resid = fmaxf(resid, fabsf(delta));
     };
     const bool g0_any = CONT && OBJ && __any(n0 > 0);
     const bool g1_any = CONT && __any(n1 > 0);
@@ -1569,13 +1591,13 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         for (int s = 0; s < CG; s++) {
             if (OBJ) {
                 L.cache[2 * s][es] = s < n0 ? L.g0id[s][es] : -1.0f;
-                L.cache[2 * s + 1][es] = s < n0 ? clam[s][0] : 0.0f;
+                L.cache[2 * s + 1][es] = s < n0 ? clam[s][0] * cjinv[s][0] : 0.0f;
             } else {
                 L.cache[2 * s][es] = -1.0f;
                 L.cache[2 * s + 1][es] = 0.0f;
             }
             L.cache[8 + 2 * s][es] = s < n1 ? L.g1id[s][es] : -1.0f;
-            L.cache[8 + 2 * s + 1][es] = s < n1 ? clam[P0 + s][0] : 0.0f;
+            L.cache[8 + 2 * s + 1][es] = s < n1 ? clam[P0 + s][0] * cjinv[P0 + s][0] : 0.0f;
         }
     }
     if (OBJ) {
