@@ -312,7 +312,7 @@ def main():
                        "envs_per_gpu": E, "global_envs": world * E, "parallelism": f"env-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "step_kernel<0, 0, 1> (ee control, no object, table contacts)",
+                         "kernel": "step_kernel<0, 0, 1, 0, 1> (ee control, no object, table contacts, 16 lanes per env)",
                          "kernel_ms": kernel_ms,
                          "alg_bytes_per_launch": alg_bytes},
             "roofline_valu": valu,

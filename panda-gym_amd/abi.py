@@ -76,7 +76,7 @@ class PgxConfig(C.Structure):
         ("joint_forces", C.c_double * MAX_DOFS), ("neutral_q", C.c_double * MAX_DOFS),
         ("ee_step", C.c_double), ("joint_step", C.c_double),
         ("model", C.POINTER(PgxModel)), ("params", C.POINTER(PgxSimParams)),
-        ("contacts", C.c_int32), ("pad2", C.c_int32),
+        ("contacts", C.c_int32), ("lanes_per_env", C.c_int32),
         ("goal_offset", C.c_double * 3), ("goal_z_zero_prob", C.c_double),
         ("obj_low", C.c_double * 3), ("obj_high", C.c_double * 3), ("obj_offset", C.c_double * 3),
         ("object_half", C.c_double), ("object_mass", C.c_double), ("object_inertia", C.c_double),
@@ -245,8 +245,9 @@ class EnvSpec:
 
 
 def make_config(spec: EnvSpec, n_envs: int, model: PgxModel, params: PgxSimParams, seed: int = 0,
-                env_id_offset: int = 0, contacts: bool = True) -> PgxConfig:
+                env_id_offset: int = 0, contacts: bool = True, lanes_per_env: int = 0) -> PgxConfig:
     c = PgxConfig()
+    c.lanes_per_env = lanes_per_env   # step layout: 0 auto, 1 or 16 (include/pgx.h)
     c.task, c.control, c.reward = spec.task, spec.control, spec.reward
     c.n_envs = n_envs
     c.max_episode_steps = spec.max_episode_steps

@@ -141,11 +141,17 @@ def seeded_reset(env_spec: abi.EnvSpec, seed: Optional[int]) -> Optional[Tuple[n
 
 # ------------------------------------------------------------ vec env
 class PandaVecEnv:
-    """N independent Panda envs stepped in lockstep by one HIP kernel launch."""
+    """N independent Panda envs stepped in lockstep by one HIP kernel launch.
+
+    ``lanes_per_env`` picks the kernel layout (results agree to fp32 rounding): 16 gives
+    each env a 16-lane DPP row (the solver's coordinates split over the lanes; fastest
+    while the batch is too small to fill the chip one lane per env), 1 one env per lane,
+    0 (default) chooses by batch size (16 up to 4096 envs)."""
 
     def __init__(self, env_id: str = "PandaReach-v3", num_envs: int = 4096, device: Any = "cuda:0", seed: int = 0,
                  env_id_offset: int = 0, max_episode_steps: Optional[int] = None, auto_reset: bool = True,
-                 n_substeps: int = 20, model_name: str = "panda_custom0", contacts: bool = True):
+                 n_substeps: int = 20, model_name: str = "panda_custom0", contacts: bool = True,
+                 lanes_per_env: int = 0):
         if torch is None:
             raise PgxError("PandaVecEnv needs torch for device buffers")
         self.lib = load()
@@ -162,7 +168,7 @@ class PandaVecEnv:
         self._params = abi.default_sim_params(n_substeps=n_substeps)
         cfg_spec = replace(self.spec, max_episode_steps=self.spec.max_episode_steps if auto_reset else 0)
         self._cfg = abi.make_config(cfg_spec, self.num_envs, self._model, self._params, seed=seed,
-                                    env_id_offset=env_id_offset, contacts=contacts)
+                                    env_id_offset=env_id_offset, contacts=contacts, lanes_per_env=lanes_per_env)
         self.obs_dim = self.lib.pgx_obs_dim(C.byref(self._cfg))
         self.action_dim = self.lib.pgx_action_dim(C.byref(self._cfg))
         h = C.c_void_p()

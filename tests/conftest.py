@@ -34,3 +34,9 @@ def upstream_model():
     from panda_gym_amd.model import load_model
 
     return abi.make_model(load_model("panda_upstream"), ee_link=6)
+
+
+@pytest.fixture(params=[16, 1], ids=["wide", "narrow"])
+def lanes(request):
+    """Both step-kernel layouts (PandaVecEnv(lanes_per_env=...)): 16 lanes per env, 1 lane per env."""
+    return request.param

@@ -32,9 +32,9 @@ def _obs(venv):
 
 
 @pytest.mark.parametrize("env_id", ["PandaPush-v3", "PandaPickAndPlace-v3", "PandaPushJoints-v3"])
-def test_object_reset_and_one_step_parity(pg, oracle, env_id):
+def test_object_reset_and_one_step_parity(pg, oracle, env_id, lanes):
     n = 256
-    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=5)
+    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=5, lanes_per_env=lanes)
     venv.reset_tensors(seed=100)
     spec = pg.spec(env_id)
     for i in (0, 17, 255):   # host PCG64 draws (RobotTaskEnv.reset(seed)) injected exactly
@@ -58,10 +58,10 @@ def test_object_reset_and_one_step_parity(pg, oracle, env_id):
     venv.close()
 
 
-def _one_step_errors(pg, oracle, env_id, n, steps, seed, actions=None):
+def _one_step_errors(pg, oracle, env_id, n, steps, seed, actions=None, lanes=0):
     """Per step, from the device state copied into the oracle: |device - oracle| of the EE
     position (obs 0:3) and the achieved goal (EE or object position)."""
-    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=seed)
+    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=seed, lanes_per_env=lanes)
     venv.reset_tensors(seed=seed)
     ref = oracle.OracleVecEnv(venv._cfg, n)
     ee_err, ag_err = [], []
@@ -82,12 +82,12 @@ def _one_step_errors(pg, oracle, env_id, n, steps, seed, actions=None):
     return np.stack(ee_err), np.stack(ag_err), final
 
 
-def test_reach_with_table_contacts(pg, oracle):
+def test_reach_with_table_contacts(pg, oracle, lanes):
     """Drive the EE into the table (a = -z): the tool-bar contact holds it at z ~ 0.042."""
     acts = [[0.3, -0.2, -1.0]] * 30
-    ee, ag, _ = _one_step_errors(pg, oracle, "PandaReach-v3", 64, 30, 3, acts)
+    ee, ag, _ = _one_step_errors(pg, oracle, "PandaReach-v3", 64, 30, 3, acts, lanes=lanes)
     assert np.percentile(ee, 99) <= 1e-5 and ee.max() <= 1e-3, (np.percentile(ee, 99), ee.max())
-    venv = pg.PandaVecEnv("PandaReach-v3", num_envs=64, device="cuda:0", seed=3)
+    venv = pg.PandaVecEnv("PandaReach-v3", num_envs=64, device="cuda:0", seed=3, lanes_per_env=lanes)
     venv.reset_tensors(seed=3)
     for a in acts:
         venv.step_tensors(torch.tensor([a] * 64, dtype=torch.float32, device="cuda:0"))
@@ -97,8 +97,8 @@ def test_reach_with_table_contacts(pg, oracle):
 
 
 @pytest.mark.parametrize("env_id", ["PandaPush-v3", "PandaPickAndPlaceJoints-v3"])
-def test_random_policy_one_step_parity(pg, oracle, env_id):
-    ee, ag, final = _one_step_errors(pg, oracle, env_id, 256, 50, 21)
+def test_random_policy_one_step_parity(pg, oracle, env_id, lanes):
+    ee, ag, final = _one_step_errors(pg, oracle, env_id, 256, 50, 21, lanes=lanes)
     for name, e in (("ee", ee), ("object", ag)):
         assert np.percentile(e, 99) <= 1e-5, (name, np.percentile(e, 99))
         assert e.max() <= 1e-3, (name, e.max())
@@ -157,3 +157,27 @@ def test_push_large_batch_properties(pg):
     assert cube[2].min() > -0.4 and cube[2].max() < 0.5      # above the plane, nothing launched
     assert np.abs(np.linalg.norm(cube[3:7], axis=0) - 1).max() < 1e-5
     venv.close()
+
+
+@pytest.mark.parametrize("env_id", ["PandaReach-v3", "PandaPush-v3", "PandaPickAndPlaceJoints-v3"])
+def test_layouts_agree_per_step(pg, env_id):
+    """The 16-lane and the one-lane kernels restate the same step; from the same state (copied
+    through the state views) one random-policy step agrees to fp32 rounding (summation order
+    of the row reductions, scaled row units).  Per step, as in the oracle parity above."""
+    n = 512
+    a = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=4, lanes_per_env=16)
+    b = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=4, lanes_per_env=1)
+    a.reset_tensors(seed=4)
+    errs = []
+    for t in range(20):
+        for k, v in a.state().items():
+            b.state()[k].copy_(v)
+        act = a.sample_actions(t).clone()
+        a.step_tensors(act)
+        b.step_tensors(act)
+        assert torch.equal(a.truncated, b.truncated)
+        errs.append((a.obs[:, :3] - b.obs[:, :3]).abs().max(dim=1).values.cpu().numpy())
+    e = np.concatenate(errs)
+    assert np.percentile(e, 99) <= 1e-5 and e.max() <= 1e-3, (np.percentile(e, 99), e.max())
+    a.close()
+    b.close()

@@ -58,9 +58,9 @@ def _gpu_out(venv):
 
 
 @pytest.mark.parametrize("env_id", ["PandaReach-v3", "PandaReachDense-v3", "PandaReachJoints-v3"])
-def test_one_step_parity(pg, oracle, env_id):
+def test_one_step_parity(pg, oracle, env_id, lanes):
     n = 512
-    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=3)
+    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=3, lanes_per_env=lanes)
     venv.reset_tensors()
     ref = oracle.OracleVecEnv(venv._cfg, n)
     for k in range(3):  # a few steps so the start states are not all neutral
@@ -78,7 +78,7 @@ def test_one_step_parity(pg, oracle, env_id):
     venv.close()
 
 
-def test_episode_trajectory_parity(pg, oracle):
+def test_episode_trajectory_parity(pg, oracle, lanes):
     """Free-running rollout across an auto-reset.
 
     Positions (ee position, achieved goal) stay within 1e-4 of the oracle for the whole episode.
@@ -89,7 +89,8 @@ def test_episode_trajectory_parity(pg, oracle):
     (DESIGN.md §5).  Without the table: a free-running trajectory through contact events is
     chaotic at fp32 rounding (test_gpu_contacts.py holds those per step)."""
     n = 256
-    venv = pg.PandaVecEnv("PandaReach-v3", num_envs=n, device="cuda:0", seed=11, contacts=False)
+    venv = pg.PandaVecEnv("PandaReach-v3", num_envs=n, device="cuda:0", seed=11, contacts=False,
+                          lanes_per_env=lanes)
     venv.reset_tensors()
     ref = oracle.OracleVecEnv(venv._cfg, n)
     _state_to_oracle(venv, ref)

@@ -20,7 +20,7 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(src=os.path.join(ROOT, "gpurun_out", "pmc"), round_tag="r01", num_envs=4096, kernel="step_kernel<0, 0, 1>"):
+def main(src=os.path.join(ROOT, "gpurun_out", "pmc"), round_tag="r01", num_envs=4096, kernel="step_kernel<0, 0, 1, 0, 1>"):
     agg = defaultdict(list)
     for p in sorted(glob.glob(os.path.join(src, "p*", "run_counter_collection.csv"))):
         for r in csv.DictReader(open(p)):
