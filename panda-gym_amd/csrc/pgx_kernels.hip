@@ -2045,6 +2045,16 @@ __device__ __forceinline__ void ao_store(const PgxDevState& s, int N, int i, con
     }
 }
 
+/* Workgroups are dealt to the 8 XCDs round-robin (block b -> XCD b % 8), each with its own
+ * L2: give every XCD a contiguous range of blocks, so the env-minor state rows one wave
+ * touches share cache lines with its neighbours' on the same L2 instead of being fetched
+ * once per XCD (PMC: 4.3 MB of HBM traffic per 4096-env launch for 0.8 MB of state). */
+__device__ __forceinline__ int xcd_block() {
+    const int nb = gridDim.x, b = blockIdx.x;
+    if (nb % 8) return b;
+    return (b % 8) * (nb / 8) + b / 8;
+}
+
 /* WIDE = 0: one env per lane (64 per wave); WIDE = 1: 16 lanes per env (4 per wave,
  * substep_g), the redundant lanes compute the same values and only the lead lane stores. */
 template <int CONTROL, int OBJ, int CONT, int AO, int WIDE>
@@ -2055,7 +2065,7 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
     const int ln = WIDE ? (int)threadIdx.x / GW : (int)threadIdx.x;   /* env slot in the wave (LDS index) */
     const int c = WIDE ? (int)threadIdx.x % GW : 0;                   /* lane within the env's row */
     const bool lead = c == 0;
-    const int i = blockIdx.x * (WIDE ? EPW : 64) + ln;
+    const int i = xcd_block() * (WIDE ? EPW : 64) + ln;
     const int N = e.n_envs;
     if (i >= N) return;
     const int ii = i;
