@@ -329,18 +329,20 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
      * per SIMD: 4096 x 16 lanes = 1024 waves), one lane per env beyond, where the one-lane
      * waves already fill enough SIMDs (tools/time_layouts.py: Reach at 8192 envs 1.37 ms
      * one-lane vs 1.66 ms wide).  cfg->lanes_per_env (0 = this rule, 1, 16) chooses;
-     * PGX_LANES_PER_ENV=1|16 overrides both (A/B timing).  ReachAO runs one lane per env. */
+     * PGX_LANES_PER_ENV=1|16 overrides both (A/B timing). */
     if (cfg->lanes_per_env != 0 && cfg->lanes_per_env != 1 && cfg->lanes_per_env != 16) {
         delete h;
         return fail(PGX_E_INVALID, "lanes_per_env must be 0, 1 or 16, got %d", cfg->lanes_per_env);
     }
-    e.lanes_per_env = cfg->lanes_per_env ? cfg->lanes_per_env : (cfg->n_envs <= 4096 ? 16 : 1);
+    /* ReachAO's per-substep capsule x obstacle checks spread over the row's lanes, so its wide
+     * layout still wins at 8192 envs (2 waves per SIMD): 1.23 vs 1.48 ms */
+    const int wide_max = e.ao ? 8192 : 4096;
+    e.lanes_per_env = cfg->lanes_per_env ? cfg->lanes_per_env : (cfg->n_envs <= wide_max ? 16 : 1);
     if (const char* lpe = std::getenv("PGX_LANES_PER_ENV")) {
         const int v = std::atoi(lpe);
         if (v != 1 && v != 16) { delete h; return fail(PGX_E_INVALID, "PGX_LANES_PER_ENV must be 1 or 16, got %s", lpe); }
         e.lanes_per_env = v;
     }
-    if (e.ao) e.lanes_per_env = 1;
 
     rc = hip_check(hipSetDevice(device), "hipSetDevice");
     if (rc) { delete h; return rc; }

@@ -1752,7 +1752,8 @@ __device__ constexpr int kAoSlot[PGX_NCAP] = {ao_slot(0), ao_slot(1), ao_slot(2)
                                               ao_slot(10), ao_slot(11), ao_slot(12), ao_slot(13)};
 static_assert(PGX_NCAP == 14, "kAoSlot table");
 
-__device__ __forceinline__ V3 lds3(const float (*a)[64], int ln) { return v3(a[0][ln], a[1][ln], a[2][ln]); }
+template <int W>
+__device__ __forceinline__ V3 lds3(const float (*a)[W], int ln) { return v3(a[0][ln], a[1][ln], a[2][ln]); }
 
 /* signed distance to the axis-aligned box (c, h) */
 __device__ __forceinline__ float box_sd(V3 P, V3 c, V3 h) {
@@ -1821,8 +1822,8 @@ __device__ __forceinline__ float capsule_box(V3 A, V3 B, float r, V3 c, V3 hf, V
 }
 
 /* world end points of every capsule at q (base capsule included) into LDS */
-template <int C = 0>
-__device__ __forceinline__ void ao_caps_walk(const Chain& k, MRef m, ContactLds& L, int ln) {
+template <int C = 0, class LT>
+__device__ __forceinline__ void ao_caps_walk(const Chain& k, MRef m, LT& L, int ln) {
     if constexpr (C < PGX_NCAP) {
         V3 A, B;
         if constexpr (kCapJ[C] < 0) {
@@ -1835,10 +1836,11 @@ __device__ __forceinline__ void ao_caps_walk(const Chain& k, MRef m, ContactLds&
         }
         L.capA[C][0][ln] = A.x; L.capA[C][1][ln] = A.y; L.capA[C][2][ln] = A.z;
         L.capB[C][0][ln] = B.x; L.capB[C][1][ln] = B.y; L.capB[C][2][ln] = B.z;
-        ao_caps_walk<C + 1>(k, m, L, ln);
+        ao_caps_walk<C + 1, LT>(k, m, L, ln);
     }
 }
-__device__ __forceinline__ void ao_caps(MRef m, const float* q, ContactLds& L, int ln) {
+template <class LT>
+__device__ __forceinline__ void ao_caps(MRef m, const float* q, LT& L, int ln) {
     Chain k;
     fk_chain(m, q, k);
     ao_caps_walk(k, m, L, ln);
@@ -1848,7 +1850,8 @@ __device__ __forceinline__ V3 ao_table_c(const PgxDevEnv& e) { return v3(e.table
 __device__ __forceinline__ V3 ao_table_h(const PgxDevEnv& e) { return v3(e.table_hx, e.table_hy, e.table_hz); }
 
 /* check_collided: any collision link within 0 of an obstacle, or links 2..ee of the table */
-__device__ __forceinline__ bool ao_collided(const PgxDevEnv& e, ContactLds& L, int ln) {
+template <class LT>
+__device__ __forceinline__ bool ao_collided(const PgxDevEnv& e, LT& L, int ln) {
     const V3 tc = ao_table_c(e), th = ao_table_h(e);
     const V3 thi = v3(th.x - kAoMargin, th.y - kAoMargin, th.z - kAoMargin);
     const V3 hcube = v3(kAoSize, kAoSize, kAoSize);
@@ -1875,7 +1878,8 @@ __device__ __forceinline__ bool ao_collided(const PgxDevEnv& e, ContactLds& L, i
 }
 
 /* per collision link: the closest obstacle's distance and unit vector into LDS */
-__device__ __forceinline__ void ao_link_obs(ContactLds& L, int ln) {
+template <class LT>
+__device__ __forceinline__ void ao_link_obs(LT& L, int ln) {
     for (int l = 0; l < PGX_AO_LINKS; l++) L.aoD[l][ln] = 3.0e38f;
     const V3 hcube = v3(kAoSize, kAoSize, kAoSize);
     for (int c = 0; c < PGX_NCAP; c++) {
@@ -1912,9 +1916,98 @@ __device__ __forceinline__ void ao_link_obs(ContactLds& L, int ln) {
     }
 }
 
+/* Wide layout (16 lanes per env): lane c evaluates capsule c (14 capsules) against the six
+ * obstacles and the table, the same per-pair arithmetic as ao_collided / ao_link_obs; the env's
+ * decision is the OR over its row (ballot), the per-link minimum is combined across the
+ * capsules of one link in capsule order with the sequential code's strict '<' (the earlier
+ * capsule keeps a tie). */
+__device__ __forceinline__ bool row_any(bool v) {
+    return ((__ballot(v) >> (threadIdx.x & ~(unsigned)(GW - 1))) & 0xFFFFull) != 0ull;
+}
+template <class LT>
+__device__ __forceinline__ bool ao_collided_g(const PgxDevEnv& e, LT& L, int es, int c) {
+    const V3 tc = ao_table_c(e), th = ao_table_h(e);
+    const V3 thi = v3(th.x - kAoMargin, th.y - kAoMargin, th.z - kAoMargin);
+    const V3 hcube = v3(kAoSize, kAoSize, kAoSize);
+    const int cc = c < PGX_NCAP ? c : 0;
+    const int slot = c < PGX_NCAP ? kAoSlot[cc] : -1;
+    bool hit = false;
+    if (slot >= 0) {
+        const V3 A = lds3(L.capA[cc], es), B = lds3(L.capB[cc], es);
+        const float r = kCapR[cc];
+        for (int o = 0; o < AO_N; o++) {
+            const V3 C = lds3(L.aoC[o], es);
+            const V3 P = seg_closest(A, B, C);
+            const float dc = norm(C - P) - r;
+            if (o < 3) hit = hit || dc - kAoSize <= 0.0f;
+            else if (dc - kAoCubeBound <= 0.0f) hit = hit || capsule_box<false>(A, B, r, C, hcube, nullptr) <= 0.0f;
+        }
+        if (slot >= 1) {
+            const float lb = fminf(box_sd(A, tc, thi), box_sd(B, tc, thi)) - 0.5f * norm(B - A) - kAoMargin - r;
+            if (lb <= 0.0f) hit = hit || capsule_box<false>(A, B, r, tc, th, nullptr) <= 0.0f;
+        }
+    }
+    return row_any(hit);
+}
+__host__ __device__ constexpr bool ao_first_of_slot(int c) {
+    for (int k = 0; k < c; k++)
+        if (ao_slot(k) == ao_slot(c)) return false;
+    return true;
+}
+template <class LT>
+__device__ __forceinline__ void ao_link_obs_g(LT& L, int es, int c) {
+    const V3 hcube = v3(kAoSize, kAoSize, kAoSize);
+    const int cc = c < PGX_NCAP ? c : 0;
+    const int slot = c < PGX_NCAP ? kAoSlot[cc] : -1;
+    float best = 3.0e38f;
+    V3 bu = v3(0.0f, 0.0f, 0.0f);
+    if (slot >= 0) {
+        const V3 A = lds3(L.capA[cc], es), B = lds3(L.capB[cc], es);
+        const float r = kCapR[cc];
+        for (int o = 0; o < AO_N; o++) {
+            const V3 C = lds3(L.aoC[o], es);
+            const V3 P = seg_closest(A, B, C);
+            const V3 v = C - P;
+            const float len = norm(v);
+            if (o < 3) {
+                const float d = len - r - kAoSize;
+                if (d < best) {
+                    best = d;
+                    const V3 n = len > 0.0f ? fast_rcp(len) * v : v3(0.0f, 0.0f, 1.0f);
+                    bu = d > 0.0f ? n : (d < 0.0f ? (-1.0f) * n : v3(0.0f, 0.0f, 0.0f));
+                }
+            } else if (len - r - kAoCubeBound < best) {
+                V3 u;
+                const float d = capsule_box<true>(A, B, r, C, hcube, &u);
+                if (d < best) { best = d; bu = u; }
+            }
+        }
+    }
+    float D[PGX_AO_LINKS], Ux[PGX_AO_LINKS], Uy[PGX_AO_LINKS], Uz[PGX_AO_LINKS];
+    sfor<0, PGX_NCAP>([&](auto kc) __attribute__((always_inline)) {
+        constexpr int C = decltype(kc)::value, sl = ao_slot(C);
+        if constexpr (sl >= 0) {
+            const float b = bcast16<C>(best), x = bcast16<C>(bu.x), y = bcast16<C>(bu.y), z = bcast16<C>(bu.z);
+            if constexpr (ao_first_of_slot(C)) {
+                D[sl] = b; Ux[sl] = x; Uy[sl] = y; Uz[sl] = z;
+            } else {
+                const bool take = b < D[sl];
+                D[sl] = take ? b : D[sl]; Ux[sl] = take ? x : Ux[sl]; Uy[sl] = take ? y : Uy[sl];
+                Uz[sl] = take ? z : Uz[sl];
+            }
+        }
+    });
+#pragma unroll
+    for (int l = 0; l < PGX_AO_LINKS; l++) {
+        L.aoD[l][es] = D[l];
+        L.aoU[l][0][es] = Ux[l]; L.aoU[l][1][es] = Uy[l]; L.aoU[l][2][es] = Uz[l];
+    }
+}
+
 /* robot obs ("ee","js": panda.py:264-288) + 9 distances + 9 unit vectors */
+template <class LT>
 __device__ __forceinline__ void ao_write_obs(float* dst, V3 pos, V3 vel, const float* q, const float* qd,
-                                             const ContactLds& L, int ln) {
+                                             const LT& L, int ln) {
     dst[0] = pos.x; dst[1] = pos.y; dst[2] = pos.z;
     dst[3] = vel.x; dst[4] = vel.y; dst[5] = vel.z;
 #pragma unroll
@@ -1928,7 +2021,8 @@ __device__ __forceinline__ void ao_write_obs(float* dst, V3 pos, V3 vel, const f
 }
 
 /* whole-robot distance (every capsule) to a sphere (kind 0) / rounded cube (1) */
-__device__ __noinline__ float ao_robot_distance(ContactLds& L, int ln, int kind, V3 C, float size) {
+template <class LT>
+__device__ __noinline__ float ao_robot_distance(LT& L, int ln, int kind, V3 C, float size) {
     float best = 3.0e38f;
     const V3 hc = v3(size, size, size);
     for (int c = 0; c < PGX_NCAP; c++) {
@@ -1968,7 +2062,8 @@ __device__ __noinline__ void ao_hollow_sphere(const PgxDevEnv& e, AoDraw& d, dou
 /* ReachAO.reset for reachao_rand (reach_ao.py:965-1082; oracle ao_reset_task): goal,
  * obstacles by rejection against robot / table / dummy sphere, 4-5 active.  Needs the
  * neutral-pose capsules in LDS; leaves the centres in L.aoC. */
-__device__ __noinline__ void ao_reset(const PgxDevEnv& e, ContactLds& L, int ln, uint64_t env, uint32_t episode, V3 ee,
+template <class LT>
+__device__ __noinline__ void ao_reset(const PgxDevEnv& e, LT& L, int ln, uint64_t env, uint32_t episode, V3 ee,
                                       const double* inject_goal, const double* inject_obst, double* goal) {
     AoDraw d{env, episode, 0};
     const V3 tc = ao_table_c(e), th = ao_table_h(e);
@@ -2030,13 +2125,15 @@ __device__ __noinline__ void ao_reset(const PgxDevEnv& e, ContactLds& L, int ln,
             for (int k = 0; k < 3; k++) L.aoC[o][k][ln] = (float)inject_obst[3 * o + k];
 }
 
-__device__ __forceinline__ void ao_load(const PgxDevState& s, int N, int i, ContactLds& L, int ln) {
+template <class LT>
+__device__ __forceinline__ void ao_load(const PgxDevState& s, int N, int i, LT& L, int ln) {
 #pragma unroll
     for (int o = 0; o < AO_N; o++)
 #pragma unroll
         for (int k = 0; k < 3; k++) L.aoC[o][k][ln] = s.obstacles[(3 * o + k) * N + i];
 }
-__device__ __forceinline__ void ao_store(const PgxDevState& s, int N, int i, const ContactLds& L, int ln) {
+template <class LT>
+__device__ __forceinline__ void ao_store(const PgxDevState& s, int N, int i, const LT& L, int ln) {
 #pragma unroll
     for (int o = 0; o < AO_N; o++) {
 #pragma unroll
@@ -2060,7 +2157,6 @@ __device__ __forceinline__ int xcd_block() {
 template <int CONTROL, int OBJ, int CONT, int AO, int WIDE>
 __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict__ mdev, PgxDevEnv e, PgxDevState s,
                                                   const float* __restrict__ action, PgxDevOut o) {
-    static_assert(!(AO && WIDE), "ReachAO runs in the one-lane layout");
     using LT = ContactLdsT<WIDE ? EPW : 64>;
     const int ln = WIDE ? (int)threadIdx.x / GW : (int)threadIdx.x;   /* env slot in the wave (LDS index) */
     const int c = WIDE ? (int)threadIdx.x % GW : 0;                   /* lane within the env's row */
@@ -2137,7 +2233,8 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
         else substep<OBJ, CONT>(mp, e, q, qd, tq, ob, L, ln);
         if constexpr (AO) {   /* ReachAO step_check_collision: check after every substep, stop on contact */
             ao_caps(*fresh(mp), q, *L, ln);
-            if (ao_collided(e, *L, ln)) { collided = true; break; }
+            const bool hit = WIDE ? ao_collided_g(e, *L, ln, c) : ao_collided(e, *L, ln);
+            if (hit) { collided = true; break; }
         }
     }
 
@@ -2165,7 +2262,10 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
         if (o.terminated) o.terminated[i] = term;
         if (o.truncated) o.truncated[i] = trunc;
     }
-    if constexpr (AO) ao_link_obs(*L, ln);
+    if constexpr (AO) {
+        if constexpr (WIDE) ao_link_obs_g(*L, ln, c);
+        else ao_link_obs(*L, ln);
+    }
     if (trunc || term) {
         if (o.terminal_obs && lead) {
             if constexpr (AO) ao_write_obs(o.terminal_obs + (size_t)i * od, pos, vel, q, qd, *L, ln);
@@ -2187,7 +2287,8 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
             ao_caps(mr, q, *L, ln);
             ao_reset(e, *L, ln, e.env_id_offset + (uint64_t)i, episode, pos, nullptr, nullptr, goal);
             episode += 1;
-            ao_link_obs(*L, ln);
+            if constexpr (WIDE) ao_link_obs_g(*L, ln, c);
+            else ao_link_obs(*L, ln);
         } else {
             reset_env<OBJ>(m, e, i, episode, nullptr, nullptr, q, qd, goal, ob);
             ee_state(m, q, qd, pos, vel);
@@ -2322,7 +2423,7 @@ __global__ __launch_bounds__(256) void compute_reward_kernel(const float* __rest
 int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState& s, const float* action,
                     const PgxDevOut& o, void* stream) {
     hipStream_t st = (hipStream_t)stream;
-    const int wide = !e.ao && e.lanes_per_env == GW;
+    const int wide = e.lanes_per_env == GW;
     const int per_block = wide ? EPW : 64;
     dim3 block(64), grid((e.n_envs + per_block - 1) / per_block);
     const int variant = e.ao ? 13 : e.control * 4 + (e.has_object ? 2 : 0) + (e.contacts ? 1 : 0);
@@ -2341,6 +2442,7 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
         case 14: PGX_STEP(1, 1, 1, 0, 0); break;
         case 15: PGX_STEP(1, 1, 1, 0, 1); break;
         case 26: PGX_STEP(1, 0, 1, 1, 0); break;
+        case 27: PGX_STEP(1, 0, 1, 1, 1); break;
         default: return (int)hipErrorInvalidValue;   /* object without contacts: rejected at create */
     }
 #undef PGX_STEP

@@ -100,9 +100,9 @@ def test_device_reset_draws_match_oracle(pg, oracle):
     venv.close()
 
 
-def test_one_step_parity_random_actions(pg, oracle):
+def test_one_step_parity_random_actions(pg, oracle, lanes):
     n = 1024
-    venv = pg.PandaVecEnv(ENV, num_envs=n, device="cuda:0", seed=21)
+    venv = pg.PandaVecEnv(ENV, num_envs=n, device="cuda:0", seed=21, lanes_per_env=lanes)
     venv.reset_tensors(seed=1000)
     ref = oracle.OracleVecEnv(venv._cfg, n)
     errs, flips = [], 0
@@ -129,9 +129,9 @@ def test_one_step_parity_random_actions(pg, oracle):
     venv.close()
 
 
-def test_collision_truncates_with_penalty(pg, oracle):
+def test_collision_truncates_with_penalty(pg, oracle, lanes):
     n = 4
-    venv = pg.PandaVecEnv(ENV, num_envs=n, device="cuda:0", seed=1)
+    venv = pg.PandaVecEnv(ENV, num_envs=n, device="cuda:0", seed=1, lanes_per_env=lanes)
     from oracle.oracle import fk
 
     com, _, _ = fk(venv._cfg.model.contents, np.array(pg.abi.NEUTRAL_Q[:7]))
@@ -177,9 +177,9 @@ def test_success_terminates(pg, oracle):
     venv.close()
 
 
-def test_large_batch_random_rollout(pg):
+def test_large_batch_random_rollout(pg, lanes):
     n = 8192
-    venv = pg.PandaVecEnv(ENV, num_envs=n, device="cuda:0", seed=7)
+    venv = pg.PandaVecEnv(ENV, num_envs=n, device="cuda:0", seed=7, lanes_per_env=lanes)
     venv.reset_tensors()
     resets = 0
     for t in range(30):
