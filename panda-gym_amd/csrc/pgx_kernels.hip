@@ -593,6 +593,135 @@ __device__ __forceinline__ void link_capsules(int j, LT& L, int ln, const M3& R,
  *   qd = clamp(qd_u + M^-1 J^T lambda); q += dt*qd   (constraint pass, stepPositions)
  *   object: p += dt v, orientation by the exponential map of w dt
  * M by composite-rigid-body, b by Newton-Euler with Bullet's link damping. */
+/* a V3 from three lane-minor LDS rows */
+template <int W>
+__device__ __forceinline__ V3 lds3(const float (*a)[W], int ln) { return v3(a[0][ln], a[1][ln], a[2][ln]); }
+
+constexpr int GW = 16;          /* lanes per env: one DPP row */
+constexpr int EPW = 64 / GW;    /* envs per wave */
+using ContactLdsG = ContactLdsT<EPW>;
+
+template <int V>
+struct IC {
+    static constexpr int value = V;
+};
+/* compile-time loop (DPP controls must be constants) */
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+    if constexpr (B < E) {
+        f(IC<B>{});
+        sfor<B + 1, E>(f);
+    }
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
+}
+/* lane SRC of this lane's 16-lane row (DPP row_newbcast, gfx90a+) */
+template <int SRC>
+__device__ __forceinline__ float bcast16(float x) {
+    return dpp<0x150 + SRC>(x);
+}
+/* sum over the 16-lane row, the same bits in every lane: each butterfly step adds two
+ * partner sums that are already equal within their halves, and fl(a+b) = fl(b+a) */
+__device__ __forceinline__ float sum16(float x) {
+    x += dpp<0xB1>(x);    /* quad_perm [1,0,3,2] */
+    x += dpp<0x4E>(x);    /* quad_perm [2,3,0,1] */
+    x += dpp<0x141>(x);   /* row_half_mirror */
+    x += dpp<0x140>(x);   /* row_mirror */
+    return x;
+}
+/* Per-lane selection by row position K as one v_cndmask with a constant lane mask.  Plain
+ * `c == k ? a[k] : v` chains get rewritten by the compiler into a dynamically indexed
+ * stack array (scratch memory); the asm keeps them as selects. */
+template <int K>
+__device__ __forceinline__ float lane_sel(float a, float other) {   /* lanes with c == K take a */
+    constexpr uint64_t mask = 0x0001000100010001ull << K;
+    float r;
+    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(other), "v"(a), "s"(mask));
+    return r;
+}
+/* object coordinate of (lin, ang) for this lane: 7-9 linear, 10-12 angular, else 0 */
+__device__ __forceinline__ float pick_obj(V3 lin, V3 ang) {
+    float v = 0.0f;
+    v = lane_sel<7>(lin.x, v); v = lane_sel<8>(lin.y, v); v = lane_sel<9>(lin.z, v);
+    v = lane_sel<10>(ang.x, v); v = lane_sel<11>(ang.y, v); v = lane_sel<12>(ang.z, v);
+    return v;
+}
+/* this lane's arm entry a[c] (c < 7), else `other` */
+__device__ __forceinline__ float pick_arm(const float* a, float other) {
+    float v = other;
+    sfor<0, NJ>([&](auto kc) __attribute__((always_inline)) { v = lane_sel<decltype(kc)::value>(a[decltype(kc)::value], v); });
+    return v;
+}
+/* generalized coordinate of (arm[7], lin, ang) for this lane: arm dof c < 7, object 7-12, else 0 */
+__device__ __forceinline__ float pick_gen(const float* arm, V3 lin, V3 ang) { return pick_arm(arm, pick_obj(lin, ang)); }
+__device__ __forceinline__ V3 pick_v3(const V3* a) {
+    float x[NJ], y[NJ], zz[NJ];
+#pragma unroll
+    for (int k = 0; k < NJ; k++) { x[k] = a[k].x; y[k] = a[k].y; zz[k] = a[k].z; }
+    return v3(pick_arm(x, 0.0f), pick_arm(y, 0.0f), pick_arm(zz, 0.0f));
+}
+
+/* the 16-lane row's mask of a predicate (bit c = lane c of this env's row) */
+__device__ __forceinline__ unsigned row_ballot(bool v) {
+    return (unsigned)((__ballot(v) >> (threadIdx.x & ~(unsigned)(GW - 1))) & 0xFFFFull);
+}
+__device__ __forceinline__ bool row_any(bool v) { return row_ballot(v) != 0u; }
+
+/* Robot capsule ends vs the table / plane in the wide layout (no object): lane c tests
+ * capsule c's end spheres (the candidates of robot_contacts' table branch); the row keeps
+ * the 4 deepest by (depth, discovery order) like g1_insert -- ranked by broadcast only when
+ * an env has more than 4 -- and every kept candidate goes straight to its id-ordered slot
+ * (ids 2c + end grow with the lane), so sort_groups has nothing left to do. */
+template <class LT>
+__device__ __forceinline__ void robot_table_contacts_g(const PgxDevEnv& e, float tau, LT& L, int es, int c) {
+    const int cc = c < PGX_NCAP ? c : 0;
+    const bool on = c < PGX_NCAP && (kCapFlags[cc] & PGX_CAP_VS_TABLE);
+    const V3 A = lds3(L.capA[cc], es), B = lds3(L.capB[cc], es);
+    const float r = kCapR[cc];
+    const bool two = kCapNs[cc] != 1;
+    const float d0 = A.z - r - ground_z(e, A.x, A.y);
+    const float d1 = B.z - r - ground_z(e, B.x, B.y);
+    const bool c0 = on && d0 < tau, c1 = on && two && d1 < tau;
+    unsigned m0 = row_ballot(c0), m1 = row_ballot(c1);
+    const int total = __builtin_popcount(m0) + __builtin_popcount(m1);
+    bool k0 = c0, k1 = c1;
+    if (__any(total > CG)) {
+        /* rank = candidates strictly before in (depth, discovery = 2 lane + end) order */
+        const float e0 = c0 ? d0 : 3.0e38f, e1 = c1 ? d1 : 3.0e38f;
+        int r0 = 0, r1 = 0;
+        sfor<0, PGX_NCAP>([&](auto kc) __attribute__((always_inline)) {
+            constexpr int K = decltype(kc)::value;
+            const float y0 = bcast16<K>(e0), y1 = bcast16<K>(e1);
+            r0 += (y0 < e0 || (y0 == e0 && K < c)) + (y1 < e0 || (y1 == e0 && K < c));
+            r1 += (y0 < e1 || (y0 == e1 && K <= c)) + (y1 < e1 || (y1 == e1 && K < c));
+        });
+        k0 = c0 && r0 < CG;
+        k1 = c1 && r1 < CG;
+        m0 = row_ballot(k0);
+        m1 = row_ballot(k1);
+    }
+    const unsigned below = (1u << (c & 15)) - 1u;
+    const int base = __builtin_popcount(m0 & below) + __builtin_popcount(m1 & below);
+    const int jc = kCapJ[cc];
+    if (k0) {
+        const int sl = base;
+        L.g1d[sl][es] = d0; L.g1id[sl][es] = (float)(2 * c); L.g1j[sl][es] = jc;
+        L.g1p[sl][0][es] = A.x; L.g1p[sl][1][es] = A.y; L.g1p[sl][2][es] = A.z - r;
+        L.g1n[sl][0][es] = 0.0f; L.g1n[sl][1][es] = 0.0f; L.g1n[sl][2][es] = 1.0f;
+        L.g1rb[sl][0][es] = 0.0f; L.g1rb[sl][1][es] = 0.0f; L.g1rb[sl][2][es] = 0.0f;
+    }
+    if (k1) {
+        const int sl = base + (k0 ? 1 : 0);
+        L.g1d[sl][es] = d1; L.g1id[sl][es] = (float)(2 * c + 1); L.g1j[sl][es] = jc;
+        L.g1p[sl][0][es] = B.x; L.g1p[sl][1][es] = B.y; L.g1p[sl][2][es] = B.z - r;
+        L.g1n[sl][0][es] = 0.0f; L.g1n[sl][1][es] = 0.0f; L.g1n[sl][2][es] = 1.0f;
+        L.g1rb[sl][0][es] = 0.0f; L.g1rb[sl][1][es] = 0.0f; L.g1rb[sl][2][es] = 0.0f;
+    }
+    L.cnt[1][es] = __builtin_popcount(m0) + __builtin_popcount(m1);
+}
+
 /* Per-substep dynamics shared by both solver layouts: contact detection at the current
  * poses (CONT), FK fused with the per-link terms, Newton-Euler bias, CRBA mass matrix,
  * Cholesky, the unconstrained velocities vu = clamp(qd + dt M^-1 (-b)) and M^-1 (lower
@@ -604,9 +733,9 @@ struct Dyn {
     V3 vcu, wcu;
 };
 
-template <int OBJ, int CONT, class LT>
+template <int OBJ, int CONT, class LT, bool PAR = false>
 __device__ __forceinline__ void substep_dyn(MRef m, const PgxDevEnv& e, const float* q, const float* qd,
-                                            const ObjState& ob, LT* Lp, int ln, Dyn& D) {
+                                            const ObjState& ob, LT* Lp, int ln, Dyn& D, int lane = 0) {
     M3 Rc;
     if (OBJ) Rc = quat_mat(ob);
     if (CONT) { Lp->cnt[0][ln] = 0; Lp->cnt[1][ln] = 0; }
@@ -653,8 +782,12 @@ __device__ __forceinline__ void substep_dyn(MRef m, const PgxDevEnv& e, const fl
         }
     }
     if (CONT) {
-        robot_contacts<OBJ>(e, m.contact_dist, *Lp, ln, ob, Rc);
-        sort_groups(*Lp, ln);
+        if constexpr (PAR && !OBJ) {
+            robot_table_contacts_g(e, m.contact_dist, *Lp, ln, lane);
+        } else {
+            robot_contacts<OBJ>(e, m.contact_dist, *Lp, ln, ob, Rc);
+            sort_groups(*Lp, ln);
+        }
     }
     PGX_PROF_MARK(1);
     const V3 g = v3(m.gravity[0], m.gravity[1], m.gravity[2]);
@@ -1164,72 +1297,6 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
  * updates and dot products.  Everything else (FK, dynamics, detection, IK, epilogue)
  * runs redundantly and bit-identically on the 16 lanes, so all lanes of an env take the
  * same branches; only the lead lane stores. */
-constexpr int GW = 16;          /* lanes per env: one DPP row */
-constexpr int EPW = 64 / GW;    /* envs per wave */
-using ContactLdsG = ContactLdsT<EPW>;
-
-template <int V>
-struct IC {
-    static constexpr int value = V;
-};
-/* compile-time loop (DPP controls must be constants) */
-template <int B, int E, class F>
-__device__ __forceinline__ void sfor(F&& f) {
-    if constexpr (B < E) {
-        f(IC<B>{});
-        sfor<B + 1, E>(f);
-    }
-}
-template <int CTRL>
-__device__ __forceinline__ float dpp(float x) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
-}
-/* lane SRC of this lane's 16-lane row (DPP row_newbcast, gfx90a+) */
-template <int SRC>
-__device__ __forceinline__ float bcast16(float x) {
-    return dpp<0x150 + SRC>(x);
-}
-/* sum over the 16-lane row, the same bits in every lane: each butterfly step adds two
- * partner sums that are already equal within their halves, and fl(a+b) = fl(b+a) */
-__device__ __forceinline__ float sum16(float x) {
-    x += dpp<0xB1>(x);    /* quad_perm [1,0,3,2] */
-    x += dpp<0x4E>(x);    /* quad_perm [2,3,0,1] */
-    x += dpp<0x141>(x);   /* row_half_mirror */
-    x += dpp<0x140>(x);   /* row_mirror */
-    return x;
-}
-/* Per-lane selection by row position K as one v_cndmask with a constant lane mask.  Plain
- * `c == k ? a[k] : v` chains get rewritten by the compiler into a dynamically indexed
- * stack array (scratch memory); the asm keeps them as selects. */
-template <int K>
-__device__ __forceinline__ float lane_sel(float a, float other) {   /* lanes with c == K take a */
-    constexpr uint64_t mask = 0x0001000100010001ull << K;
-    float r;
-    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(other), "v"(a), "s"(mask));
-    return r;
-}
-/* object coordinate of (lin, ang) for this lane: 7-9 linear, 10-12 angular, else 0 */
-__device__ __forceinline__ float pick_obj(V3 lin, V3 ang) {
-    float v = 0.0f;
-    v = lane_sel<7>(lin.x, v); v = lane_sel<8>(lin.y, v); v = lane_sel<9>(lin.z, v);
-    v = lane_sel<10>(ang.x, v); v = lane_sel<11>(ang.y, v); v = lane_sel<12>(ang.z, v);
-    return v;
-}
-/* this lane's arm entry a[c] (c < 7), else `other` */
-__device__ __forceinline__ float pick_arm(const float* a, float other) {
-    float v = other;
-    sfor<0, NJ>([&](auto kc) __attribute__((always_inline)) { v = lane_sel<decltype(kc)::value>(a[decltype(kc)::value], v); });
-    return v;
-}
-/* generalized coordinate of (arm[7], lin, ang) for this lane: arm dof c < 7, object 7-12, else 0 */
-__device__ __forceinline__ float pick_gen(const float* arm, V3 lin, V3 ang) { return pick_arm(arm, pick_obj(lin, ang)); }
-__device__ __forceinline__ V3 pick_v3(const V3* a) {
-    float x[NJ], y[NJ], zz[NJ];
-#pragma unroll
-    for (int k = 0; k < NJ; k++) { x[k] = a[k].x; y[k] = a[k].y; zz[k] = a[k].z; }
-    return v3(pick_arm(x, 0.0f), pick_arm(y, 0.0f), pick_arm(zz, 0.0f));
-}
-
 /* One stepSimulation() in the wide layout: the same restatement as substep() (dynamics
  * shared through substep_dyn), rows solved in the same order with the same exit rule. */
 template <int OBJ, int CONT>
@@ -1237,7 +1304,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                                           ObjState& ob, ContactLdsG* Lp, int es, int c) {
     MRef m = *fresh(mp);
     Dyn D;
-    substep_dyn<OBJ, CONT>(m, e, q, qd, ob, Lp, es, D);
+    substep_dyn<OBJ, CONT, ContactLdsG, true>(m, e, q, qd, ob, Lp, es, D, c);
     const V3 (&z)[NJ] = D.z;
     const V3 (&o)[NJ] = D.o;
     const float (&Mi)[NJ][NJ] = D.Mi;
@@ -1752,8 +1819,6 @@ __device__ constexpr int kAoSlot[PGX_NCAP] = {ao_slot(0), ao_slot(1), ao_slot(2)
                                               ao_slot(10), ao_slot(11), ao_slot(12), ao_slot(13)};
 static_assert(PGX_NCAP == 14, "kAoSlot table");
 
-template <int W>
-__device__ __forceinline__ V3 lds3(const float (*a)[W], int ln) { return v3(a[0][ln], a[1][ln], a[2][ln]); }
 
 /* signed distance to the axis-aligned box (c, h) */
 __device__ __forceinline__ float box_sd(V3 P, V3 c, V3 h) {
@@ -1921,9 +1986,6 @@ __device__ __forceinline__ void ao_link_obs(LT& L, int ln) {
  * decision is the OR over its row (ballot), the per-link minimum is combined across the
  * capsules of one link in capsule order with the sequential code's strict '<' (the earlier
  * capsule keeps a tie). */
-__device__ __forceinline__ bool row_any(bool v) {
-    return ((__ballot(v) >> (threadIdx.x & ~(unsigned)(GW - 1))) & 0xFFFFull) != 0ull;
-}
 template <class LT>
 __device__ __forceinline__ bool ao_collided_g(const PgxDevEnv& e, LT& L, int es, int c) {
     const V3 tc = ao_table_c(e), th = ao_table_h(e);
