@@ -1518,7 +1518,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
      * with v_d the row's velocity: one DPP-sourced v_sub/v_add of the broadcast delta-v off
      * a sum formed off the chain; delta' = delta den is the residual Bullet tracks, and the
      * coordinate updates take the columns pre-multiplied by jinv.  Chain per row:
-     * v_sub_dpp -> med3 -> sub -> fmac (the next broadcast's source). */
+     * v_sub_dpp -> med3 -> fmac (the next broadcast's source). */
     float mcs[NJ], wms[NJ], mhi[NJ], lhi[NJ];
 #pragma unroll
     for (int d = 0; d < NJ; d++) {
@@ -1530,11 +1530,12 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     auto mrow = [&](auto rc, float& resid) __attribute__((always_inline)) {
         constexpr int r = decltype(rc)::value;
         constexpr int kind = kPgxRowCode[r] >> 4, d = kPgxRowCode[r] & 15;
-        const float t = lam[r] + rhs[r];
-        const float x = kind == 2 ? t + bcast16<d>(gv) : t - bcast16<d>(gv);
-        const float nl = kind == 0 ? __builtin_amdgcn_fmed3f(x, -mhi[d], mhi[d]) : __builtin_amdgcn_fmed3f(x, 0.0f, lhi[d]);
-        const float delta = nl - lam[r];
-        lam[r] = nl;
+        /* delta' = clamp(rhs' - s v_d, lo' - lambda', hi' - lambda'): the shifted bounds are
+         * formed off the chain, so the clamp yields the impulse increment directly */
+        const float x = kind == 2 ? rhs[r] + bcast16<d>(gv) : rhs[r] - bcast16<d>(gv);
+        const float delta = kind == 0 ? __builtin_amdgcn_fmed3f(x, -mhi[d] - lam[r], mhi[d] - lam[r])
+                                      : __builtin_amdgcn_fmed3f(x, -lam[r], lhi[d] - lam[r]);
+        lam[r] += delta;
         const float sd = kind == 2 ? -delta : delta;
         gv += mcs[d] * sd;
         if constexpr (WROWS) gw += wms[d] * sd;

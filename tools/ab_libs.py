@@ -1,9 +1,37 @@
-import os, sys, json
-sys.argv = [sys.argv[0], "100"]
+"""A/B the step kernel of two builds of libpgx on one box (box-to-box clock variance is a few %):
+alternates the libraries in child processes and prints the median ms per config.
+Usage: python tools/ab_libs.py libA.so libB.so"""
+import json
+import os
+import subprocess
+import sys
+
+CASES = [("PandaReach-v3", 4096, 1), ("PandaPush-v3", 4096, 1), ("PandaReachAO-v3", 8192, 1), ("PandaReach-v3", 4096, 0)]
+CHILD = r'''
+import os, sys, json, torch
 sys.path.insert(0, os.getcwd())
-import tools.time_layouts as T
-T.CASES = [("PandaReach-v3", 4096, True), ("PandaReach-v3", 4096, False), ("PandaPush-v3", 4096, True)]
-os.environ["PGX_LANES_PER_ENV"] = "1"
-for env_id, n, c in T.CASES:
-    ms = [T.run(env_id, n, c, 100) for _ in range(3)]
-    print(json.dumps({"lib": os.environ.get("PGX_LIB", "new"), "env": env_id, "contacts": c, "ms": [round(x, 4) for x in ms]}), flush=True)
+import panda_gym_amd as pg
+env_id, n, contacts = sys.argv[1], int(sys.argv[2]), bool(int(sys.argv[3]))
+venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=0, contacts=contacts)
+venv.reset_tensors()
+for t in range(30):
+    venv.step_tensors(venv.sample_actions(t))
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+torch.cuda.synchronize(); e0.record()
+for t in range(100):
+    venv.step_tensors(venv.sample_actions(30 + t))
+e1.record(); torch.cuda.synchronize()
+print(e0.elapsed_time(e1) / 100)
+'''
+
+if __name__ == "__main__":
+    libs = sys.argv[1:3]
+    res = {lib: {c[0] + str(c[1]) + ("" if c[2] else "-free"): [] for c in CASES} for lib in libs}
+    for rep in range(3):
+        for lib in libs:
+            for env_id, n, contacts in CASES:
+                out = subprocess.run([sys.executable, "-c", CHILD, env_id, str(n), str(contacts)], capture_output=True,
+                                     text=True, env={**os.environ, "PGX_LIB": os.path.abspath(lib)}, timeout=120)
+                res[lib][env_id + str(n) + ("" if contacts else "-free")].append(float(out.stdout.strip().split()[-1]))
+    for lib in libs:
+        print(json.dumps({"lib": os.path.basename(lib), **{k: round(sorted(v)[1], 4) for k, v in res[lib].items()}}))
