@@ -23,10 +23,11 @@
 
 /* ----------------------------------------------------------------- small vec */
 /* diagnostics (tools/diag_iterations.py): histograms of PGS sweeps [0,64), contact
- * points per substep [64,80) and IK iterations [80,112); not part of the restatement */
-int64_t pgxo_diag_hist[112];
+ * points per substep [64,80), IK iterations [80,112), substeps ending with a joint-limit
+ * impulse [112], with robot contacts [113], both [114]; not part of the restatement */
+int64_t pgxo_diag_hist[128];
 void pgxo_diag_read(int64_t* out, int clear) {
-    for (int i = 0; i < 112; i++) { out[i] = pgxo_diag_hist[i]; if (clear) pgxo_diag_hist[i] = 0; }
+    for (int i = 0; i < 128; i++) { out[i] = pgxo_diag_hist[i]; if (clear) pgxo_diag_hist[i] = 0; }
 }
 
 static void v3_cross(const double* a, const double* b, double* o) {
@@ -687,6 +688,12 @@ static void substep_impl(const pgx_model* m, const pgx_sim_params* p, const doub
     if (st) st->solver_iterations = it_used;
     pgxo_diag_hist[it_used < 63 ? it_used : 63]++;
     pgxo_diag_hist[64 + (ncon < 15 ? ncon : 15)]++;
+    {
+        int lim = 0, rob = 0;
+        for (int r = 0; r < nr; r++) lim |= m->row_kind[r] != PGX_ROW_MOTOR && lam[r] != 0.0;
+        for (int c2 = 0; c2 < ncon; c2++) rob |= con[c2].grp != 0;
+        pgxo_diag_hist[112] += lim; pgxo_diag_hist[113] += rob; pgxo_diag_hist[114] += lim && rob;
+    }
     double vn[D];
     for (int d = 0; d < nd; d++) vn[d] = clampd(vu[d] + dv[d], -p->max_coord_vel, p->max_coord_vel);
     if (p->flags & PGX_FLAG_CONSTRAINT_PASS_BIAS) {

@@ -336,6 +336,9 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     }
     /* ReachAO's per-substep capsule x obstacle checks spread over the row's lanes, so its wide
      * layout still wins at 8192 envs (2 waves per SIMD): 1.23 vs 1.48 ms */
+    /* test hook for the exactness of the speculative limit-row skip (substep_g) */
+    e.pgs_mode = 0;
+    if (const char* pm = std::getenv("PGX_PGS_MODE")) e.pgs_mode = std::atoi(pm);
     const int wide_max = e.ao ? 8192 : 4096;
     e.lanes_per_env = cfg->lanes_per_env ? cfg->lanes_per_env : (cfg->n_envs <= wide_max ? 16 : 1);
     if (const char* lpe = std::getenv("PGX_LANES_PER_ENV")) {

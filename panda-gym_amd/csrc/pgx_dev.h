@@ -59,6 +59,8 @@ struct PgxDevEnv {
     int32_t terminate_on_success;
     double collision_reward;
     int32_t lanes_per_env;         /* step layout: 1 (env per lane) or 16 (env per DPP row) */
+    int32_t pgs_mode;              /* test hook (PGX_PGS_MODE): 0 auto, 2 never speculate on the limit
+                                      rows, 3 always redo the speculative solve with them */
 };
 
 struct PgxDevState {

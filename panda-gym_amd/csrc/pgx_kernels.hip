@@ -1502,7 +1502,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         }
     };
     /* exact limit-row skip (see substep()) */
-    bool far = n1 == 0;
+    bool far_nc = true;   /* the motor-impulse bound alone keeps every limit row idle */
 #pragma unroll
     for (int d = 0; d < NJ; d++) {
         float B = 0.0f;
@@ -1510,8 +1510,9 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         for (int k = 0; k < NJ; k++) B += fabsf(MINV(d, k)) * m.max_impulse[k];
         B = B * 1.001f + 1e-6f;
         const float penl = q[d] - kLower[d], penu = kUpper[d] - q[d];
-        far = far && penl > 0.0f && penu > 0.0f && (vu[d] - B) > -penl * m.inv_dt && (vu[d] + B) < penu * m.inv_dt;
+        far_nc = far_nc && penl > 0.0f && penu > 0.0f && (vu[d] - B) > -penl * m.inv_dt && (vu[d] + B) < penu * m.inv_dt;
     }
+    const bool far = far_nc && n1 == 0;
     /* Rows in scaled units: each row equation multiplied by its den (= J M^-1 J^T), so
      * lambda' = lambda den, rhs' = rhs den and the unclamped update is
      *   lambda' + delta' = (lambda' + rhs') - s v_d        (jinv den = 1)
@@ -1608,12 +1609,28 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     PGX_PROF_MARK(3);
     PGX_PROF_COUNT(9, 1);
     PGX_PROF_SWEEPS_DECL;
-    if (__all(far)) {
+    /* Three solves, chosen per wave.  far: the motor-impulse bound proves every limit row
+     * idle and there are no robot contacts -> motor (+ object contact) rows only.  Else, if
+     * the motor-impulse bound alone holds (only robot-contact impulses, unbounded, stand in
+     * the way), the sweeps run speculatively without the limit rows and every lane checks,
+     * at each position the limit block would take in the order, that its dof's two limit
+     * rows would compute x' <= 0 there (delta' = 0: the block would be a no-op, bit for
+     * bit); a wave in which any env fails that check (0.05 % of contact substeps, fp64
+     * oracle under the random policy) is solved again from the same start with the limit
+     * rows.  Otherwise all 21 joint rows run. */
+    float rl_c = -1.0f, ru_c = -1.0f;
+    bool viol = false;
+    auto limit_check = [&]() __attribute__((always_inline)) {
+        viol = viol || (rl_c - gv > 0.0f) || (ru_c + gv > 0.0f);
+    };
+    auto solve = [&](auto mode_c) __attribute__((always_inline)) {
+        constexpr int MODE = decltype(mode_c)::value;   /* 0 far, 1 speculative, 2 all rows */
         for (int it = 0; it < n_it; it += 2) {
             float resid = 0.0f;
+            if constexpr (MODE == 1) limit_check();
             sfor<0, PGX_N_ROWS>([&](auto i) __attribute__((always_inline)) {
                 constexpr int r = PGX_N_ROWS - 1 - decltype(i)::value;
-                if constexpr ((kPgxRowCode[r] >> 4) == 0) mrow(IC<r>{}, resid);
+                if constexpr (MODE == 2 || (kPgxRowCode[r] >> 4) == 0) mrow(IC<r>{}, resid);
             });
             if (CONT && any_contact) contact_rows(resid);
             PGX_PROF_SWEEP();
@@ -1621,26 +1638,53 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             resid = 0.0f;
             sfor<0, PGX_N_ROWS>([&](auto i) __attribute__((always_inline)) {
                 constexpr int r = decltype(i)::value;
-                if constexpr ((kPgxRowCode[r] >> 4) == 0) mrow(IC<r>{}, resid);
+                if constexpr (MODE == 2 || (kPgxRowCode[r] >> 4) == 0) mrow(IC<r>{}, resid);
             });
+            if constexpr (MODE == 1) limit_check();
             if (CONT && any_contact) contact_rows(resid);
             PGX_PROF_SWEEP();
             if (resid * resid <= m.residual_thr) break;
         }
+    };
+    if (__all(far)) {
+        solve(IC<0>{});
     } else {
         PGX_PROF_COUNT(10, 1);
         init_limit_rows();
-        for (int it = 0; it < n_it; it += 2) {
-            float resid = 0.0f;
-            sfor<0, PGX_N_ROWS>([&](auto i) __attribute__((always_inline)) { mrow(IC<PGX_N_ROWS - 1 - decltype(i)::value>{}, resid); });
-            if (CONT && any_contact) contact_rows(resid);
-            PGX_PROF_SWEEP();
-            if (resid * resid <= m.residual_thr || it + 1 >= n_it) break;
-            resid = 0.0f;
-            sfor<0, PGX_N_ROWS>([&](auto i) __attribute__((always_inline)) { mrow(i, resid); });
-            if (CONT && any_contact) contact_rows(resid);
-            PGX_PROF_SWEEP();
-            if (resid * resid <= m.residual_thr) break;
+        /* (not for the object tasks: a third copy of their 24-row sweep grows the kernel past
+         * the instruction cache -- Push measured 1.6 -> 2.4 ms) */
+        if (!OBJ && __all(far_nc) && e.pgs_mode != 2) {
+            float rl[NJ], ru[NJ];
+#pragma unroll
+            for (int r = NJ; r < PGX_N_ROWS; r++) {
+                const int kind = kPgxRowCode[r] >> 4, d = kPgxRowCode[r] & 15;
+                if (kind == 1) rl[d] = rhs[r];
+                else ru[d] = rhs[r];
+            }
+            rl_c = pick_arm(rl, -1.0f);
+            ru_c = pick_arm(ru, -1.0f);
+            const float gv0 = gv, gw0 = gw;
+            float cl0[NPP];
+#pragma unroll
+            for (int p = 0; p < NP; p++) cl0[p] = clam[p][0];
+            solve(IC<1>{});
+            if (__any(row_any(viol)) || e.pgs_mode == 3) {
+                PGX_PROF_COUNT(12, 1);
+                gv = gv0;
+                gw = gw0;
+#pragma unroll
+                for (int p = 0; p < NP; p++) {
+                    clam[p][0] = cl0[p];
+                    clam[p][1] = 0.0f;
+                    clam[p][2] = 0.0f;
+                }
+#pragma unroll
+                for (int r = 0; r < PGX_N_ROWS; r++) lam[r] = 0.0f;
+                solve(IC<2>{});
+            }
+        } else {
+            PGX_PROF_COUNT(13, 1);
+            solve(IC<2>{});
         }
     }
 #undef MINV

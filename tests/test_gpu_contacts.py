@@ -181,3 +181,28 @@ def test_layouts_agree_per_step(pg, env_id):
     assert np.percentile(e, 99) <= 1e-5 and e.max() <= 1e-3, (np.percentile(e, 99), e.max())
     a.close()
     b.close()
+
+
+def test_speculative_limit_skip_is_exact(pg, monkeypatch):
+    """substep_g solves contact substeps without the joint-limit rows when the motor-impulse
+    bound alone keeps them idle, checks at every limit-block position that they would have
+    computed a zero impulse, and redoes the solve with them otherwise.  The claim is bit-exact
+    equality with the all-rows solve: compared here against PGX_PGS_MODE=2 (never speculate)
+    and PGX_PGS_MODE=3 (always redo), on table-contact Reach steps from the same states."""
+    n = 256
+    runs = {}
+    for mode in ("0", "2", "3"):
+        monkeypatch.setenv("PGX_PGS_MODE", mode)
+        v = pg.PandaVecEnv("PandaReach-v3", num_envs=n, device="cuda:0", seed=9, lanes_per_env=16)
+        v.reset_tensors(seed=9)
+        outs = []
+        for t in range(25):
+            a = torch.zeros((n, 3), device="cuda:0")
+            a[:, 2] = -1.0                          # press the tool bar onto the table
+            a[:, :2] = v.sample_actions(t)[:, :2]
+            v.step_tensors(a)
+            outs.append(torch.cat([v.obs, v.state()["qd"].T], 1).cpu().numpy().copy())
+        runs[mode] = np.stack(outs)
+        v.close()
+    assert np.array_equal(runs["0"], runs["2"])
+    assert np.array_equal(runs["0"], runs["3"])

@@ -23,7 +23,7 @@ cfg = abi.make_config(abi.EnvSpec(task=task), n, model, params, contacts=True)
 env = O.OracleVecEnv(cfg, n)
 env.reset()
 lib = O.lib()
-h = (C.c_int64 * 112)()
+h = (C.c_int64 * 128)()
 lib.pgxo_diag_read(h, 1)
 sweeps = np.zeros(64)
 cons = np.zeros(16)
@@ -33,9 +33,11 @@ for t in range(steps):
     lib.pgxo_diag_read(h, 1)
     a = np.array(h[:])
     sweeps += a[:64]; cons += a[64:80]; ik += a[80:112]
+    lim = a[112:115] + (lim if t else 0)
 tot = sweeps.sum()
 mean = (sweeps * np.arange(64)).sum() / tot
 print(f"substeps {int(tot)}: mean PGS sweeps {mean:.1f}; share at 50: {sweeps[50] / tot:.2f}")
 print("sweep histogram (count>0):", {i: int(c) for i, c in enumerate(sweeps) if c})
 print("contact points per substep:", {i: int(c) for i, c in enumerate(cons) if c})
 print(f"IK iterations mean {(ik * np.arange(32)).sum() / ik.sum():.1f}:", {i: int(c) for i, c in enumerate(ik) if c})
+print(f"substeps with a joint-limit impulse {lim[0] / tot:.4f}, with robot contacts {lim[1] / tot:.3f}, both {lim[2] / tot:.4f}")

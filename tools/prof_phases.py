@@ -45,6 +45,7 @@ def run(env_id, n, contacts, launches=100, warm=50):
            "share": {NAMES[k]: round(per[k] / tot, 3) for k in range(7)},
            "sweeps_per_substep": per[8] / max(per[9], 1e-9), "nonfar_frac": per[10] / max(per[9], 1e-9),
            "contact_substep_frac": per[11] / max(per[9], 1e-9),
+           "speculation_redo_frac": per[12] / max(per[9], 1e-9), "all_rows_frac": per[13] / max(per[9], 1e-9),
            "cycles_per_sweep": per[4] / max(per[8], 1e-9)}
     venv.close()
     return out
