@@ -1881,7 +1881,7 @@ __device__ __forceinline__ V3 seg_closest(V3 A, V3 B, V3 C) {
     return A + t * ab;
 }
 
-/* capsule (A, B, r) vs rounded box (c, full half extents hf): 40 ternary-search steps
+/* capsule (A, B, r) vs rounded box (c, full half extents hf): a golden-section search
  * on the inner box's signed distance along the axis; the unit vector (from the
  * capsule's closest point to the box's, utils.unit_vector) when asked for */
 template <bool VEC>
@@ -1891,10 +1891,22 @@ __device__ __forceinline__ float capsule_box(V3 A, V3 B, float r, V3 c, V3 hf, V
     float lo = 0.0f, hi = 1.0f;
     const bool seg = dot(ab, ab) > 0.0f;
     if (seg) {
-        for (int it = 0; it < 40; it++) {
-            const float m1 = lo + (hi - lo) * (1.0f / 3.0f), m2 = hi - (hi - lo) * (1.0f / 3.0f);
-            if (box_sd(A + m1 * ab, c, h) <= box_sd(A + m2 * ab, c, h)) hi = m2;
-            else lo = m1;
+        /* golden-section search of the convex box_sd along the axis: one evaluation per step,
+         * 34 steps shrink [0, 1] to 0.618^34 = 8e-8 (the ternary search's 40 steps of two
+         * evaluations reach 9e-8) */
+        const float gr = 0.61803398875f;
+        float t1 = hi - gr * (hi - lo), t2 = lo + gr * (hi - lo);
+        float f1 = box_sd(A + t1 * ab, c, h), f2 = box_sd(A + t2 * ab, c, h);
+        for (int it = 0; it < 34; it++) {
+            if (f1 <= f2) {
+                hi = t2; t2 = t1; f2 = f1;
+                t1 = hi - gr * (hi - lo);
+                f1 = box_sd(A + t1 * ab, c, h);
+            } else {
+                lo = t1; t1 = t2; f1 = f2;
+                t2 = lo + gr * (hi - lo);
+                f2 = box_sd(A + t2 * ab, c, h);
+            }
         }
     }
     V3 P = A + (seg ? 0.5f * (lo + hi) : 0.0f) * ab;
