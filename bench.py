@@ -270,8 +270,9 @@ def main():
     # on the same random-policy workload: the actions are drawn up front
     K = args.kernel_launches
     acts = torch.empty((K, E, venv.action_dim), dtype=torch.float32, device=dev)
+    base = venv._step_index
     for k in range(K):
-        acts[k].copy_(venv.sample_actions())
+        acts[k].copy_(venv.sample_actions(base + k))   # a fresh Philox draw per launch, as in the timed loop
     stream = torch.cuda.current_stream(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
