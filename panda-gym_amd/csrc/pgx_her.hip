@@ -257,32 +257,46 @@ __global__ __launch_bounds__(64) void sample_kernel(RingPtrs p, RingDims d, int6
         dr[lane] = w;
     }
     __syncthreads();
-    /* phase 2: 16-lane groups copy 4 records per iteration */
+    /* phase 2: 16-lane groups copy 4 records per step; the loads of UNROLL steps are issued
+     * before their stores, so each lane keeps several 16-B reads in flight */
     const int g = lane % GROUP;
-    for (int s = lane / GROUP; s < 64 && b0 + s < B; s += 64 / GROUP) {
-        const Draw& w = dr[s];
-        float* out = o.rows + w.row * d.S;
-        for (int c = g; 4 * c < d.S; c += GROUP) {
-            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (w.rec >= 0) {
-                v = *reinterpret_cast<const float4*>(p.rec + w.rec * d.R + 4 * c);
-                if (w.her) {
-                    float* vv = reinterpret_cast<float*>(&v);
+    constexpr int UNROLL = 4;
+    auto fetch = [&](const Draw& w, int c) {
+        float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (w.rec >= 0 && 4 * c < d.S) v = *reinterpret_cast<const float4*>(p.rec + w.rec * d.R + 4 * c);
+        return v;
+    };
+    auto finish = [&](const Draw& w, int c, float4 v) {
+        if (4 * c >= d.S) return;
+        float* vv = reinterpret_cast<float*>(&v);
+        if (w.rec >= 0 && w.her) {
 #pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        const int f = 4 * c + k;
-                        if (f >= d.dg && f < d.dg + 3) vv[k] = w.goal[f - d.dg];
-                        else if (f >= d.ndg && f < d.ndg + 3) vv[k] = w.goal[f - d.ndg];
-                        else if (f == d.rew) vv[k] = w.reward;
-                    }
-                }
+            for (int k = 0; k < 4; k++) {
+                const int f = 4 * c + k;
+                if (f >= d.dg && f < d.dg + 3) vv[k] = w.goal[f - d.dg];
+                else if (f >= d.ndg && f < d.ndg + 3) vv[k] = w.goal[f - d.ndg];
+                else if (f == d.rew) vv[k] = w.reward;
             }
-            /* the record's ep_start/ep_length may share the last float4: not part of a row */
-            float* vv = reinterpret_cast<float*>(&v);
+        }
+        /* the record's ep_start/ep_length may share the last float4: not part of a row */
 #pragma unroll
-            for (int k = 0; k < 4; k++)
-                if (4 * c + k >= d.eps) vv[k] = 0.0f;
-            *reinterpret_cast<float4*>(out + 4 * c) = v;
+        for (int k = 0; k < 4; k++)
+            if (4 * c + k >= d.eps) vv[k] = 0.0f;
+        *reinterpret_cast<float4*>(o.rows + w.row * d.S + 4 * c) = v;
+    };
+    for (int c = g; 4 * c < d.S; c += GROUP) {
+        for (int s0 = lane / GROUP; s0 < 64; s0 += UNROLL * (64 / GROUP)) {
+            float4 v[UNROLL];
+#pragma unroll
+            for (int u = 0; u < UNROLL; u++) {
+                const int s = s0 + u * (64 / GROUP);
+                v[u] = (s < 64 && b0 + s < B) ? fetch(dr[s], c) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
+#pragma unroll
+            for (int u = 0; u < UNROLL; u++) {
+                const int s = s0 + u * (64 / GROUP);
+                if (s < 64 && b0 + s < B) finish(dr[s], c, v[u]);
+            }
         }
     }
 }
