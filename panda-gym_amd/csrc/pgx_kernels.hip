@@ -850,6 +850,7 @@ __device__ __forceinline__ void substep_dyn(MRef m, const PgxDevEnv& e, const fl
         }
     }
 
+    PGX_PROF_MARK(14);
     /* composite-rigid-body mass matrix (lower triangle, row >= col) */
     float Mt[NJ][NJ];
     {
@@ -882,6 +883,7 @@ __device__ __forceinline__ void substep_dyn(MRef m, const PgxDevEnv& e, const fl
         for (int j = 0; j < NJ; j++) vu[j] = fminf(fmaxf(qd[j] + m.dt * qdd[j], -m.max_vel), m.max_vel);
     }
 
+    PGX_PROF_MARK(15);
     /* M^-1 = L^-T L^-1 (symmetric, lower triangle kept) */
     float (&Mi)[NJ][NJ] = D.Mi;
     {

@@ -38,7 +38,7 @@ def run(env_id, n, contacts, launches=100, warm=50):
     lib.pgx_prof_read(buf, 1)
     waves = n // 64
     per = [buf[k] / (waves * launches) for k in range(16)]
-    tot = sum(per[:7])
+    tot = sum(per[:7]) + per[14] + per[15]
     out = {"env_id": env_id, "n": n, "contacts": contacts, "ms_per_step": ms,
            "cycles_per_wave_step": tot, "clock_ghz_est": tot / (ms * 1e6),
            "phases": {NAMES[k]: round(per[k]) for k in range(7)},
@@ -46,7 +46,9 @@ def run(env_id, n, contacts, launches=100, warm=50):
            "sweeps_per_substep": per[8] / max(per[9], 1e-9), "nonfar_frac": per[10] / max(per[9], 1e-9),
            "contact_substep_frac": per[11] / max(per[9], 1e-9),
            "speculation_redo_frac": per[12] / max(per[9], 1e-9), "all_rows_frac": per[13] / max(per[9], 1e-9),
-           "cycles_per_sweep": per[4] / max(per[8], 1e-9)}
+           "cycles_per_sweep": per[4] / max(per[8], 1e-9),
+           "dynamics_split": {"newton_euler": round(per[14]), "crba_cholesky": round(per[15]),
+                              "minv_and_rest": round(per[2])}}
     venv.close()
     return out
 
