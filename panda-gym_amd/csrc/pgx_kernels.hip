@@ -126,6 +126,100 @@ __device__ __forceinline__ void joint_sincos(float x, float* s_out, float* c_out
     *c_out = ((q + 1) & 2) ? -cc : cc;
 }
 
+/* a V3 from three lane-minor LDS rows */
+template <int W>
+__device__ __forceinline__ V3 lds3(const float (*a)[W], int ln) { return v3(a[0][ln], a[1][ln], a[2][ln]); }
+
+constexpr int GW = 16;          /* lanes per env: one DPP row */
+constexpr int EPW = 64 / GW;    /* envs per wave */
+
+template <int V>
+struct IC {
+    static constexpr int value = V;
+};
+/* compile-time loop (DPP controls must be constants) */
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+    if constexpr (B < E) {
+        f(IC<B>{});
+        sfor<B + 1, E>(f);
+    }
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
+}
+/* lane SRC of this lane's 16-lane row (DPP row_newbcast, gfx90a+) */
+template <int SRC>
+__device__ __forceinline__ float bcast16(float x) {
+    return dpp<0x150 + SRC>(x);
+}
+/* sum over the 16-lane row, the same bits in every lane: each butterfly step adds two
+ * partner sums that are already equal within their halves, and fl(a+b) = fl(b+a) */
+__device__ __forceinline__ float sum16(float x) {
+    x += dpp<0xB1>(x);    /* quad_perm [1,0,3,2] */
+    x += dpp<0x4E>(x);    /* quad_perm [2,3,0,1] */
+    x += dpp<0x141>(x);   /* row_half_mirror */
+    x += dpp<0x140>(x);   /* row_mirror */
+    return x;
+}
+/* Per-lane selection by row position K as one v_cndmask with a constant lane mask.  Plain
+ * `c == k ? a[k] : v` chains get rewritten by the compiler into a dynamically indexed
+ * stack array (scratch memory); the asm keeps them as selects. */
+template <int K>
+__device__ __forceinline__ float lane_sel(float a, float other) {   /* lanes with c == K take a */
+    constexpr uint64_t mask = 0x0001000100010001ull << K;
+    float r;
+    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(other), "v"(a), "s"(mask));
+    return r;
+}
+/* object coordinate of (lin, ang) for this lane: 7-9 linear, 10-12 angular, else 0 */
+__device__ __forceinline__ float pick_obj(V3 lin, V3 ang) {
+    float v = 0.0f;
+    v = lane_sel<7>(lin.x, v); v = lane_sel<8>(lin.y, v); v = lane_sel<9>(lin.z, v);
+    v = lane_sel<10>(ang.x, v); v = lane_sel<11>(ang.y, v); v = lane_sel<12>(ang.z, v);
+    return v;
+}
+/* this lane's arm entry a[c] (c < 7), else `other` */
+__device__ __forceinline__ float pick_arm(const float* a, float other) {
+    float v = other;
+    sfor<0, NJ>([&](auto kc) __attribute__((always_inline)) { v = lane_sel<decltype(kc)::value>(a[decltype(kc)::value], v); });
+    return v;
+}
+/* generalized coordinate of (arm[7], lin, ang) for this lane: arm dof c < 7, object 7-12, else 0 */
+__device__ __forceinline__ float pick_gen(const float* arm, V3 lin, V3 ang) { return pick_arm(arm, pick_obj(lin, ang)); }
+__device__ __forceinline__ V3 pick_v3(const V3* a) {
+    float x[NJ], y[NJ], zz[NJ];
+#pragma unroll
+    for (int k = 0; k < NJ; k++) { x[k] = a[k].x; y[k] = a[k].y; zz[k] = a[k].z; }
+    return v3(pick_arm(x, 0.0f), pick_arm(y, 0.0f), pick_arm(zz, 0.0f));
+}
+
+/* the 16-lane row's mask of a predicate (bit c = lane c of this env's row) */
+__device__ __forceinline__ unsigned row_ballot(bool v) {
+    return (unsigned)((__ballot(v) >> (threadIdx.x & ~(unsigned)(GW - 1))) & 0xFFFFull);
+}
+__device__ __forceinline__ bool row_any(bool v) { return row_ballot(v) != 0u; }
+
+/* sin/cos of the 7 joint angles.  PAR (wide layout, all 16 lanes of an env hold the same
+ * q): lane c evaluates joint c and the row broadcasts, 14 DPP moves instead of 7
+ * polynomial evaluations per lane. */
+template <bool PAR>
+__device__ __forceinline__ void joint_sincos_all(const float* q, float* s, float* c) {
+    if constexpr (PAR) {
+        float ls, lc;
+        joint_sincos(pick_arm(q, 0.0f), &ls, &lc);
+        sfor<0, PGX_NJ>([&](auto jc) __attribute__((always_inline)) {
+            constexpr int j = decltype(jc)::value;
+            s[j] = bcast16<j>(ls);
+            c[j] = bcast16<j>(lc);
+        });
+    } else {
+#pragma unroll
+        for (int j = 0; j < PGX_NJ; j++) joint_sincos(q[j], &s[j], &c[j]);
+    }
+}
+
 /* row-major 3x3 */
 struct M3 {
     float m[9];
@@ -209,15 +303,17 @@ struct Chain {
     V3 o[NJ];
 };
 
+template <bool PAR = false>
 __device__ __forceinline__ void fk_chain(MRef m, const float* q, Chain& k) {
     M3 PR = {{1, 0, 0, 0, 1, 0, 0, 0, 1}};
     V3 PO = v3(m.base[0], m.base[1], m.base[2]);
+    float sj[NJ], cj[NJ];
+    joint_sincos_all<PAR>(q, sj, cj);
 #pragma unroll
     for (int j = 0; j < NJ; j++) {
         M3 R = mulm(PR, kJr[j]);
         V3 o = PO + mulc(PR, kJp[j]);
-        float s, c;
-        joint_sincos(q[j], &s, &c);
+        const float s = sj[j], c = cj[j];
         /* R * Rz(q): rotate the first two columns */
 #pragma unroll
         for (int r = 0; r < 3; r++) {
@@ -311,6 +407,7 @@ __device__ __forceinline__ void chol7_solve(const float L[NJ][NJ], const float* 
  * link's joint pivot; dq = (J^T J + 0.5 I)^-1 J^T e clamped to max|dq|<=pi/4.
  * The orientation error angle is taken as 2*atan2(|v|, w) (== 2*acos(w) for a
  * unit quaternion, but well conditioned in fp32 for small angles). */
+template <bool PAR = false>
 __device__ __forceinline__ void ik(MPtr mp, const float* q0, V3 target, const float* torn, float* qout) {
     float qs[NJ];
 #pragma unroll
@@ -322,7 +419,7 @@ __device__ __forceinline__ void ik(MPtr mp, const float* q0, V3 target, const fl
         if (!(diff > residual)) break;
         MRef m = *fresh(mp);
         Chain k;
-        fk_chain(m, qs, k);
+        fk_chain<PAR>(m, qs, k);
         V3 x = k.o[6] + mulc(k.R[6], kEePivot);
         M3 Ree = mulm(k.R[6], kEeRot);
         float cq[4], dq[4];
@@ -406,6 +503,7 @@ struct ContactLdsT {
     float aoD[PGX_AO_LINKS][W], aoU[PGX_AO_LINKS][3][W];
 };
 using ContactLds = ContactLdsT<64>;   /* one env per lane */
+using ContactLdsG = ContactLdsT<EPW>;
 
 struct ObjState {
     V3 p, v, w;
@@ -593,82 +691,6 @@ __device__ __forceinline__ void link_capsules(int j, LT& L, int ln, const M3& R,
  *   qd = clamp(qd_u + M^-1 J^T lambda); q += dt*qd   (constraint pass, stepPositions)
  *   object: p += dt v, orientation by the exponential map of w dt
  * M by composite-rigid-body, b by Newton-Euler with Bullet's link damping. */
-/* a V3 from three lane-minor LDS rows */
-template <int W>
-__device__ __forceinline__ V3 lds3(const float (*a)[W], int ln) { return v3(a[0][ln], a[1][ln], a[2][ln]); }
-
-constexpr int GW = 16;          /* lanes per env: one DPP row */
-constexpr int EPW = 64 / GW;    /* envs per wave */
-using ContactLdsG = ContactLdsT<EPW>;
-
-template <int V>
-struct IC {
-    static constexpr int value = V;
-};
-/* compile-time loop (DPP controls must be constants) */
-template <int B, int E, class F>
-__device__ __forceinline__ void sfor(F&& f) {
-    if constexpr (B < E) {
-        f(IC<B>{});
-        sfor<B + 1, E>(f);
-    }
-}
-template <int CTRL>
-__device__ __forceinline__ float dpp(float x) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
-}
-/* lane SRC of this lane's 16-lane row (DPP row_newbcast, gfx90a+) */
-template <int SRC>
-__device__ __forceinline__ float bcast16(float x) {
-    return dpp<0x150 + SRC>(x);
-}
-/* sum over the 16-lane row, the same bits in every lane: each butterfly step adds two
- * partner sums that are already equal within their halves, and fl(a+b) = fl(b+a) */
-__device__ __forceinline__ float sum16(float x) {
-    x += dpp<0xB1>(x);    /* quad_perm [1,0,3,2] */
-    x += dpp<0x4E>(x);    /* quad_perm [2,3,0,1] */
-    x += dpp<0x141>(x);   /* row_half_mirror */
-    x += dpp<0x140>(x);   /* row_mirror */
-    return x;
-}
-/* Per-lane selection by row position K as one v_cndmask with a constant lane mask.  Plain
- * `c == k ? a[k] : v` chains get rewritten by the compiler into a dynamically indexed
- * stack array (scratch memory); the asm keeps them as selects. */
-template <int K>
-__device__ __forceinline__ float lane_sel(float a, float other) {   /* lanes with c == K take a */
-    constexpr uint64_t mask = 0x0001000100010001ull << K;
-    float r;
-    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(other), "v"(a), "s"(mask));
-    return r;
-}
-/* object coordinate of (lin, ang) for this lane: 7-9 linear, 10-12 angular, else 0 */
-__device__ __forceinline__ float pick_obj(V3 lin, V3 ang) {
-    float v = 0.0f;
-    v = lane_sel<7>(lin.x, v); v = lane_sel<8>(lin.y, v); v = lane_sel<9>(lin.z, v);
-    v = lane_sel<10>(ang.x, v); v = lane_sel<11>(ang.y, v); v = lane_sel<12>(ang.z, v);
-    return v;
-}
-/* this lane's arm entry a[c] (c < 7), else `other` */
-__device__ __forceinline__ float pick_arm(const float* a, float other) {
-    float v = other;
-    sfor<0, NJ>([&](auto kc) __attribute__((always_inline)) { v = lane_sel<decltype(kc)::value>(a[decltype(kc)::value], v); });
-    return v;
-}
-/* generalized coordinate of (arm[7], lin, ang) for this lane: arm dof c < 7, object 7-12, else 0 */
-__device__ __forceinline__ float pick_gen(const float* arm, V3 lin, V3 ang) { return pick_arm(arm, pick_obj(lin, ang)); }
-__device__ __forceinline__ V3 pick_v3(const V3* a) {
-    float x[NJ], y[NJ], zz[NJ];
-#pragma unroll
-    for (int k = 0; k < NJ; k++) { x[k] = a[k].x; y[k] = a[k].y; zz[k] = a[k].z; }
-    return v3(pick_arm(x, 0.0f), pick_arm(y, 0.0f), pick_arm(zz, 0.0f));
-}
-
-/* the 16-lane row's mask of a predicate (bit c = lane c of this env's row) */
-__device__ __forceinline__ unsigned row_ballot(bool v) {
-    return (unsigned)((__ballot(v) >> (threadIdx.x & ~(unsigned)(GW - 1))) & 0xFFFFull);
-}
-__device__ __forceinline__ bool row_any(bool v) { return row_ballot(v) != 0u; }
-
 /* Robot capsule ends vs the table / plane in the wide layout (no object): lane c tests
  * capsule c's end spheres (the candidates of robot_contacts' table branch); the row keeps
  * the 4 deepest by (depth, discovery order) like g1_insert -- ranked by broadcast only when
@@ -759,12 +781,13 @@ __device__ __forceinline__ void substep_dyn(MRef m, const PgxDevEnv& e, const fl
     {
         M3 PR = {{1, 0, 0, 0, 1, 0, 0, 0, 1}};
         V3 PO = v3(m.base[0], m.base[1], m.base[2]);
+        float sjs[NJ], cjs[NJ];
+        joint_sincos_all<PAR>(q, sjs, cjs);
 #pragma unroll
         for (int j = 0; j < NJ; j++) {
             M3 R = mulm(PR, kJr[j]);
             V3 oj = PO + mulc(PR, kJp[j]);
-            float s, cs;
-            joint_sincos(q[j], &s, &cs);
+            const float s = sjs[j], cs = cjs[j];
 #pragma unroll
             for (int r = 0; r < 3; r++) {
                 float a = R.m[r * 3], b = R.m[r * 3 + 1];
@@ -2332,12 +2355,12 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
 #pragma unroll
         for (int c = 0; c < 3; c++) a[c] = fminf(fmaxf(action[(size_t)ii * A + c], -1.0f), 1.0f);
         Chain k;
-        fk_chain(m, q, k);
+        fk_chain<WIDE != 0>(m, q, k);
         V3 pos = k.o[NJ - 1] + mulc(k.R[NJ - 1], kEeCom);
         V3 tgt = pos + v3(a[0] * m.ee_step, a[1] * m.ee_step, a[2] * m.ee_step);
         tgt.z = fmaxf(0.0f, tgt.z);
         const float torn[4] = {1.0f, 0.0f, 0.0f, 0.0f};
-        ik(mp, q, tgt, torn, tq);
+        ik<WIDE != 0>(mp, q, tgt, torn, tq);
     } else {
 #pragma unroll
         for (int j = 0; j < NJ; j++) {
