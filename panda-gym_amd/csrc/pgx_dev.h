@@ -88,6 +88,9 @@ struct PgxDevOut {
 };
 
 /* launchers (pgx_kernels.hip); return hipError_t as int */
+/* the arm-only (Reach) step kernels: their own translation unit (pgx_kernels.hip, PGX_TU) */
+int pgx_launch_step_arm(const PgxDevModel* m_device, const PgxDevEnv& e, const PgxDevState& s, const float* action,
+                        const PgxDevOut& o, void* stream);
 int pgx_launch_step(const PgxDevModel* m_device, const PgxDevEnv& e, const PgxDevState& s, const float* action,
                     const PgxDevOut& o, void* stream);
 int pgx_launch_reset(const PgxDevModel* m_device, const PgxDevEnv& e, const PgxDevState& s, const uint8_t* mask,

@@ -2564,32 +2564,54 @@ __global__ __launch_bounds__(256) void compute_reward_kernel(const float* __rest
 
 }  // namespace
 
+/* PGX_TU splits the library into two translation units (Makefile): 1 holds the arm-only
+ * step kernels (Reach, both control modes), compiled with SLP vectorisation -- packed
+ * fp32 (v_pk_fma/add/mul_f32) in the redundant per-lane kinematics and dynamics, -2 % on the
+ * headline kernel; 2 holds everything else, compiled without it (the object tasks' register
+ * pressure turns the packed pairs into scratch spills).  0 = one unit (the profiling build). */
+#ifndef PGX_TU
+#define PGX_TU 0
+#endif
+#define PGX_STEP(C, O, K, A, W) hipLaunchKernelGGL((step_kernel<C, O, K, A, W>), grid, block, 0, st, m, e, s, action, o)
+#if PGX_TU != 2
+int pgx_launch_step_arm(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState& s, const float* action,
+                        const PgxDevOut& o, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const int wide = e.lanes_per_env == GW;
+    const int per_block = wide ? EPW : 64;
+    dim3 block(64), grid((e.n_envs + per_block - 1) / per_block);
+    switch ((e.control * 4 + (e.contacts ? 1 : 0)) * 2 + wide) {
+        case 0: PGX_STEP(0, 0, 0, 0, 0); break;
+        case 1: PGX_STEP(0, 0, 0, 0, 1); break;
+        case 2: PGX_STEP(0, 0, 1, 0, 0); break;
+        case 3: PGX_STEP(0, 0, 1, 0, 1); break;
+        case 8: PGX_STEP(1, 0, 0, 0, 0); break;
+        case 9: PGX_STEP(1, 0, 0, 0, 1); break;
+        case 10: PGX_STEP(1, 0, 1, 0, 0); break;
+        case 11: PGX_STEP(1, 0, 1, 0, 1); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+}
+#endif
+#if PGX_TU != 1
 int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState& s, const float* action,
                     const PgxDevOut& o, void* stream) {
+    if (!e.ao && !e.has_object) return pgx_launch_step_arm(m, e, s, action, o, stream);
     hipStream_t st = (hipStream_t)stream;
     const int wide = e.lanes_per_env == GW;
     const int per_block = wide ? EPW : 64;
     dim3 block(64), grid((e.n_envs + per_block - 1) / per_block);
     const int variant = e.ao ? 13 : e.control * 4 + (e.has_object ? 2 : 0) + (e.contacts ? 1 : 0);
-#define PGX_STEP(C, O, K, A, W) hipLaunchKernelGGL((step_kernel<C, O, K, A, W>), grid, block, 0, st, m, e, s, action, o)
     switch (variant * 2 + wide) {
-        case 0: PGX_STEP(0, 0, 0, 0, 0); break;
-        case 1: PGX_STEP(0, 0, 0, 0, 1); break;
-        case 2: PGX_STEP(0, 0, 1, 0, 0); break;
-        case 3: PGX_STEP(0, 0, 1, 0, 1); break;
         case 6: PGX_STEP(0, 1, 1, 0, 0); break;
         case 7: PGX_STEP(0, 1, 1, 0, 1); break;
-        case 8: PGX_STEP(1, 0, 0, 0, 0); break;
-        case 9: PGX_STEP(1, 0, 0, 0, 1); break;
-        case 10: PGX_STEP(1, 0, 1, 0, 0); break;
-        case 11: PGX_STEP(1, 0, 1, 0, 1); break;
         case 14: PGX_STEP(1, 1, 1, 0, 0); break;
         case 15: PGX_STEP(1, 1, 1, 0, 1); break;
         case 26: PGX_STEP(1, 0, 1, 1, 0); break;
         case 27: PGX_STEP(1, 0, 1, 1, 1); break;
         default: return (int)hipErrorInvalidValue;   /* object without contacts: rejected at create */
     }
-#undef PGX_STEP
     return (int)hipGetLastError();
 }
 
@@ -2620,3 +2642,5 @@ int pgx_launch_compute_reward(const float* ag, const float* dg, int64_t n, int32
                        reward_type, (float)thr, out);
     return (int)hipGetLastError();
 }
+#endif  /* PGX_TU != 1 */
+#undef PGX_STEP
