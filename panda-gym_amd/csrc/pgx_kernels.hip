@@ -130,6 +130,7 @@ __device__ __forceinline__ void joint_sincos(float x, float* s_out, float* c_out
 template <int W>
 __device__ __forceinline__ V3 lds3(const float (*a)[W], int ln) { return v3(a[0][ln], a[1][ln], a[2][ln]); }
 
+typedef float f2 __attribute__((ext_vector_type(2)));   /* packed fp32 pair (v_pk_*_f32) */
 constexpr int GW = 16;          /* lanes per env: one DPP row */
 constexpr int EPW = 64 / GW;    /* envs per wave */
 
@@ -1559,8 +1560,16 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         /* delta' = clamp(rhs' - s v_d, lo' - lambda', hi' - lambda'): the shifted bounds are
          * formed off the chain, so the clamp yields the impulse increment directly */
         const float x = kind == 2 ? rhs[r] + bcast16<d>(gv) : rhs[r] - bcast16<d>(gv);
-        const float delta = kind == 0 ? __builtin_amdgcn_fmed3f(x, -mhi[d] - lam[r], mhi[d] - lam[r])
-                                      : __builtin_amdgcn_fmed3f(x, -lam[r], lhi[d] - lam[r]);
+        float delta;
+        if constexpr (kind == 0 && !OBJ) {   /* the bound pair in one v_pk_add_f32 (measured: a
+                                               * gain on the arm tasks, a loss on the object ones) */
+            const f2 b = (f2){-mhi[d], mhi[d]} - lam[r];
+            delta = __builtin_amdgcn_fmed3f(x, b.x, b.y);
+        } else if constexpr (kind == 0) {
+            delta = __builtin_amdgcn_fmed3f(x, -mhi[d] - lam[r], mhi[d] - lam[r]);
+        } else {
+            delta = __builtin_amdgcn_fmed3f(x, -lam[r], lhi[d] - lam[r]);
+        }
         lam[r] += delta;
         const float sd = kind == 2 ? -delta : delta;
         gv += mcs[d] * sd;
@@ -1592,22 +1601,54 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
 #pragma unroll
         for (int q = 0; q < NQ; q++) Wc[q] *= cjinv[q / 3][q % 3];
     }
+    /* shifted bounds as for the joint rows: delta' = clamp(rhs' - w, lo' - lambda', hi' - lambda').
+     * A normal row's upper bound is +inf (0 with lambda' = 0 for an unusable row, below); a
+     * friction row is idle (bounds 0) while its normal impulse is 0. */
+    float chi[NPP];
+#pragma unroll
+    for (int p = 0; p < NP; p++) {
+        chi[p] = rok[p][0] ? 3.0e38f : 0.0f;
+        if (WROWS && !rok[p][0]) clam[p][0] = 0.0f;   /* already applied to gv; the cache stores lambda' jinv = 0 */
+    }
     auto crow = [&](auto pc, auto dc, const bool fr, float& resid) __attribute__((always_inline)) {
         constexpr int p = decltype(pc)::value, dir = decltype(dc)::value;
         const float ln_n = clam[p][0], lm = clam[p][dir];
-        const bool idle = !rok[p][dir] || (fr && !(ln_n > 0.0f));
-        const float lo = idle ? lm : (fr ? -fk[p][dir] * ln_n : 0.0f);
-        const float hi = idle ? lm : (fr ? fk[p][dir] * ln_n : 3.0e38f);
-        float jdv;
-        if constexpr (WROWS) jdv = bcast16<3 * p + dir>(gw);
-        else jdv = sum16(cJ[p][dir] * gv);
-        const float nl = __builtin_amdgcn_fmed3f((lm + crhs[p][dir]) - jdv, lo, hi);
-        const float delta = nl - lm;
-        clam[p][dir] = nl;
+        float delta;
+        if constexpr (WROWS) {
+            float lo, hi;
+            if (fr) {
+                const bool idle = !rok[p][dir] || !(ln_n > 0.0f);
+                const f2 b = (f2){-fk[p][dir], fk[p][dir]} * ln_n - lm;
+                lo = idle ? 0.0f : b.x;
+                hi = idle ? 0.0f : b.y;
+            } else {
+                lo = -lm;
+                hi = chi[p];
+            }
+            delta = __builtin_amdgcn_fmed3f(crhs[p][dir] - bcast16<3 * p + dir>(gw), lo, hi);
+            clam[p][dir] = lm + delta;
+        } else {   /* the object tasks keep the clamped-sum form (measured faster there: Push
+                    * 1.61 vs 1.66 ms, the 16-lane reduction dominates their rows) */
+            const bool idle = !rok[p][dir] || (fr && !(ln_n > 0.0f));
+            const float lo = idle ? lm : (fr ? -fk[p][dir] * ln_n : 0.0f);
+            const float hi = idle ? lm : (fr ? fk[p][dir] * ln_n : 3.0e38f);
+            const float nl = __builtin_amdgcn_fmed3f((lm + crhs[p][dir]) - sum16(cJ[p][dir] * gv), lo, hi);
+            delta = nl - lm;
+            clam[p][dir] = nl;
+        }
         gv += cR[p][dir] * delta;
         if constexpr (WROWS) gw += Wc[3 * p + dir] * delta;
-        resid = fmaxf(resid, fabsf(delta));
+        /* a normal row sits alone between branches, where fmaxf costs a canonicalising max
+         * and an and; med3 against +big is the same maximum in one instruction */
+        if (fr || !WROWS) resid = fmaxf(resid, fabsf(delta));
+        else resid = __builtin_amdgcn_fmed3f(fabsf(delta), resid, 3.0e38f);
     };
+    /* the wave's largest robot-point count, a scalar: the per-point branches in the sweep
+     * are s_cmp on it (a per-point bool there turns into a VALU mask round trip per row) */
+    int n1w = 0;
+#pragma unroll
+    for (int k = 0; k < CG; k++) n1w = g1k_any[k] ? k + 1 : n1w;
+    n1w = __builtin_amdgcn_readfirstlane(n1w);
     const bool g0_any = CONT && OBJ && __any(n0 > 0);
     const bool g1_any = CONT && __any(n1 > 0);
     auto contact_rows = [&](float& resid) __attribute__((always_inline)) {
@@ -1622,7 +1663,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             if (!g1_any) continue;
             sfor<0, (CONT ? CG : 0)>([&](auto kc) __attribute__((always_inline)) {
                 constexpr int k = decltype(kc)::value;
-                if (g1k_any[k]) {
+                if (WROWS ? k < n1w : g1k_any[k]) {   /* (the object tasks measured faster with the bool) */
                     if (fr) { crow(IC<P0 + k>{}, IC<1>{}, true, resid); crow(IC<P0 + k>{}, IC<2>{}, true, resid); }
                     else crow(IC<P0 + k>{}, IC<0>{}, false, resid);
                 }
