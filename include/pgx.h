@@ -173,7 +173,7 @@ typedef struct pgx_config {
     const pgx_sim_params* params;
     /* scene (Task._create_scene, push.py:31-47; pybullet.py:759-817) */
     int32_t contacts;             /* 1: robot/table/object contacts (the reference's scene) */
-    int32_t lanes_per_env;        /* step layout: 0 auto (16 up to 4096 envs, else 1), 1 = one env
+    int32_t lanes_per_env;        /* step layout: 0 auto (16 up to 8192 envs, else 1), 1 = one env
                                      per lane, 16 = one env per 16-lane DPP row; ReachAO: 1 */
     double goal_offset[3];        /* goal = offset + uniform(goal_low, goal_high): (0,0,0.02) Push/PnP */
     double goal_z_zero_prob;      /* PickAndPlace: noise z = 0 with probability 0.3 */

@@ -325,21 +325,20 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     e.ao = cfg->task == PGX_TASK_REACH_AO;
     e.terminate_on_success = cfg->terminate_on_success ? 1 : 0;
     e.collision_reward = cfg->collision_reward;
-    /* Step layout (pgx_kernels.hip): 16 lanes per env up to 4096 envs (at most one wide wave
-     * per SIMD: 4096 x 16 lanes = 1024 waves), one lane per env beyond, where the one-lane
-     * waves already fill enough SIMDs (tools/time_layouts.py: Reach at 8192 envs 1.37 ms
-     * one-lane vs 1.66 ms wide).  cfg->lanes_per_env (0 = this rule, 1, 16) chooses;
-     * PGX_LANES_PER_ENV=1|16 overrides both (A/B timing). */
+    /* Step layout (pgx_kernels.hip): 16 lanes per env up to 8192 envs (4096 x 16 lanes = 1024
+     * waves = one per SIMD; at 8192, two), one lane per env beyond, where the one-lane waves
+     * fill enough SIMDs (tools/time_layouts.py, profiles/r01/time_layouts_v11.json: Reach at
+     * 8192 envs 1.21 ms wide vs 1.32 one-lane, PickAndPlace 2.99 vs 3.52; at 16384 the
+     * one-lane layout wins, 1.33 vs 2.27 and 3.54 vs 5.49).  cfg->lanes_per_env (0 = this
+     * rule, 1, 16) chooses; PGX_LANES_PER_ENV=1|16 overrides both (A/B timing). */
     if (cfg->lanes_per_env != 0 && cfg->lanes_per_env != 1 && cfg->lanes_per_env != 16) {
         delete h;
         return fail(PGX_E_INVALID, "lanes_per_env must be 0, 1 or 16, got %d", cfg->lanes_per_env);
     }
-    /* ReachAO's per-substep capsule x obstacle checks spread over the row's lanes, so its wide
-     * layout still wins at 8192 envs (2 waves per SIMD): 1.23 vs 1.48 ms */
     /* test hook for the exactness of the speculative limit-row skip (substep_g) */
     e.pgs_mode = 0;
     if (const char* pm = std::getenv("PGX_PGS_MODE")) e.pgs_mode = std::atoi(pm);
-    const int wide_max = e.ao ? 8192 : 4096;
+    const int wide_max = 8192;
     e.lanes_per_env = cfg->lanes_per_env ? cfg->lanes_per_env : (cfg->n_envs <= wide_max ? 16 : 1);
     if (const char* lpe = std::getenv("PGX_LANES_PER_ENV")) {
         const int v = std::atoi(lpe);
