@@ -6,7 +6,7 @@ import os
 import subprocess
 import sys
 
-CASES = [("PandaReach-v3", 4096, 1), ("PandaPush-v3", 4096, 1), ("PandaReachAO-v3", 8192, 1), ("PandaReach-v3", 4096, 0),
+CASES = [("PandaReach-v3", 4096, 1), ("PandaPush-v3", 4096, 1), ("PandaReachAO-v3", 8192, 1), ("PandaReach-v3", 4096, 0), ("PandaReach-v3", 8192, 1),
          ("PandaReach-v3", 16384, 1)]
 CHILD = r'''
 import os, sys, json, torch
