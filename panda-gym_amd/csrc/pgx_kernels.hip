@@ -1527,17 +1527,34 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             rhs[r] = perr + verr;   /* scaled units */
         }
     };
-    /* exact limit-row skip (see substep()) */
-    bool far_nc = true;   /* the motor-impulse bound alone keeps every limit row idle */
+    /* exact limit-row skip (see substep()); lane c < 7 tests dof c (its M^-1 row is mcol, the
+     * same terms in the same order as the redundant loop), the row's ballot ANDs them */
+    bool ok_c = true;
+    bool far_nc = true;
+    if constexpr (WROWS) {   /* (Reach with contacts measured 0.9 % faster with the redundant loop) */
 #pragma unroll
-    for (int d = 0; d < NJ; d++) {
+        for (int d = 0; d < NJ; d++) {
+            float B = 0.0f;
+#pragma unroll
+            for (int k = 0; k < NJ; k++) B += fabsf(MINV(d, k)) * m.max_impulse[k];
+            B = B * 1.001f + 1e-6f;
+            const float penl = q[d] - kLower[d], penu = kUpper[d] - q[d];
+            far_nc = far_nc && penl > 0.0f && penu > 0.0f && (vu[d] - B) > -penl * m.inv_dt &&
+                     (vu[d] + B) < penu * m.inv_dt;
+        }
+    } else if (arm) {
         float B = 0.0f;
 #pragma unroll
-        for (int k = 0; k < NJ; k++) B += fabsf(MINV(d, k)) * m.max_impulse[k];
+        for (int k = 0; k < NJ; k++) B += fabsf(mcol[k]) * m.max_impulse[k];
         B = B * 1.001f + 1e-6f;
-        const float penl = q[d] - kLower[d], penu = kUpper[d] - q[d];
-        far_nc = far_nc && penl > 0.0f && penu > 0.0f && (vu[d] - B) > -penl * m.inv_dt && (vu[d] + B) < penu * m.inv_dt;
+        float lo_a[NJ], up_a[NJ];
+#pragma unroll
+        for (int d = 0; d < NJ; d++) { lo_a[d] = kLower[d]; up_a[d] = kUpper[d]; }
+        const float qc = pick_arm(q, 0.0f);
+        const float penl = qc - pick_arm(lo_a, 0.0f), penu = pick_arm(up_a, 0.0f) - qc;
+        ok_c = penl > 0.0f && penu > 0.0f && (vu_c - B) > -penl * m.inv_dt && (vu_c + B) < penu * m.inv_dt;
     }
+    if constexpr (!WROWS) far_nc = !row_any(!ok_c);   /* the motor-impulse bound alone keeps every limit row idle */
     const bool far = far_nc && n1 == 0;
     /* Rows in scaled units: each row equation multiplied by its den (= J M^-1 J^T), so
      * lambda' = lambda den, rhs' = rhs den and the unclamped update is
