@@ -282,7 +282,10 @@ __global__ __launch_bounds__(64) void sample_kernel(RingPtrs p, RingDims d, int6
 #pragma unroll
         for (int k = 0; k < 4; k++)
             if (4 * c + k >= d.eps) vv[k] = 0.0f;
-        *reinterpret_cast<float4*>(o.rows + w.row * d.S + 4 * c) = v;
+        /* streaming store: the batch is written once and read by the learner later */
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v nv4 = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(nv4, reinterpret_cast<f4v*>(o.rows + w.row * d.S + 4 * c));
     };
     for (int c = g; 4 * c < d.S; c += GROUP) {
         for (int s0 = lane / GROUP; s0 < 64; s0 += UNROLL * (64 / GROUP)) {
