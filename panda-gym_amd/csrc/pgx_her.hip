@@ -260,7 +260,7 @@ __global__ __launch_bounds__(64) void sample_kernel(RingPtrs p, RingDims d, int6
     /* phase 2: 16-lane groups copy 4 records per step; the loads of UNROLL steps are issued
      * before their stores, so each lane keeps several 16-B reads in flight */
     const int g = lane % GROUP;
-    constexpr int UNROLL = 4;
+    constexpr int UNROLL = 8;
     auto fetch = [&](const Draw& w, int c) {
         float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (w.rec >= 0 && 4 * c < d.S) v = *reinterpret_cast<const float4*>(p.rec + w.rec * d.R + 4 * c);
