@@ -224,9 +224,28 @@ def sharded_leg(dev, env_id: str, n: int, steps: int, warmup: int, dist, rank: i
             "policy": "device Philox random actions, in-kernel collision / success / TimeLimit auto-reset"}
 
 
+def launch_ranks(n: int) -> int:
+    """``--gpus N`` without a torch.distributed launcher: run N ranks (one per GPU) as a child
+    torch.distributed.run job on this node and return its exit code.  Nothing here has touched
+    the GPU, and the launcher is a child process, not an exec."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -298,7 +317,7 @@ def main():
                 traffic = prof.get("hbm_bytes_per_launch")
                 ins = prof.get("valu_lane_ops_per_launch")
                 if ins:
-                    valu = {"bound": "valu", "achieved": ins / (kernel_ms * 1e-3) / 1e12 * 2.0,
+                    valu = {"bound": "valu", "binding": True, "achieved": ins / (kernel_ms * 1e-3) / 1e12 * 2.0,
                             "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s-equiv (2 x VALU lane-ops)",
                             "source": os.path.relpath(PROFILE_JSON, ROOT)}
                     valu["frac"] = valu["achieved"] / VALU_PEAK_TFLOPS
@@ -311,7 +330,12 @@ def main():
             "config": {"workload": f"{args.env_id} (ee control, sparse reward), {E} envs per GPU, the "
                                    f"reference's scene: table / plane contacts of the robot (BASELINE configs[1])",
                        "envs_per_gpu": E, "global_envs": world * E, "parallelism": f"env-sharded x{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            # HBM is reported as the contract asks but does not bind this kernel: a step is ~200 B of
+            # state against a long dependent VALU chain per env, so the
+            # kernel is latency / VALU-issue bound; roofline_valu is the figure that measures it
+            "roofline": {"bound": "hbm", "binding": False,
+                         "binds": "dependent VALU issue of one wave per SIMD (see roofline_valu)",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "step_kernel<0, 0, 1, 0, 1> (ee control, no object, table contacts, 16 lanes per env)",
                          "kernel_ms": kernel_ms,

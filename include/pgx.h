@@ -158,7 +158,12 @@ typedef struct pgx_config {
     int32_t n_envs;
     int32_t max_episode_steps;    /* TimeLimit; 0 = never truncate */
     int32_t block_gripper;        /* Reach/Push: 1 */
-    int32_t pad0, pad1;
+    int32_t no_auto_reset;        /* 0: a finished env (terminated or truncated) is reset inside
+                                     pgx_step, SB3 VecEnv style (terminal_* outputs hold the
+                                     finished episode); 1: it keeps its final state until
+                                     pgx_reset, like one gymnasium env (RobotTaskEnv + TimeLimit,
+                                     core.py:352-368) */
+    int32_t pad1;
     uint64_t seed;                /* device Philox key for auto-reset draws */
     uint64_t env_id_offset;       /* global id of env 0 (multi-GPU sharding) */
     double base_pos[3];           /* robot base (-0.6,0,0) (panda_tasks.py:85) */

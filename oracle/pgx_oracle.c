@@ -1446,6 +1446,8 @@ int pgxo_vec_step(const pgx_config* c, int64_t n, double* q, double* qd, double*
         if (truncated) truncated[e] = trunc;
         if (trunc || term) {
             if (terminal_obs) memcpy(terminal_obs + od * e, o, sizeof(float) * od);
+        }
+        if ((trunc || term) && !c->no_auto_reset) {
             reset_one(c, e, NULL, NULL, qe, qde, ge, oe, elapsed + e, episode + e);
             env_obs(c, qe, qde, ge, oe, o, agv, dgv);
         }

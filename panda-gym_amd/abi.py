@@ -69,7 +69,7 @@ class PgxSimParams(C.Structure):
 class PgxConfig(C.Structure):
     _fields_ = [
         ("task", C.c_int32), ("control", C.c_int32), ("reward", C.c_int32), ("n_envs", C.c_int32),
-        ("max_episode_steps", C.c_int32), ("block_gripper", C.c_int32), ("pad0", C.c_int32),
+        ("max_episode_steps", C.c_int32), ("block_gripper", C.c_int32), ("no_auto_reset", C.c_int32),
         ("pad1", C.c_int32), ("seed", C.c_uint64), ("env_id_offset", C.c_uint64),
         ("base_pos", C.c_double * 3), ("distance_threshold", C.c_double),
         ("goal_low", C.c_double * 3), ("goal_high", C.c_double * 3),

@@ -324,6 +324,7 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     e.table_hz = (float)cfg->table_half[2];
     e.ao = cfg->task == PGX_TASK_REACH_AO;
     e.terminate_on_success = cfg->terminate_on_success ? 1 : 0;
+    e.no_auto_reset = cfg->no_auto_reset ? 1 : 0;
     e.collision_reward = cfg->collision_reward;
     /* Step layout (pgx_kernels.hip): 16 lanes per env up to 8192 envs (4096 x 16 lanes = 1024
      * waves = one per SIMD; at 8192, two), one lane per env beyond, where the one-lane waves

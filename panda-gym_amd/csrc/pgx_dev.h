@@ -57,6 +57,7 @@ struct PgxDevEnv {
     float table_hz;
     int32_t ao;                    /* ReachAO (obstacles, per-substep collision check) */
     int32_t terminate_on_success;
+    int32_t no_auto_reset;         /* pgx_config.no_auto_reset: finished envs keep their state */
     double collision_reward;
     int32_t lanes_per_env;         /* step layout: 1 (env per lane) or 16 (env per DPP row) */
     int32_t pgs_mode;              /* test hook (PGX_PGS_MODE): 0 auto, 2 never speculate on the limit

@@ -2481,6 +2481,9 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
             o.terminal_dg[3 * (size_t)i] = (float)goal[0]; o.terminal_dg[3 * (size_t)i + 1] = (float)goal[1];
             o.terminal_dg[3 * (size_t)i + 2] = (float)goal[2];
         }
+    }
+    /* SB3 VecEnv auto-reset of a finished env (off for a single gymnasium env: no_auto_reset) */
+    if ((trunc || term) && !e.no_auto_reset) {
         if constexpr (AO) {
             MRef mr = *fresh(mp);
 #pragma unroll

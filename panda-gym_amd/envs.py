@@ -166,9 +166,11 @@ class PandaVecEnv:
             raise PgxError("PandaVecEnv runs on a HIP device only (no CPU physics fallback)")
         self._model = abi.make_model(load_model(model_name), ee_link=11)
         self._params = abi.default_sim_params(n_substeps=n_substeps)
-        cfg_spec = replace(self.spec, max_episode_steps=self.spec.max_episode_steps if auto_reset else 0)
-        self._cfg = abi.make_config(cfg_spec, self.num_envs, self._model, self._params, seed=seed,
+        self._cfg = abi.make_config(self.spec, self.num_envs, self._model, self._params, seed=seed,
                                     env_id_offset=env_id_offset, contacts=contacts, lanes_per_env=lanes_per_env)
+        # auto_reset=False: a finished env keeps its terminal state until reset (one gymnasium env)
+        self._cfg.no_auto_reset = 0 if auto_reset else 1
+        self.auto_reset = bool(auto_reset)
         self.obs_dim = self.lib.pgx_obs_dim(C.byref(self._cfg))
         self.action_dim = self.lib.pgx_action_dim(C.byref(self._cfg))
         h = C.c_void_p()
@@ -204,6 +206,7 @@ class PandaVecEnv:
         self._snapshots: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
         self._next_snap = 0
         self._pending: Optional[torch.Tensor] = None
+        self._pending_seed: Optional[int] = None
         self._step_index = 0
 
     # ---------------------------------------------------------------- core
@@ -293,10 +296,15 @@ class PandaVecEnv:
 
     # ------------------------------------------------------- SB3 VecEnv API
     def reset(self, seed: Optional[int] = None, options: Optional[dict] = None):
+        """SB3 VecEnv.reset: a seed given to ``seed()`` beforehand applies to this reset only."""
+        if seed is None:
+            seed = self._pending_seed
+        self._pending_seed = None
         self.reset_tensors(seed=seed)
         return self._numpy_obs()
 
     def seed(self, seed: Optional[int] = None) -> List[Optional[int]]:
+        """SB3 VecEnv.seed: env i is seeded with seed + i at the next reset()."""
         self._pending_seed = seed
         return [None if seed is None else seed + i for i in range(self.num_envs)]
 
@@ -314,7 +322,9 @@ class PandaVecEnv:
         tr = trunc.bool().cpu().numpy()
         te = term.bool().cpu().numpy()
         sc = succ.bool().cpu().numpy()
-        infos: List[Dict[str, Any]] = [{"is_success": bool(sc[i]), "is_truncated": False} for i in range(self.num_envs)]
+        col = self.task_truncated(r)
+        infos: List[Dict[str, Any]] = [{"is_success": bool(sc[i]), "is_truncated": bool(col[i])}
+                                       for i in range(self.num_envs)]
         idx = np.nonzero(d)[0]
         if len(idx):
             tobs = self.terminal_obs.cpu().numpy()
@@ -329,6 +339,14 @@ class PandaVecEnv:
     def step(self, actions):
         self.step_async(actions)
         return self.step_wait()
+
+    def task_truncated(self, reward):
+        """Task.is_truncated of the step that returned ``reward``: False for Reach / Push /
+        PickAndPlace (reach.py:53-54); ReachAO's is_collided (reach_ao.py:1263-1264), which is
+        exactly the steps whose sparse reward carries collision_reward (-1 - 100 vs -1 / +0)."""
+        col = np.asarray(reward) < 0.5 * self._cfg.collision_reward if self.spec.task == abi.TASK_REACH_AO \
+            else np.zeros(np.shape(reward), dtype=bool)
+        return col if np.ndim(col) else bool(col)
 
     def _numpy_obs(self) -> Dict[str, np.ndarray]:
         return {k: v.cpu().numpy().copy() for k, v in self._obs_dict().items()}
@@ -412,8 +430,6 @@ class PandaEnv:
         self.spec = self._vec.spec
         self.observation_space = self._vec.observation_space
         self.action_space = self._vec.action_space
-        self._elapsed = 0
-        self._saved_elapsed: Dict[int, int] = {}
 
     def reset(self, seed: Optional[int] = None, options: Optional[dict] = None):
         r = seeded_reset(self.spec, seed)
@@ -421,7 +437,6 @@ class PandaEnv:
             self._vec.reset_tensors()
         else:
             self._vec.reset_tensors(goals=r[0][None, :], objects=None if r[1] is None else r[1][None, :])
-        self._elapsed = 0
         obs = self._vec._numpy_obs()
         obs = {k: v[0] for k, v in obs.items()}
         return obs, {"is_success": bool(self._vec.success[0].item())}
@@ -429,27 +444,25 @@ class PandaEnv:
     def step(self, action):
         a = torch.as_tensor(np.asarray(action, dtype=np.float32).reshape(1, -1), device=self._vec.device)
         obs, rew, term, trunc, succ = self._vec.step_tensors(a)
-        self._elapsed += 1
         o = {k: v[0].cpu().numpy().copy() for k, v in obs.items()}
-        truncated = self.spec.max_episode_steps > 0 and self._elapsed >= self.spec.max_episode_steps
-        info = {"is_success": bool(succ[0].item()), "is_truncated": False}
-        return o, float(rew[0].item()), bool(term[0].item()), bool(truncated), info
+        r = float(rew[0].item())
+        # the kernel's truncated flag = Task.is_truncated (ReachAO collision) or the TimeLimit
+        # (gymnasium TimeLimit.step ORs them); info carries the task's own flag (core.py:363-365)
+        info = {"is_success": bool(succ[0].item()), "is_truncated": self._vec.task_truncated(r)}
+        return o, r, bool(term[0].item()), bool(trunc[0].item()), info
 
     def compute_reward(self, achieved_goal, desired_goal, info=None):
         return self._vec.compute_reward(achieved_goal, desired_goal, info)
 
     def save_state(self) -> int:
-        sid = self._vec.save_state()
-        self._saved_elapsed[sid] = self._elapsed
-        return sid
+        """Snapshot of the env's device state, TimeLimit counter included."""
+        return self._vec.save_state()
 
     def restore_state(self, state_id: int) -> None:
         self._vec.restore_state(state_id)
-        self._elapsed = self._saved_elapsed[state_id]
 
     def remove_state(self, state_id: int) -> None:
         self._vec.remove_state(state_id)
-        self._saved_elapsed.pop(state_id, None)
 
     def close(self) -> None:
         self._vec.close()

@@ -187,12 +187,13 @@ class HerReplayBuffer:
         """Store the step just taken by ``venv.step_tensors(action)`` from ``obs``, on device.
 
         ``obs`` is a copy of the observation the action was taken from.  next_obs is
-        the terminal observation for envs that were auto-reset (SB3 off_policy_algorithm
-        _store_transition), dones = terminated | truncated, timeouts = truncated & ~terminated."""
+        the terminal observation for every env that was auto-reset, terminated or truncated
+        (SB3 off_policy_algorithm _store_transition reads infos["terminal_observation"] of
+        any done env), dones = terminated | truncated, timeouts = truncated & ~terminated."""
         tr = venv.truncated.bool()
         te = venv.terminated.bool()
         done = (tr | te).to(torch.uint8)
-        m = tr.unsqueeze(1)
+        m = (tr | te).unsqueeze(1)   # every auto-reset env (time limit, collision, terminate_on_success)
         next_o = torch.where(m, venv.terminal_obs, venv.obs)
         next_ag = torch.where(m, venv.terminal_ag, venv.achieved_goal)
         next_dg = torch.where(m, venv.terminal_dg, venv.desired_goal)

@@ -174,3 +174,33 @@ def test_full_size_properties(her_mod):
     assert torch.equal(rew, s["reward"][v])
     assert bool((s["done"] == 0).all())      # every episode end here is a time-out
     buf.close()
+
+
+def test_vec_env_feed_terminated_episodes_use_terminal_obs(her_mod):
+    """terminate_on_success (ReachAO): a successful transition is stored with the terminal
+    next_obs / next_achieved_goal, not the auto-reset episode's (SB3 _store_transition takes
+    infos["terminal_observation"] of every done env)."""
+    import panda_gym_amd as pg
+    from oracle.oracle import fk
+
+    N = 64
+    venv = pg.PandaVecEnv("PandaReachAO-v3", num_envs=N, device="cuda:0", seed=1)
+    com, _, _ = fk(venv._cfg.model.contents, np.array(pg.abi.NEUTRAL_Q[:7]))
+    far = np.tile(np.array([99.9, 99.9, -99.9]), (N, 6, 1))
+    venv.reset_tensors(goals=np.tile(com[11] + 0.01, (N, 1)), objects=far)
+    buf = her_mod.HerReplayBuffer(16 * N, env=venv, device="cuda:0", seed=2)
+    obs = {k: v.clone() for k, v in venv._obs_dict().items()}
+    a = torch.zeros((N, 7), device="cuda:0")
+    venv.step_tensors(a)
+    assert bool(venv.terminated.bool().all()) and not bool(venv.truncated.bool().any())
+    tag, tobs = venv.terminal_ag.clone(), venv.terminal_obs.clone()
+    assert not torch.equal(tag, venv.achieved_goal)              # the reset moved the goal / pose
+    buf.add_from_vec_env(venv, obs, a)
+    r = buf.sample_raw(4096)
+    e = r["env"].long()
+    assert bool((r["slot"] == 0).all())
+    assert torch.equal(r["next_achieved_goal"], tag[e])
+    assert torch.equal(r["next_obs"], tobs[e])
+    assert bool((r["done"] == 1).all())                         # terminated, not a time-out
+    venv.close()
+    buf.close()

@@ -237,6 +237,19 @@ def test_sb3_vecenv_protocol(pg):
     venv.close()
 
 
+def test_vecenv_seed_applies_to_next_reset(pg):
+    """SB3 protocol: VecEnv.seed(s) then reset() seeds env i with s + i (as reset(seed=s))."""
+    venv = pg.PandaVecEnv("PandaReach-v3", num_envs=8, device="cuda:0")
+    assert venv.seed(123) == [123 + i for i in range(8)]
+    a = venv.reset()["desired_goal"]
+    b = venv.reset(seed=123)["desired_goal"]
+    c = venv.reset()["desired_goal"]          # the pending seed was consumed: a fresh draw
+    assert np.array_equal(a, b) and not np.array_equal(a, c)
+    want = np.stack([pg.seeded_goal(venv.spec, 123 + i) for i in range(8)]).astype(np.float32)
+    assert np.array_equal(a, want)
+    venv.close()
+
+
 def test_large_batch_properties(pg):
     """Full-size batch (65536 envs): finite, bounded, deterministic, reward consistent with success."""
     n = 65536

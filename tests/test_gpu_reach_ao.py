@@ -201,3 +201,60 @@ def test_reach_ao_relabel_reward(pg):
     r = venv.compute_reward(ag, np.zeros((3, 3), np.float32), None)
     assert r.tolist() == [0.0, -1.0, 0.0]
     venv.close()
+
+
+def test_single_env_collision_and_success_keep_terminal_state(pg):
+    """One gymnasium env (PandaEnv, no auto-reset): a collision step returns truncated=True,
+    info["is_truncated"]=True (ReachAO.is_truncated, reach_ao.py:1263-1264) and the colliding
+    observation itself; a success step returns terminated=True and the state it reached."""
+    from oracle.oracle import fk
+
+    env = pg.make(ENV)
+    v = env._vec
+    com, _, _ = fk(v._cfg.model.contents, np.array(pg.abi.NEUTRAL_Q[:7]))
+    ee = com[11]
+    obst = np.array([[ee[0], ee[1] + 0.14, ee[2]]] + [[99.9, 99.9, -99.9]] * 5)
+    v.reset_tensors(goals=np.array([[0.5, 0.3, 0.3]]), objects=obst[None])
+    a = np.zeros(7, np.float32)
+    a[0] = 1.0
+    for k in range(10):
+        obs, r, term, trunc, info = env.step(a)
+        if trunc:
+            break
+        assert info["is_truncated"] is False and r == -1.0
+    assert trunc and info["is_truncated"] is True and r == -101.0 and not term
+    assert obs["observation"][20:29].min() <= 1e-3                 # the colliding state, not a reset
+    assert np.abs(obs["observation"][13:20]).max() > 0.0
+    st = v.state()
+    assert int(st["elapsed"][0].item()) == k + 1
+    # success: goal next to the EE, zero action -> terminated, the state is kept
+    far = np.tile(np.array([99.9, 99.9, -99.9]), (6, 1))[None]
+    v.reset_tensors(goals=(ee + 0.01)[None], objects=far)
+    obs, r, term, trunc, info = env.step(np.zeros(7, np.float32))
+    assert term and not trunc and info["is_success"] and info["is_truncated"] is False and r == 0.0
+    obs2, *_ = env.step(np.zeros(7, np.float32))
+    assert int(v.state()["elapsed"][0].item()) == 2              # no reset in between
+    env.close()
+
+
+def test_vec_env_infos_is_truncated_on_collision(pg):
+    n = 4
+    venv = pg.PandaVecEnv(ENV, num_envs=n, device="cuda:0", seed=1)
+    from oracle.oracle import fk
+
+    com, _, _ = fk(venv._cfg.model.contents, np.array(pg.abi.NEUTRAL_Q[:7]))
+    ee = com[11]
+    obst = np.array([[ee[0], ee[1] + 0.14, ee[2]]] + [[99.9, 99.9, -99.9]] * 5)
+    far = np.array([[99.9, 99.9, -99.9]] * 6)
+    objs = np.stack([obst, far, obst, far])
+    venv.reset_tensors(goals=np.tile([[0.5, 0.3, 0.3]], (n, 1)), objects=objs)
+    a = np.zeros((n, 7), np.float32)
+    a[:, 0] = 1.0
+    for _ in range(10):
+        _, rew, dones, infos = venv.step(a)
+        if dones.any():
+            break
+    assert dones.tolist() == [True, False, True, False]
+    assert [i["is_truncated"] for i in infos] == [True, False, True, False]
+    assert infos[0]["TimeLimit.truncated"] is True and "terminal_observation" in infos[0]
+    venv.close()

@@ -218,3 +218,35 @@ def test_reach_ao_compute_reward(oracle):
     r = compute_reward_f32(ag, dg, abi.REWARD_SPARSE_AO, thr)
     assert r.tolist() == [0.0, -1.0, 0.0] and not np.signbit(r[0])
     assert np.array_equal(her_reward(ag, dg, 2, thr), r)
+
+
+def test_no_auto_reset_keeps_the_terminal_state(oracle):
+    """pgx_config.no_auto_reset (one gymnasium env): a collision truncates, the returned obs is
+    the colliding one and the state stays there; the TimeLimit still reports truncation."""
+    from oracle import oracle as O
+    from oracle.oracle import fk
+
+    cfg = _cfg(n=1)
+    cfg.no_auto_reset = 1
+    env = O.OracleVecEnv(cfg, 1)
+    com, _, _ = fk(cfg.model.contents, np.array(abi.NEUTRAL_Q[:7]))
+    ee = com[11]
+    obst = np.array([[ee[0], ee[1] + 0.14, ee[2]]] + [[99.9, 99.9, -99.9]] * 5)
+    env.reset(inject_goal=np.array([[0.5, 0.3, 0.3]]), inject_obj=obst[None])
+    ep0 = int(env.episode[0])
+    for k in range(10):
+        b = env.step(np.array([[1.0, 0, 0, 0, 0, 0, 0]], np.float32))
+        if b["truncated"][0]:
+            break
+    assert b["truncated"][0] and b["reward"][0] == -101.0
+    assert np.array_equal(b["obs"], b["terminal_obs"])          # no reset in between
+    assert b["obs"][0, 20:29].min() <= 1e-3 and np.abs(b["obs"][0, 13:20]).max() > 0
+    assert env.elapsed[0] == k + 1 and env.episode[0] == ep0
+    # TimeLimit without auto-reset: truncated at max_episode_steps, the state is kept
+    cfg2 = _cfg(n=1)
+    cfg2.no_auto_reset, cfg2.max_episode_steps = 1, 3
+    env2 = O.OracleVecEnv(cfg2, 1)
+    far = np.array([[99.9, 99.9, -99.9]] * 6)
+    env2.reset(inject_goal=np.array([[0.5, 0.3, 0.3]]), inject_obj=far[None])
+    tr = [bool(env2.step(np.zeros((1, 7), np.float32))["truncated"][0]) for _ in range(3)]
+    assert tr == [False, False, True] and env2.elapsed[0] == 3
