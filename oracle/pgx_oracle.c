@@ -29,6 +29,11 @@ int64_t pgxo_diag_hist[128];
 void pgxo_diag_read(int64_t* out, int clear) {
     for (int i = 0; i < 128; i++) { out[i] = pgxo_diag_hist[i]; if (clear) pgxo_diag_hist[i] = 0; }
 }
+/* optional trace of every solve's sweep count, in call order (env-major within a vec step) */
+static int32_t* diag_trace;
+static int64_t diag_trace_cap, diag_trace_pos;
+void pgxo_diag_trace(int32_t* buf, int64_t cap) { diag_trace = buf; diag_trace_cap = cap; diag_trace_pos = 0; }
+int64_t pgxo_diag_trace_len(void) { return diag_trace_pos; }
 
 static void v3_cross(const double* a, const double* b, double* o) {
     double x = a[1] * b[2] - a[2] * b[1];
@@ -687,6 +692,7 @@ static void substep_impl(const pgx_model* m, const pgx_sim_params* p, const doub
     }
     if (st) st->solver_iterations = it_used;
     pgxo_diag_hist[it_used < 63 ? it_used : 63]++;
+    if (diag_trace && diag_trace_pos < diag_trace_cap) diag_trace[diag_trace_pos++] = it_used;
     pgxo_diag_hist[64 + (ncon < 15 ? ncon : 15)]++;
     {
         int lim = 0, rob = 0;

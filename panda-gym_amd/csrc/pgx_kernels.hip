@@ -1668,7 +1668,12 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     n1w = __builtin_amdgcn_readfirstlane(n1w);
     const bool g0_any = CONT && OBJ && __any(n0 > 0);
     const bool g1_any = CONT && __any(n1 > 0);
-    auto contact_rows = [&](float& resid) __attribute__((always_inline)) {
+    /* NW (Reach, WROWS): the robot points the sweep runs, a compile-time count chosen per wave
+     * outside the sweep loop (2 or 4, n1w rounded up): the rows of points n1w..NW-1 are idle
+     * (bounds [lambda', lambda'] with lambda' = 0 -> delta' = 0, bit for bit), so no per-point
+     * branch sits inside the sweep.  NW < 0: the per-point branches (rare all-rows solve). */
+    auto contact_rows = [&](auto nw_c, float& resid) __attribute__((always_inline)) {
+        constexpr int NW = decltype(nw_c)::value;
 #pragma unroll
         for (int fr = 0; fr < 2; fr++) {
             if (OBJ && g0_any) {
@@ -1677,10 +1682,10 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                     else crow(kc, IC<0>{}, false, resid);
                 });
             }
-            if (!g1_any) continue;
-            sfor<0, (CONT ? CG : 0)>([&](auto kc) __attribute__((always_inline)) {
+            if (NW < 0 && !g1_any) continue;
+            sfor<0, (CONT ? (NW >= 0 ? NW : CG) : 0)>([&](auto kc) __attribute__((always_inline)) {
                 constexpr int k = decltype(kc)::value;
-                if (WROWS ? k < n1w : g1k_any[k]) {   /* (the object tasks measured faster with the bool) */
+                if (NW >= 0 || (WROWS ? k < n1w : g1k_any[k])) {   /* (the object tasks measured faster with the bool) */
                     if (fr) { crow(IC<P0 + k>{}, IC<1>{}, true, resid); crow(IC<P0 + k>{}, IC<2>{}, true, resid); }
                     else crow(IC<P0 + k>{}, IC<0>{}, false, resid);
                 }
@@ -1706,8 +1711,9 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     auto limit_check = [&]() __attribute__((always_inline)) {
         viol = viol || (rl_c - gv > 0.0f) || (ru_c + gv > 0.0f);
     };
-    auto solve = [&](auto mode_c) __attribute__((always_inline)) {
+    auto solve = [&](auto mode_c, auto nw_c) __attribute__((always_inline)) {
         constexpr int MODE = decltype(mode_c)::value;   /* 0 far, 1 speculative, 2 all rows */
+        constexpr int NW = decltype(nw_c)::value;
         for (int it = 0; it < n_it; it += 2) {
             float resid = 0.0f;
             if constexpr (MODE == 1) limit_check();
@@ -1715,7 +1721,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 constexpr int r = PGX_N_ROWS - 1 - decltype(i)::value;
                 if constexpr (MODE == 2 || (kPgxRowCode[r] >> 4) == 0) mrow(IC<r>{}, resid);
             });
-            if (CONT && any_contact) contact_rows(resid);
+            if (CONT && (NW > 0 || (NW < 0 && any_contact))) contact_rows(nw_c, resid);
             PGX_PROF_SWEEP();
             if (resid * resid <= m.residual_thr || it + 1 >= n_it) break;
             resid = 0.0f;
@@ -1724,13 +1730,23 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 if constexpr (MODE == 2 || (kPgxRowCode[r] >> 4) == 0) mrow(IC<r>{}, resid);
             });
             if constexpr (MODE == 1) limit_check();
-            if (CONT && any_contact) contact_rows(resid);
+            if (CONT && (NW > 0 || (NW < 0 && any_contact))) contact_rows(nw_c, resid);
             PGX_PROF_SWEEP();
             if (resid * resid <= m.residual_thr) break;
         }
     };
-    if (__all(far)) {
-        solve(IC<0>{});
+    /* the speculative Reach solve with the robot point count fixed at compile time (above) */
+    auto solve_spec = [&]() __attribute__((always_inline)) {
+        if constexpr (WROWS) {
+            if (n1w == 0) solve(IC<1>{}, IC<0>{});
+            else if (n1w <= 2) solve(IC<1>{}, IC<2>{});
+            else solve(IC<1>{}, IC<4>{});
+        } else {
+            solve(IC<1>{}, IC<-1>{});
+        }
+    };
+    if (__all(far)) {   /* (Reach: far implies no robot point in the wave) */
+        solve(IC<0>{}, IC<WROWS ? 0 : -1>{});
     } else {
         PGX_PROF_COUNT(10, 1);
         init_limit_rows();
@@ -1750,7 +1766,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             float cl0[NPP];
 #pragma unroll
             for (int p = 0; p < NP; p++) cl0[p] = clam[p][0];
-            solve(IC<1>{});
+            solve_spec();
             if (__any(row_any(viol)) || e.pgs_mode == 3) {
                 PGX_PROF_COUNT(12, 1);
                 gv = gv0;
@@ -1763,11 +1779,11 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 }
 #pragma unroll
                 for (int r = 0; r < PGX_N_ROWS; r++) lam[r] = 0.0f;
-                solve(IC<2>{});
+                solve(IC<2>{}, IC<-1>{});
             }
         } else {
             PGX_PROF_COUNT(13, 1);
-            solve(IC<2>{});
+            solve(IC<2>{}, IC<-1>{});
         }
     }
 #undef MINV

@@ -26,7 +26,9 @@ print(e0.elapsed_time(e1) / 100)
 '''
 
 if __name__ == "__main__":
-    libs = sys.argv[1:3]
+    libs = sys.argv[1:]
+    if os.environ.get("AB_CASES"):   # e.g. AB_CASES="PandaReach-v3:4096:1,PandaPush-v3:4096:1"
+        CASES = [(a, int(b), int(c)) for a, b, c in (x.split(":") for x in os.environ["AB_CASES"].split(","))]
     res = {lib: {c[0] + str(c[1]) + ("" if c[2] else "-free"): [] for c in CASES} for lib in libs}
     for rep in range(3):
         for lib in libs:
