@@ -2373,8 +2373,8 @@ __device__ __forceinline__ int xcd_block() {
 /* WIDE = 0: one env per lane (64 per wave); WIDE = 1: 16 lanes per env (4 per wave,
  * substep_g), the redundant lanes compute the same values and only the lead lane stores. */
 template <int CONTROL, int OBJ, int CONT, int AO, int WIDE>
-__global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict__ mdev, PgxDevEnv e, PgxDevState s,
-                                                  const float* __restrict__ action, PgxDevOut o) {
+__device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, const PgxDevEnv& e,
+                                          const PgxDevState& s, const float* __restrict__ action, const PgxDevOut& o) {
     using LT = ContactLdsT<WIDE ? EPW : 64>;
     const int ln = WIDE ? (int)threadIdx.x / GW : (int)threadIdx.x;   /* env slot in the wave (LDS index) */
     const int c = WIDE ? (int)threadIdx.x % GW : 0;                   /* lane within the env's row */
@@ -2553,6 +2553,23 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
 #endif
 }
 
+/* The step kernel at one wave per SIMD (all of the register file: no spills; the batch
+ * fills the chip only to one wave per SIMD, 4096 envs in the wide layout) and at two
+ * (register budget 256, some spilled to scratch): beyond 1024 waves a second wave per
+ * SIMD hides the first one's dependent latency -- ReachAO at 8192 envs 1.00 -> 0.78 ms,
+ * Reach 1.11 -> 1.07 ms (joint-control Reach, fewer contacts, 0.57 -> 0.75: not used
+ * there), while at 4096 envs the spills would cost 0.63 -> 0.89 ms. */
+template <int CONTROL, int OBJ, int CONT, int AO, int WIDE>
+__global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict__ mdev, PgxDevEnv e, PgxDevState s,
+                                                  const float* __restrict__ action, PgxDevOut o) {
+    step_body<CONTROL, OBJ, CONT, AO, WIDE>(mdev, e, s, action, o);
+}
+template <int CONTROL, int OBJ, int CONT, int AO, int WIDE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void step_kernel_o2(
+    const PgxDevModel* __restrict__ mdev, PgxDevEnv e, PgxDevState s, const float* __restrict__ action, PgxDevOut o) {
+    step_body<CONTROL, OBJ, CONT, AO, WIDE>(mdev, e, s, action, o);
+}
+
 template <int OBJ, int AO>
 __global__ __launch_bounds__(64) void reset_kernel(const PgxDevModel* __restrict__ mdev, PgxDevEnv e, PgxDevState s,
                                                    const uint8_t* mask, const double* inject_goal,
@@ -2650,6 +2667,11 @@ __global__ __launch_bounds__(256) void compute_reward_kernel(const float* __rest
 #define PGX_TU 0
 #endif
 #define PGX_STEP(C, O, K, A, W) hipLaunchKernelGGL((step_kernel<C, O, K, A, W>), grid, block, 0, st, m, e, s, action, o)
+#define PGX_STEP2(C, O, K, A, W)                                                                            \
+    do {                                                                                                    \
+        if (two) hipLaunchKernelGGL((step_kernel_o2<C, O, K, A, W>), grid, block, 0, st, m, e, s, action, o); \
+        else hipLaunchKernelGGL((step_kernel<C, O, K, A, W>), grid, block, 0, st, m, e, s, action, o);        \
+    } while (0)
 #if PGX_TU != 2
 int pgx_launch_step_arm(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState& s, const float* action,
                         const PgxDevOut& o, void* stream) {
@@ -2657,15 +2679,16 @@ int pgx_launch_step_arm(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevSt
     const int wide = e.lanes_per_env == GW;
     const int per_block = wide ? EPW : 64;
     dim3 block(64), grid((e.n_envs + per_block - 1) / per_block);
+    const bool two = wide && grid.x > 1024;   /* more waves than SIMDs: two per SIMD */
     switch ((e.control * 4 + (e.contacts ? 1 : 0)) * 2 + wide) {
         case 0: PGX_STEP(0, 0, 0, 0, 0); break;
         case 1: PGX_STEP(0, 0, 0, 0, 1); break;
         case 2: PGX_STEP(0, 0, 1, 0, 0); break;
-        case 3: PGX_STEP(0, 0, 1, 0, 1); break;
+        case 3: PGX_STEP2(0, 0, 1, 0, 1); break;
         case 8: PGX_STEP(1, 0, 0, 0, 0); break;
         case 9: PGX_STEP(1, 0, 0, 0, 1); break;
         case 10: PGX_STEP(1, 0, 1, 0, 0); break;
-        case 11: PGX_STEP(1, 0, 1, 0, 1); break;
+        case 11: PGX_STEP(1, 0, 1, 0, 1); break;   /* (joint-control Reach at 8192: 0.57 -> 0.75 ms with two) */
         default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
@@ -2679,6 +2702,7 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
     const int wide = e.lanes_per_env == GW;
     const int per_block = wide ? EPW : 64;
     dim3 block(64), grid((e.n_envs + per_block - 1) / per_block);
+    const bool two = wide && grid.x > 1024;   /* more waves than SIMDs: two per SIMD */
     const int variant = e.ao ? 13 : e.control * 4 + (e.has_object ? 2 : 0) + (e.contacts ? 1 : 0);
     switch (variant * 2 + wide) {
         case 6: PGX_STEP(0, 1, 1, 0, 0); break;
@@ -2686,7 +2710,7 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
         case 14: PGX_STEP(1, 1, 1, 0, 0); break;
         case 15: PGX_STEP(1, 1, 1, 0, 1); break;
         case 26: PGX_STEP(1, 0, 1, 1, 0); break;
-        case 27: PGX_STEP(1, 0, 1, 1, 1); break;
+        case 27: PGX_STEP2(1, 0, 1, 1, 1); break;
         default: return (int)hipErrorInvalidValue;   /* object without contacts: rejected at create */
     }
     return (int)hipGetLastError();
@@ -2721,3 +2745,4 @@ int pgx_launch_compute_reward(const float* ag, const float* dg, int64_t n, int32
 }
 #endif  /* PGX_TU != 1 */
 #undef PGX_STEP
+#undef PGX_STEP2

@@ -268,3 +268,26 @@ def test_large_batch_properties(pg):
     assert np.array_equal(outs[0][0], outs[1][0])  # bitwise deterministic
     assert np.array_equal(r == 0.0, s.astype(bool) | (r == 0.0))
     assert set(np.unique(r)).issubset({-1.0, 0.0})
+
+
+@pytest.mark.parametrize("env_id", ["PandaReach-v3", "PandaReachAO-v3"])
+def test_two_wave_variant_matches_one_wave_shards(pg, env_id):
+    """8192 envs in the wide layout launch the two-waves-per-SIMD build of the step kernel;
+    two 4096-env shards (global ids 0.. and 4096..) launch the one-wave build.  Same global
+    ids, same Philox actions and resets: the results agree bit for bit."""
+    n = 8192
+    big = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=5, lanes_per_env=16)
+    parts = [pg.PandaVecEnv(env_id, num_envs=n // 2, device="cuda:0", seed=5, lanes_per_env=16,
+                            env_id_offset=k * (n // 2)) for k in range(2)]
+    for v in [big] + parts:
+        v.reset_tensors()
+    for t in range(12):
+        big.step_tensors(big.sample_actions(t))
+        for v in parts:
+            v.step_tensors(v.sample_actions(t))
+        got = torch.cat([v.obs for v in parts])
+        assert torch.equal(got.view(torch.int32), big.obs.view(torch.int32)), t
+        assert torch.equal(torch.cat([v.reward for v in parts]), big.reward), t
+        assert torch.equal(torch.cat([v.truncated for v in parts]), big.truncated), t
+    for v in [big] + parts:
+        v.close()
