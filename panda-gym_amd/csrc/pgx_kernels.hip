@@ -946,6 +946,269 @@ __device__ __forceinline__ void substep_dyn(MRef m, const PgxDevEnv& e, const fl
     }
 }
 
+/* ------------------------------------------- wide layout: lane-parallel dynamics */
+/* In the wide layout lane c < 7 of an env's row owns arm link c for the Newton-Euler bias
+ * and the mass matrix: the recursions over the chain become prefix / suffix sums over the
+ * row (three DPP adds each, row_shr / row_shl 1, 2, 4), every per-link term is evaluated
+ * once instead of on all 16 lanes, and the results the redundant Cholesky needs (the
+ * bias b, the lower triangle of M) are broadcast back.  Same equations as substep_dyn,
+ * rearranged (below); only fp32 rounding differs. */
+struct LaneK {   /* link c's constants (lanes >= 7: zero) */
+    float mass, com[3];
+    float I[6], Iown[6];   /* inertia about the COM in the link frame (xx,yy,zz,xy,xz,yz); the
+                              one its angular damping uses (link-7 group: the bodies' own) */
+};
+__device__ __forceinline__ void lane_consts(LaneK& k) {
+    k.mass = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 3; t++) k.com[t] = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 6; t++) { k.I[t] = 0.0f; k.Iown[t] = 0.0f; }
+    sfor<0, NJ>([&](auto jc) __attribute__((always_inline)) {
+        constexpr int j = decltype(jc)::value;
+        k.mass = lane_sel<j>(kMass[j], k.mass);
+#pragma unroll
+        for (int t = 0; t < 3; t++) k.com[t] = lane_sel<j>(kCom[j][t], k.com[t]);
+#pragma unroll
+        for (int t = 0; t < 6; t++) {
+            const float a = j < NJ - 1 ? (t < 3 ? kInertia[j < NJ - 1 ? j : 0][t < 3 ? t : 0] : 0.0f) : kI6c[t];
+            const float b = j < NJ - 1 ? a : kI6own[t];
+            if (a != 0.0f) k.I[t] = lane_sel<j>(a, k.I[t]);
+            if (b != 0.0f) k.Iown[t] = lane_sel<j>(b, k.Iown[t]);
+        }
+    });
+}
+/* inclusive prefix (suffix) sum over lanes 0..c (c..15) of each 16-lane row */
+__device__ __forceinline__ float row_pre(float x) {
+    x += dpp<0x111>(x);   /* row_shr:1 (lane 0 reads 0) */
+    x += dpp<0x112>(x);   /* row_shr:2 */
+    x += dpp<0x114>(x);   /* row_shr:4 */
+    return x;
+}
+__device__ __forceinline__ float row_suf(float x) {
+    x += dpp<0x101>(x);   /* row_shl:1 */
+    x += dpp<0x102>(x);   /* row_shl:2 */
+    x += dpp<0x104>(x);   /* row_shl:4 */
+    return x;
+}
+__device__ __forceinline__ V3 row_pre(V3 a) { return v3(row_pre(a.x), row_pre(a.y), row_pre(a.z)); }
+__device__ __forceinline__ V3 row_suf(V3 a) { return v3(row_suf(a.x), row_suf(a.y), row_suf(a.z)); }
+/* x on the link lanes 0..6 of every row, 0 elsewhere (one v_cndmask) */
+__device__ __forceinline__ float link_only(float x) {
+    float r;
+    asm("v_cndmask_b32 %0, 0, %1, %2" : "=v"(r) : "v"(x), "s"(0x007F007F007F007Full));
+    return r;
+}
+__device__ __forceinline__ V3 link_only(V3 a) { return v3(link_only(a.x), link_only(a.y), link_only(a.z)); }
+/* R S R^T for a symmetric S held in registers */
+__device__ __forceinline__ S3 rot_sym_r(const M3& R, const float* s) {
+    const float Sm[9] = {s[0], s[3], s[4], s[3], s[1], s[5], s[4], s[5], s[2]};
+    float T[9];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+            T[i * 3 + j] = R.m[i * 3] * Sm[j] + R.m[i * 3 + 1] * Sm[3 + j] + R.m[i * 3 + 2] * Sm[6 + j];
+    auto e = [&](int i, int j) { return T[i * 3] * R.m[j * 3] + T[i * 3 + 1] * R.m[j * 3 + 1] + T[i * 3 + 2] * R.m[j * 3 + 2]; };
+    S3 o;
+    o.xx = e(0, 0); o.yy = e(1, 1); o.zz = e(2, 2); o.xy = e(0, 1); o.xz = e(0, 2); o.yz = e(1, 2);
+    return o;
+}
+__device__ __forceinline__ V3 mul_sym(const float* s, V3 v) {
+    return v3(s[0] * v.x + s[3] * v.y + s[4] * v.z, s[3] * v.x + s[1] * v.y + s[5] * v.z,
+              s[4] * v.x + s[5] * v.y + s[2] * v.z);
+}
+
+/* substep_dyn for the wide layout (16 lanes per env, lane c of the row).  Positions are
+ * taken relative to the robot base.  With t_k = qd_k z_k (joint k's contribution to the
+ * angular velocity) and prefix sums over the links k <= c:
+ *   w_c = sum t_k,  S_c = sum t_k x o_k,  COM velocity v_c = w_c x c_c - S_c,
+ *   pivot velocity u_c = w_c x o_c - S_c,  alpha_c = sum w_{k-1} x t_k   (qdd = 0),
+ *   dS_c = sum (w_{k-1} x t_k) x o_k + t_k x u_k,  a_c = alpha_c x c_c + w_c x v_c - dS_c,
+ * i.e. d/dt of v_c; the link wrenches at the COM are those of substep_dyn; the bias is
+ *   b_c = -z_c . (sum_{k>=c} (T_k + c_k x F_k) - o_c x sum_{k>=c} F_k)   (suffix sums).
+ * Mass matrix: the subtree of joint c has mass M, first moment H = sum m c and inertia
+ * about the base I (suffix sums); spun about z_c through o_c its momentum is
+ * f = z_c x (H - M o_c) and its angular momentum about o_c is n = I_o z_c with
+ *   I_o z = I z - 2 (H.o) z + H (o.z) + o (H.z) + M (|o|^2 z - o (o.z)),
+ * and M[c][i] = z_i . (n + (o_c - o_i) x f) for i <= c (CRBA), broadcast to every lane. */
+template <int OBJ, int CONT>
+__device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const float* q, const float* qd,
+                                              const ObjState& ob, ContactLdsG* Lp, int es, Dyn& D, int c,
+                                              const LaneK& K) {
+    M3 Rc;
+    if (OBJ) Rc = quat_mat(ob);
+    if (CONT) { Lp->cnt[0][es] = 0; Lp->cnt[1][es] = 0; }
+    if (OBJ) { /* object vertices vs the box top under them */
+        const float h = e.obj_half;
+#pragma unroll
+        for (int vtx = 0; vtx < 8; vtx++) {
+            const V3 r = mul(Rc, v3((vtx & 1) ? h : -h, (vtx & 2) ? h : -h, (vtx & 4) ? h : -h));
+            const V3 P = ob.p + r;
+            const float d = P.z - ground_z(e, P.x, P.y);
+            if (d < m.contact_dist) g0_insert(*Lp, es, d, (float)vtx, r);
+        }
+    }
+    /* FK (redundant: constant-folded per link), capsule end points, and this lane's link */
+    V3 (&z)[NJ] = D.z;
+    V3 (&o)[NJ] = D.o;
+    M3 Rl = {{0, 0, 0, 0, 0, 0, 0, 0, 0}};
+    V3 ol = v3(0, 0, 0);
+    {
+        M3 PR = {{1, 0, 0, 0, 1, 0, 0, 0, 1}};
+        V3 PO = v3(m.base[0], m.base[1], m.base[2]);
+        float sjs[NJ], cjs[NJ];
+        joint_sincos_all<true>(q, sjs, cjs);
+        sfor<0, NJ>([&](auto jc) __attribute__((always_inline)) {
+            constexpr int j = decltype(jc)::value;
+            M3 R = mulm(PR, kJr[j]);
+            V3 oj = PO + mulc(PR, kJp[j]);
+            const float sn = sjs[j], cs = cjs[j];
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                float a = R.m[r * 3], b = R.m[r * 3 + 1];
+                R.m[r * 3] = cs * a + sn * b;
+                R.m[r * 3 + 1] = -sn * a + cs * b;
+            }
+            z[j] = col(R, 2);
+            o[j] = oj;
+            if constexpr (CONT) link_capsules(j, *Lp, es, R, oj);
+#pragma unroll
+            for (int t = 0; t < 9; t++) Rl.m[t] = lane_sel<j>(R.m[t], Rl.m[t]);
+            ol = v3(lane_sel<j>(oj.x, ol.x), lane_sel<j>(oj.y, ol.y), lane_sel<j>(oj.z, ol.z));
+            PR = R;
+            PO = oj;
+        });
+    }
+    if (CONT) {
+        if constexpr (!OBJ) {
+            robot_table_contacts_g(e, m.contact_dist, *Lp, es, c);
+        } else {
+            robot_contacts<OBJ>(e, m.contact_dist, *Lp, es, ob, Rc);
+            sort_groups(*Lp, es);
+        }
+    }
+    PGX_PROF_MARK(1);
+    const V3 g = v3(m.gravity[0], m.gravity[1], m.gravity[2]);
+    const V3 base = v3(m.base[0], m.base[1], m.base[2]);
+    const V3 zl = col(Rl, 2);
+    const V3 ob_l = ol - base;                                   /* pivot, base-relative */
+    const V3 cw = ol + mul(Rl, v3(K.com[0], K.com[1], K.com[2]));   /* COM, world */
+    const V3 cb = cw - base;
+
+    /* ---- Newton-Euler bias by prefix / suffix sums over the link lanes */
+    const float qdl = pick_arm(qd, 0.0f);
+    const V3 t1 = qdl * zl;
+    const V3 w = row_pre(t1);
+    const V3 alt = cross(w - t1, t1);
+    const V3 al = row_pre(alt);
+    const V3 S = row_pre(cross(t1, ob_l));
+    const V3 u = cross(w, ob_l) - S;                             /* pivot velocity */
+    const V3 dS = row_pre(cross(alt, ob_l) + cross(t1, u));
+    const V3 v = cross(w, cb) - S;                               /* COM velocity */
+    const V3 a = cross(al, cb) + cross(w, v) - dS;               /* COM acceleration */
+    const S3 Iw = rot_sym_r(Rl, K.I);
+    const V3 Iww = mul(Iw, w);
+    const float wn = norm(w);
+    const V3 Iow = mul(Rl, mul_sym(K.Iown, mul_t(Rl, w)));
+    V3 F = K.mass * (a - g);
+    V3 T = mul(Iw, al) + cross(w, Iww) + (m.ang_damp + m.ang_damp * wn) * Iow;
+    {
+        /* damping m v (k + k|v|): per link; the link-7 group per body (lane 6's values) */
+        const V3 Fd = (K.mass * (m.lin_damp + m.lin_damp * norm(v))) * v;
+        V3 Fg = v3(0, 0, 0), Tg = v3(0, 0, 0);
+#pragma unroll
+        for (int b = 0; b < PGX_NDAMP; b++) {
+            const V3 rb = mulc(Rl, kDpos[b]);
+            const V3 vb = u + cross(w, rb);
+            const V3 fd = (kDmass[b] * (m.lin_damp + m.lin_damp * norm(vb))) * vb;
+            Fg = Fg + fd;
+            Tg = Tg + cross(ol + rb - cw, fd);
+        }
+        F = F + v3(lane_sel<NJ - 1>(Fg.x, Fd.x), lane_sel<NJ - 1>(Fg.y, Fd.y), lane_sel<NJ - 1>(Fg.z, Fd.z));
+        T = T + v3(lane_sel<NJ - 1>(Tg.x, 0.0f), lane_sel<NJ - 1>(Tg.y, 0.0f), lane_sel<NJ - 1>(Tg.z, 0.0f));
+    }
+    const V3 Fs = row_suf(link_only(F));
+    const V3 Ms = row_suf(link_only(T + cross(cb, F)));
+    const float nbl = -dot(zl, Ms - cross(ob_l, Fs));
+    float nb[NJ];
+    sfor<0, NJ>([&](auto jc) __attribute__((always_inline)) {
+        constexpr int j = decltype(jc)::value;
+        nb[j] = bcast16<j>(nbl);
+    });
+    PGX_PROF_MARK(14);
+
+    /* ---- mass matrix (CRBA) by suffix sums of mass, first moment and base-referred inertia */
+    float Mt[NJ][NJ];
+    {
+        const float ml = link_only(K.mass);
+        const S3 st = steiner(ml, cb);
+        const float Mc = row_suf(ml);
+        const V3 H = row_suf(ml * cb);
+        const float Ixx = row_suf(link_only(Iw.xx + st.xx)), Iyy = row_suf(link_only(Iw.yy + st.yy));
+        const float Izz = row_suf(link_only(Iw.zz + st.zz)), Ixy = row_suf(link_only(Iw.xy + st.xy));
+        const float Ixz = row_suf(link_only(Iw.xz + st.xz)), Iyz = row_suf(link_only(Iw.yz + st.yz));
+        const S3 Is = {Ixx, Iyy, Izz, Ixy, Ixz, Iyz};
+        const V3 f = cross(zl, H - Mc * ob_l);
+        const float Ho = dot(H, ob_l), oz = dot(ob_l, zl), Hz = dot(H, zl), oo = dot(ob_l, ob_l);
+        const V3 n = mul(Is, zl) + (Mc * oo - 2.0f * Ho) * zl + oz * H + Hz * ob_l - (Mc * oz) * ob_l;
+        float colv[NJ];
+#pragma unroll
+        for (int i = 0; i < NJ; i++) colv[i] = dot(z[i], n + cross(ol - o[i], f));   /* M[c][i], i <= c */
+        sfor<0, NJ>([&](auto jc) __attribute__((always_inline)) {
+            constexpr int j = decltype(jc)::value;
+            sfor<0, j + 1>([&](auto ic) __attribute__((always_inline)) {
+                constexpr int i = decltype(ic)::value;
+                Mt[j][i] = bcast16<j>(colv[i]);
+            });
+        });
+    }
+    chol7(Mt);
+    float (&vu)[NJ] = D.vu;
+    {
+        float qdd[NJ];
+        chol7_solve(Mt, nb, qdd);
+#pragma unroll
+        for (int j = 0; j < NJ; j++) vu[j] = fminf(fmaxf(qd[j] + m.dt * qdd[j], -m.max_vel), m.max_vel);
+    }
+
+    PGX_PROF_MARK(15);
+    /* M^-1 = L^-T L^-1 (symmetric, lower triangle kept) */
+    float (&Mi)[NJ][NJ] = D.Mi;
+    {
+        float X[NJ][NJ];
+#pragma unroll
+        for (int i = 0; i < NJ; i++) {
+            float inv = Mt[i][i];
+#pragma unroll
+            for (int jj = 0; jj <= i; jj++) {
+                float sacc = (jj == i) ? 1.0f : 0.0f;
+#pragma unroll
+                for (int kk = jj; kk < i; kk++) sacc -= Mt[i][kk] * X[kk][jj];
+                X[i][jj] = sacc * inv;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NJ; i++)
+#pragma unroll
+            for (int jj = 0; jj <= i; jj++) {
+                float sacc = 0.0f;
+#pragma unroll
+                for (int l = i; l < NJ; l++) sacc += X[l][i] * X[l][jj];
+                Mi[i][jj] = sacc;
+            }
+    }
+    V3& vcu = D.vcu;
+    V3& wcu = D.wcu;
+    vcu = v3(0, 0, 0);
+    wcu = v3(0, 0, 0);
+    if (OBJ) {
+        const float vn = norm(ob.v), wn2 = norm(ob.w);
+        vcu = ob.v + m.dt * (g - (m.lin_damp + m.lin_damp * vn) * ob.v - cross(ob.w, ob.v));
+        wcu = ob.w - (m.dt * (m.ang_damp + m.ang_damp * wn2)) * ob.w;
+    }
+}
+
 /* floating-base object: v, w after the constraint pass; p += dt v, orientation by the
  * exponential map (btMultiBody::stepPositionsMultiDof) */
 __device__ __forceinline__ void object_integrate(MRef m, ObjState& ob, V3 v, V3 w) {
@@ -1327,10 +1590,10 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
  * shared through substep_dyn), rows solved in the same order with the same exit rule. */
 template <int OBJ, int CONT>
 __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q, float* qd, const float* tq,
-                                          ObjState& ob, ContactLdsG* Lp, int es, int c) {
+                                          ObjState& ob, ContactLdsG* Lp, int es, int c, const LaneK& K) {
     MRef m = *fresh(mp);
     Dyn D;
-    substep_dyn<OBJ, CONT, ContactLdsG, true>(m, e, q, qd, ob, Lp, es, D, c);
+    substep_dyn_g<OBJ, CONT>(m, e, q, qd, ob, Lp, es, D, c, K);
     const V3 (&z)[NJ] = D.z;
     const V3 (&o)[NJ] = D.o;
     const float (&Mi)[NJ][NJ] = D.Mi;
@@ -2444,10 +2707,12 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     }
 
     PGX_PROF_MARK(0);
+    LaneK lk;
+    if constexpr (WIDE) lane_consts(lk);
     const int n_substeps = m.n_substeps;
     bool collided = false;
     for (int st = 0; st < n_substeps; st++) {
-        if constexpr (WIDE) substep_g<OBJ, CONT>(mp, e, q, qd, tq, ob, L, ln, c);
+        if constexpr (WIDE) substep_g<OBJ, CONT>(mp, e, q, qd, tq, ob, L, ln, c, lk);
         else substep<OBJ, CONT>(mp, e, q, qd, tq, ob, L, ln);
         if constexpr (AO) {   /* ReachAO step_check_collision: check after every substep, stop on contact */
             ao_caps(*fresh(mp), q, *L, ln);
