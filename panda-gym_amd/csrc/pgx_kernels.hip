@@ -2645,7 +2645,11 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     const int i = xcd_block() * (WIDE ? EPW : 64) + ln;
     const int N = e.n_envs;
     if (i >= N) return;
-    const int ii = i;
+    /* the prologue loads index by a laundered copy of i: the compiler cannot reuse their
+     * 64-bit addresses for the epilogue stores and keep ~17 address pairs live across the
+     * whole step (recomputing them at the end is a few adds) */
+    int ii = i;
+    asm volatile("" : "+v"(ii));
     LT* L = nullptr;
     if constexpr (CONT) {
         __shared__ LT lds_buf;   /* one-lane: ~126 KB, one wave per CU; wide: ~9 KB */
