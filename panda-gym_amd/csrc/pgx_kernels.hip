@@ -751,7 +751,9 @@ __device__ __forceinline__ void robot_table_contacts_g(const PgxDevEnv& e, float
  * triangle); the object's unconstrained velocities (OBJ). */
 struct Dyn {
     V3 z[NJ], o[NJ];
-    float Mi[NJ][NJ];
+    float Mi[NJ][NJ];     /* one-lane layout: M^-1, lower triangle */
+    float mcol[NJ];       /* wide layout: lane c's column of M^-1 (0 on lanes >= 7) */
+    float mdiag[NJ];      /* wide layout: diag(M^-1) on every lane */
     float vu[NJ];
     V3 vcu, wcu;
 };
@@ -1173,30 +1175,30 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
     }
 
     PGX_PROF_MARK(15);
-    /* M^-1 = L^-T L^-1 (symmetric, lower triangle kept) */
-    float (&Mi)[NJ][NJ] = D.Mi;
+    /* M^-1 lane-parallel: lane c solves L L^T x = e_c (its column; e = 0 on lanes >= 7), the
+     * diagonal is broadcast from the lanes that own it */
     {
-        float X[NJ][NJ];
+        float y[NJ], x[NJ];
+        sfor<0, NJ>([&](auto ic) __attribute__((always_inline)) {
+            constexpr int i = decltype(ic)::value;
+            float sacc = lane_sel<i>(1.0f, 0.0f);
 #pragma unroll
-        for (int i = 0; i < NJ; i++) {
-            float inv = Mt[i][i];
+            for (int k = 0; k < i; k++) sacc -= Mt[i][k] * y[k];
+            y[i] = sacc * Mt[i][i];   /* chol7 stores the inverted diagonal */
+        });
 #pragma unroll
-            for (int jj = 0; jj <= i; jj++) {
-                float sacc = (jj == i) ? 1.0f : 0.0f;
+        for (int i = NJ - 1; i >= 0; i--) {
+            float sacc = y[i];
 #pragma unroll
-                for (int kk = jj; kk < i; kk++) sacc -= Mt[i][kk] * X[kk][jj];
-                X[i][jj] = sacc * inv;
-            }
+            for (int k = i + 1; k < NJ; k++) sacc -= Mt[k][i] * x[k];
+            x[i] = sacc * Mt[i][i];
         }
 #pragma unroll
-        for (int i = 0; i < NJ; i++)
-#pragma unroll
-            for (int jj = 0; jj <= i; jj++) {
-                float sacc = 0.0f;
-#pragma unroll
-                for (int l = i; l < NJ; l++) sacc += X[l][i] * X[l][jj];
-                Mi[i][jj] = sacc;
-            }
+        for (int k = 0; k < NJ; k++) D.mcol[k] = x[k];
+        sfor<0, NJ>([&](auto dc) __attribute__((always_inline)) {
+            constexpr int d = decltype(dc)::value;
+            D.mdiag[d] = bcast16<d>(x[d]);
+        });
     }
     V3& vcu = D.vcu;
     V3& wcu = D.wcu;
@@ -1596,22 +1598,15 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     substep_dyn_g<OBJ, CONT>(m, e, q, qd, ob, Lp, es, D, c, K);
     const V3 (&z)[NJ] = D.z;
     const V3 (&o)[NJ] = D.o;
-    const float (&Mi)[NJ][NJ] = D.Mi;
     const float (&vu)[NJ] = D.vu;
     const V3 vcu = D.vcu, wcu = D.wcu;
-#define MINV(a, b) ((a) >= (b) ? Mi[a][b] : Mi[b][a])
     PGX_PROF_MARK(2);
     const bool arm = c < NJ;
     const float inv_m = e.obj_inv_mass, inv_i = e.obj_inv_inertia;
     /* this lane's coordinate: M^-1 row (arm), object inverse mass / inertia, velocity */
     float mcol[NJ];
 #pragma unroll
-    for (int d = 0; d < NJ; d++) {
-        float col[NJ];
-#pragma unroll
-        for (int k = 0; k < NJ; k++) col[k] = MINV(k, d);
-        mcol[d] = pick_arm(col, 0.0f);
-    }
+    for (int d = 0; d < NJ; d++) mcol[d] = D.mcol[d];
     const float kobj = OBJ ? ((c >= 7 && c < 10) ? inv_m : ((c >= 10 && c < 13) ? inv_i : 0.0f)) : 0.0f;
     const float vu_c = pick_gen(vu, vcu, wcu);
     float gv = 0.0f;   /* this lane's velocity delta */
@@ -1762,7 +1757,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     float den[NJ], jinv[NJ];
 #pragma unroll
     for (int d = 0; d < NJ; d++) {
-        den[d] = Mi[d][d];
+        den[d] = D.mdiag[d];
         jinv[d] = den[d] > 2.220446e-16f ? fast_rcp(den[d]) : 0.0f;
     }
     float rhs[PGX_N_ROWS], lam[PGX_N_ROWS];
@@ -1794,18 +1789,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
      * same terms in the same order as the redundant loop), the row's ballot ANDs them */
     bool ok_c = true;
     bool far_nc = true;
-    if constexpr (WROWS) {   /* (Reach with contacts measured 0.9 % faster with the redundant loop) */
-#pragma unroll
-        for (int d = 0; d < NJ; d++) {
-            float B = 0.0f;
-#pragma unroll
-            for (int k = 0; k < NJ; k++) B += fabsf(MINV(d, k)) * m.max_impulse[k];
-            B = B * 1.001f + 1e-6f;
-            const float penl = q[d] - kLower[d], penu = kUpper[d] - q[d];
-            far_nc = far_nc && penl > 0.0f && penu > 0.0f && (vu[d] - B) > -penl * m.inv_dt &&
-                     (vu[d] + B) < penu * m.inv_dt;
-        }
-    } else if (arm) {
+    if (arm) {
         float B = 0.0f;
 #pragma unroll
         for (int k = 0; k < NJ; k++) B += fabsf(mcol[k]) * m.max_impulse[k];
@@ -1817,7 +1801,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         const float penl = qc - pick_arm(lo_a, 0.0f), penu = pick_arm(up_a, 0.0f) - qc;
         ok_c = penl > 0.0f && penu > 0.0f && (vu_c - B) > -penl * m.inv_dt && (vu_c + B) < penu * m.inv_dt;
     }
-    if constexpr (!WROWS) far_nc = !row_any(!ok_c);   /* the motor-impulse bound alone keeps every limit row idle */
+    far_nc = !row_any(!ok_c);   /* the motor-impulse bound alone keeps every limit row idle */
     const bool far = far_nc && n1 == 0;
     /* Rows in scaled units: each row equation multiplied by its den (= J M^-1 J^T), so
      * lambda' = lambda den, rhs' = rhs den and the unclamped update is
@@ -2049,7 +2033,6 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             solve(IC<2>{}, IC<-1>{});
         }
     }
-#undef MINV
     PGX_PROF_SWEEPS_DONE();
     PGX_PROF_MARK(4);
     PGX_PROF_COUNT(11, any_contact ? 1 : 0);
