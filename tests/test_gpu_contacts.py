@@ -233,17 +233,18 @@ def test_layouts_agree_per_step(pg, env_id):
     b.close()
 
 
-def test_speculative_limit_skip_is_exact(pg, monkeypatch):
+@pytest.mark.parametrize("env_id", ["PandaReach-v3", "PandaPush-v3"])
+def test_speculative_limit_skip_is_exact(pg, monkeypatch, env_id):
     """substep_g solves contact substeps without the joint-limit rows when the motor-impulse
     bound alone keeps them idle, checks at every limit-block position that they would have
     computed a zero impulse, and redoes the solve with them otherwise.  The claim is bit-exact
     equality with the all-rows solve: compared here against PGX_PGS_MODE=2 (never speculate)
-    and PGX_PGS_MODE=3 (always redo), on table-contact Reach steps from the same states."""
+    and PGX_PGS_MODE=3 (always redo), on table-contact Reach and Push steps from the same states."""
     n = 256
     runs = {}
     for mode in ("0", "2", "3"):
         monkeypatch.setenv("PGX_PGS_MODE", mode)
-        v = pg.PandaVecEnv("PandaReach-v3", num_envs=n, device="cuda:0", seed=9, lanes_per_env=16)
+        v = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=9, lanes_per_env=16)
         v.reset_tensors(seed=9)
         outs = []
         for t in range(25):
