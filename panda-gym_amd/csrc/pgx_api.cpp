@@ -245,6 +245,16 @@ static int build_dev_model(const pgx_config* cfg, PgxDevModel* dm) {
     dm->ang_damp = (float)p->ang_damping;
     dm->max_vel = (float)p->max_coord_vel;
     dm->residual_thr = (float)p->residual_threshold;
+    {   /* fl(t * t) is monotone in t, so {t >= 0 : fl(t * t) <= thr} = [0, residual_abs] */
+        volatile float thr = dm->residual_thr, t = std::sqrt(thr);
+        while (t > 0.0f && (float)(t * t) > thr) t = std::nextafter((float)t, 0.0f);
+        for (;;) {
+            volatile float u = std::nextafter((float)t, INFINITY);
+            if (!((float)(u * u) <= thr)) break;
+            t = u;
+        }
+        dm->residual_abs = t;
+    }
     dm->erp = (float)p->erp;
     dm->limit_max_imp = (float)p->limit_max_impulse;
     dm->kp = (float)p->motor_kp;

@@ -40,6 +40,8 @@ struct PgxDevModel {
     float neutral_q[PGX_NJ];
     /* contacts (pgx_sim_params) */
     float contact_dist, contact_erp, friction, warmstart;
+    float residual_abs;       /* largest t >= 0 with fl(t * t) <= residual_thr: the sweep exit
+                                 test resid * resid <= residual_thr as one compare, resid <= t */
 };
 
 struct PgxDevEnv {

@@ -30,11 +30,18 @@
 #include "pgx_rows.h"
 
 #ifdef PGX_PROF
-__device__ unsigned long long pgx_prof_counters[16];
+#define PGX_PROF_N 24
+__device__ unsigned long long pgx_prof_counters[PGX_PROF_N];
+/* per wave of the last launch (block id): start / end s_memtime, sweeps, non-far, redo, all-rows */
+#define PGX_PROF_WAVES 16384
+__device__ unsigned long long pgx_prof_wave[PGX_PROF_WAVES][8];
+extern "C" int pgx_prof_wave_read(unsigned long long* out, int n) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pgx_prof_wave), sizeof(unsigned long long) * 8 * (size_t)n);
+}
 extern "C" int pgx_prof_read(unsigned long long* out, int clear) {
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(pgx_prof_counters), sizeof(unsigned long long) * 16);
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(pgx_prof_counters), sizeof(unsigned long long) * PGX_PROF_N);
     if (e == hipSuccess && clear) {
-        unsigned long long z[16] = {0};
+        unsigned long long z[PGX_PROF_N] = {0};
         e = hipMemcpyToSymbol(HIP_SYMBOL(pgx_prof_counters), z, sizeof z);
     }
     return (int)e;
@@ -63,7 +70,7 @@ __device__ __forceinline__ MPtr fresh(MPtr p) { return fresh((uint64_t)p); }
  * deltas accumulated in LDS by phase, summed over waves into pgx_prof_counters at the
  * end of the launch.  Compiled out of the product library. */
 #ifdef PGX_PROF
-__shared__ volatile unsigned long long g_prof[16];   /* volatile: never kept in per-lane registers */
+__shared__ volatile unsigned long long g_prof[PGX_PROF_N];   /* volatile: never kept in per-lane registers */
 __shared__ volatile unsigned long long g_prof_t;
 __device__ __forceinline__ void prof_mark(int k) {
     const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -502,6 +509,9 @@ struct ContactLdsT {
     /* ReachAO: obstacle centres, per collision link the closest distance and unit vector */
     float aoC[PGX_AO_OBSTACLES][3][W];
     float aoD[PGX_AO_LINKS][W], aoU[PGX_AO_LINKS][3][W];
+    /* wide layout (Reach): the robot contact rows' J and M^-1 J^T per env, row-major
+     * [row q][dof], so lane q reads its row back with two ds_read_b128 (a transpose) */
+    float4 wJ[W == 64 ? 1 : W][3 * CG][2], wR[W == 64 ? 1 : W][3 * CG][2];
 };
 using ContactLds = ContactLdsT<64>;   /* one env per lane */
 using ContactLdsG = ContactLdsT<EPW>;
@@ -1525,14 +1535,14 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
                 if ((kPgxRowCode[r] >> 4) == 0) row(r, resid);
             if (CONT && any_contact) contact_rows(resid);
             PGX_PROF_SWEEP();
-            if (resid * resid <= m.residual_thr || it + 1 >= n_it) break;
+            if (resid <= m.residual_abs || it + 1 >= n_it) break;
             resid = 0.0f;
 #pragma unroll
             for (int r = 0; r < PGX_N_ROWS; r++)
                 if ((kPgxRowCode[r] >> 4) == 0) row(r, resid);
             if (CONT && any_contact) contact_rows(resid);
             PGX_PROF_SWEEP();
-            if (resid * resid <= m.residual_thr) break;
+            if (resid <= m.residual_abs) break;
         }
     } else {
         PGX_PROF_COUNT(10, 1);
@@ -1543,13 +1553,13 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
             for (int r = PGX_N_ROWS - 1; r >= 0; r--) row(r, resid);
             if (CONT && any_contact) contact_rows(resid);
             PGX_PROF_SWEEP();
-            if (resid * resid <= m.residual_thr || it + 1 >= n_it) break;
+            if (resid <= m.residual_abs || it + 1 >= n_it) break;
             resid = 0.0f;
 #pragma unroll
             for (int r = 0; r < PGX_N_ROWS; r++) row(r, resid);
             if (CONT && any_contact) contact_rows(resid);
             PGX_PROF_SWEEP();
-            if (resid * resid <= m.residual_thr) break;
+            if (resid <= m.residual_abs) break;
         }
     }
 #undef MINV
@@ -1590,7 +1600,18 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
  * same branches; only the lead lane stores. */
 /* One stepSimulation() in the wide layout: the same restatement as substep() (dynamics
  * shared through substep_dyn), rows solved in the same order with the same exit rule. */
-template <int OBJ, int CONT>
+/* the row table's limit block: (lower, upper) pairs of one dof each, after the 7 motor rows */
+constexpr bool limit_rows_paired() {
+    for (int r = 0; r < NJ; r++)
+        if ((kPgxRowCode[r] >> 4) != 0) return false;
+    for (int r = NJ; r + 1 < PGX_N_ROWS; r += 2)
+        if ((kPgxRowCode[r] >> 4) != 1 || (kPgxRowCode[r + 1] >> 4) != 2 ||
+            (kPgxRowCode[r] & 15) != (kPgxRowCode[r + 1] & 15))
+            return false;
+    return (PGX_N_ROWS - NJ) % 2 == 0;
+}
+
+template <int OBJ, int CONT, int PART = 1>
 __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q, float* qd, const float* tq,
                                           ObjState& ob, ContactLdsG* Lp, int es, int c, const LaneK& K) {
     MRef m = *fresh(mp);
@@ -1733,24 +1754,49 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
 #pragma unroll
     for (int s2 = 0; s2 < NQ; s2++) Wc[s2] = 0.0f;
     if constexpr (WROWS) {
-        sfor<0, NQ>([&](auto qc) __attribute__((always_inline)) {
-            constexpr int q = decltype(qc)::value, pq = q / 3, dq = q % 3;
-            if (g1k_any[pq]) {
-                sfor<0, NJ>([&](auto dc) __attribute__((always_inline)) {
-                    constexpr int d = decltype(dc)::value;
-                    Wm[d] = lane_sel<q>(bcast16<d>(cR[pq][dq]), Wm[d]);
+        if (g1k_any[0]) {   /* any robot point in the wave (points fill from slot 0) */
+            /* transpose through LDS: lane c < 7 holds J_q[c], (M^-1 J_q^T)[c] of every row q; lane
+             * q reads row q back.  Rows of idle points are zero (their J and R are), so every row
+             * is written.  One wave per workgroup: LDS ops of the wave complete in order. */
+            ContactLdsG& L = *Lp;
+            if (arm) {
+                float* wj = &L.wJ[es][0][0].x;
+                float* wr = &L.wR[es][0][0].x;
+                sfor<0, NQ>([&](auto qc) __attribute__((always_inline)) {
+                    constexpr int q = decltype(qc)::value;
+                    wj[8 * q + c] = cJ[q / 3][q % 3];
+                    wr[8 * q + c] = cR[q / 3][q % 3];
                 });
-                sfor<0, q + 1>([&](auto sc) __attribute__((always_inline)) {
-                    constexpr int s2 = decltype(sc)::value;
-                    if (g1k_any[s2 / 3]) {
-                        const float w = sum16(cJ[pq][dq] * cR[s2 / 3][s2 % 3]);
-                        Wc[s2] = lane_sel<q>(w, Wc[s2]);
-                        if constexpr (s2 != q) Wc[q] = lane_sel<s2>(w, Wc[q]);
-                    }
-                });
-                gw = lane_sel<q>(sum16(cJ[pq][dq] * gv), gw);
             }
-        });
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            const int qr = c < NQ ? c : NQ - 1;
+            const float4 ja = L.wJ[es][qr][0], jb = L.wJ[es][qr][1];
+            const float4 ra = L.wR[es][qr][0], rb = L.wR[es][qr][1];
+            const bool rl = c < NQ;
+            const float Jq[NJ] = {rl ? ja.x : 0.0f, rl ? ja.y : 0.0f, rl ? ja.z : 0.0f, rl ? ja.w : 0.0f,
+                                  rl ? jb.x : 0.0f, rl ? jb.y : 0.0f, rl ? jb.z : 0.0f};
+            Wm[0] = rl ? ra.x : 0.0f; Wm[1] = rl ? ra.y : 0.0f; Wm[2] = rl ? ra.z : 0.0f;
+            Wm[3] = rl ? ra.w : 0.0f; Wm[4] = rl ? rb.x : 0.0f; Wm[5] = rl ? rb.y : 0.0f;
+            Wm[6] = rl ? rb.z : 0.0f;
+            /* W[q][s] = J_q . (M^-1 J_s^T): lane q against the row broadcasts of column s */
+            sfor<0, NQ>([&](auto sc) __attribute__((always_inline)) {
+                constexpr int s2 = decltype(sc)::value;
+                if (g1k_any[s2 / 3]) {
+                    float w = Jq[0] * bcast16<0>(cR[s2 / 3][s2 % 3]);
+                    sfor<1, NJ>([&](auto lc) __attribute__((always_inline)) {
+                        constexpr int l = decltype(lc)::value;
+                        w = fmaf(Jq[l], bcast16<l>(cR[s2 / 3][s2 % 3]), w);
+                    });
+                    Wc[s2] = w;
+                }
+            });
+            float w = Jq[0] * bcast16<0>(gv);
+            sfor<1, NJ>([&](auto lc) __attribute__((always_inline)) {
+                constexpr int l = decltype(lc)::value;
+                w = fmaf(Jq[l], bcast16<l>(gv), w);
+            });
+            gw = w;
+        }
     }
 
     /* ---- motor / limit rows (as substep()): per row rhs and lambda, per dof jinv / den */
@@ -1760,11 +1806,10 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         den[d] = D.mdiag[d];
         jinv[d] = den[d] > 2.220446e-16f ? fast_rcp(den[d]) : 0.0f;
     }
-    float rhs[PGX_N_ROWS], lam[PGX_N_ROWS];
+    float rhs[PGX_N_ROWS];
 #pragma unroll
     for (int r = 0; r < PGX_N_ROWS; r++) {
         const int kind = kPgxRowCode[r] >> 4, d = kPgxRowCode[r] & 15;
-        lam[r] = 0.0f;
         rhs[r] = 0.0f;
         if (kind == 0) {
             const float pos_term = (tq[d] - q[d]) * m.inv_dt;
@@ -1810,14 +1855,27 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
      * a sum formed off the chain; delta' = delta den is the residual Bullet tracks, and the
      * coordinate updates take the columns pre-multiplied by jinv.  Chain per row:
      * v_sub_dpp -> med3 -> fmac (the next broadcast's source). */
-    float mcs[NJ], wms[NJ], mhi[NJ], lhi[NJ];
+    float mcs[NJ], wms[NJ];
+    /* motor rows: the shifted bound pair (lo' - lambda', hi' - lambda') tracked instead of
+     * lambda', one v_pk_add_f32 per row update (lambda' itself is not needed after the solve:
+     * joint rows are not warm-started); limit rows keep lambda' (fewer live registers) */
+    f2 bnd[NJ];
+    float lam[PGX_N_ROWS], lhi[NJ];
 #pragma unroll
     for (int d = 0; d < NJ; d++) {
         mcs[d] = mcol[d] * jinv[d];
         wms[d] = Wm[d] * jinv[d];
-        mhi[d] = m.max_impulse[d] * den[d];
         lhi[d] = m.limit_max_imp * den[d];
     }
+    auto init_bounds = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < PGX_N_ROWS; r++) {
+            const int kind = kPgxRowCode[r] >> 4, d = kPgxRowCode[r] & 15;
+            lam[r] = 0.0f;
+            if (kind == 0) bnd[d] = (f2){-m.max_impulse[d] * den[d], m.max_impulse[d] * den[d]};
+        }
+    };
+    init_bounds();
     auto mrow = [&](auto rc, float& resid) __attribute__((always_inline)) {
         constexpr int r = decltype(rc)::value;
         constexpr int kind = kPgxRowCode[r] >> 4, d = kPgxRowCode[r] & 15;
@@ -1825,16 +1883,13 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
          * formed off the chain, so the clamp yields the impulse increment directly */
         const float x = kind == 2 ? rhs[r] + bcast16<d>(gv) : rhs[r] - bcast16<d>(gv);
         float delta;
-        if constexpr (kind == 0 && !OBJ) {   /* the bound pair in one v_pk_add_f32 (measured: a
-                                               * gain on the arm tasks, a loss on the object ones) */
-            const f2 b = (f2){-mhi[d], mhi[d]} - lam[r];
-            delta = __builtin_amdgcn_fmed3f(x, b.x, b.y);
-        } else if constexpr (kind == 0) {
-            delta = __builtin_amdgcn_fmed3f(x, -mhi[d] - lam[r], mhi[d] - lam[r]);
+        if constexpr (kind == 0) {
+            delta = __builtin_amdgcn_fmed3f(x, bnd[d].x, bnd[d].y);
+            bnd[d] -= (f2){delta, delta};
         } else {
             delta = __builtin_amdgcn_fmed3f(x, -lam[r], lhi[d] - lam[r]);
+            lam[r] += delta;
         }
-        lam[r] += delta;
         const float sd = kind == 2 ? -delta : delta;
         gv += mcs[d] * sd;
         if constexpr (WROWS) gw += wms[d] * sd;
@@ -1958,48 +2013,87 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     auto limit_check = [&]() __attribute__((always_inline)) {
         viol = viol || (rl_c - gv > 0.0f) || (ru_c + gv > 0.0f);
     };
-    auto solve = [&](auto mode_c, auto nw_c) __attribute__((always_inline)) {
-        constexpr int MODE = decltype(mode_c)::value;   /* 0 far, 1 speculative, 2 all rows */
+    /* MODE 3 (partial, arm tasks): the limit pairs of the dofs the motor-impulse bound cannot
+     * clear in some env of the wave (dmask, at most 2 of them) run, the others are checked as in
+     * MODE 1 -- at the block's start and after every pair that runs, i.e. once per stretch of
+     * constant velocity, which covers each skipped pair's own position.  The running pairs sit
+     * in slots: lane 7 + S (an idle coordinate lane of the arm tasks) mirrors dof d_S -- it gets
+     * lane d_S's coefficients, so its velocity delta evolves bit for bit as lane d_S's -- and a
+     * slot row reads it with a compile-time broadcast, so the sweep has no runtime branch (a
+     * branch per pair measured slower than all 21 rows).  Same arithmetic as mrow: the result is
+     * bitwise the all-rows solve's. */
+    constexpr int KMAX = 1;
+    unsigned dmask = 0u;
+    float smcs[KMAX], swms[KMAX], srh[KMAX][2], slhi[KMAX], slam[KMAX][2];
+    auto srow = [&](auto sc, auto kc, float& resid) __attribute__((always_inline)) {
+        constexpr int S = decltype(sc)::value, KIND = decltype(kc)::value;   /* 1 lower, 2 upper */
+        const float x = KIND == 2 ? srh[S][1] + bcast16<NJ + S>(gv) : srh[S][0] - bcast16<NJ + S>(gv);
+        const float delta = __builtin_amdgcn_fmed3f(x, -slam[S][KIND - 1], slhi[S] - slam[S][KIND - 1]);
+        slam[S][KIND - 1] += delta;
+        const float sd = KIND == 2 ? -delta : delta;
+        gv += smcs[S] * sd;
+        if constexpr (WROWS) gw += swms[S] * sd;
+        resid = fmaxf(resid, fabsf(delta));
+    };
+    static_assert(limit_rows_paired(), "limit rows come as (lower, upper) pairs of one dof after the motor rows");
+    auto solve = [&](auto mode_c, auto nw_c, auto k_c) __attribute__((always_inline)) {
+        constexpr int MODE = decltype(mode_c)::value;   /* 0 far, 1 speculative, 2 all rows, 3 partial */
         constexpr int NW = decltype(nw_c)::value;
+        constexpr int K = decltype(k_c)::value;         /* MODE 3: slots in use */
         for (int it = 0; it < n_it; it += 2) {
             float resid = 0.0f;
-            if constexpr (MODE == 1) limit_check();
+            if constexpr (MODE == 1 || MODE == 3) limit_check();
+            if constexpr (MODE == 3) {   /* the limit block leads the reversed sweep */
+                sfor<0, K>([&](auto i) __attribute__((always_inline)) {
+                    constexpr int S = K - 1 - decltype(i)::value;
+                    srow(IC<S>{}, IC<2>{}, resid);
+                    srow(IC<S>{}, IC<1>{}, resid);
+                    limit_check();
+                });
+            }
             sfor<0, PGX_N_ROWS>([&](auto i) __attribute__((always_inline)) {
                 constexpr int r = PGX_N_ROWS - 1 - decltype(i)::value;
                 if constexpr (MODE == 2 || (kPgxRowCode[r] >> 4) == 0) mrow(IC<r>{}, resid);
             });
             if (CONT && (NW > 0 || (NW < 0 && any_contact))) contact_rows(nw_c, resid);
             PGX_PROF_SWEEP();
-            if (resid * resid <= m.residual_thr || it + 1 >= n_it) break;
+            if (resid <= m.residual_abs || it + 1 >= n_it) break;
             resid = 0.0f;
             sfor<0, PGX_N_ROWS>([&](auto i) __attribute__((always_inline)) {
                 constexpr int r = decltype(i)::value;
                 if constexpr (MODE == 2 || (kPgxRowCode[r] >> 4) == 0) mrow(IC<r>{}, resid);
             });
-            if constexpr (MODE == 1) limit_check();
+            if constexpr (MODE == 1 || MODE == 3) limit_check();
+            if constexpr (MODE == 3) {
+                sfor<0, K>([&](auto sc) __attribute__((always_inline)) {
+                    srow(sc, IC<1>{}, resid);
+                    srow(sc, IC<2>{}, resid);
+                    limit_check();
+                });
+            }
             if (CONT && (NW > 0 || (NW < 0 && any_contact))) contact_rows(nw_c, resid);
             PGX_PROF_SWEEP();
-            if (resid * resid <= m.residual_thr) break;
+            if (resid <= m.residual_abs) break;
         }
     };
-    /* the speculative Reach solve with the robot point count fixed at compile time (above) */
-    auto solve_spec = [&]() __attribute__((always_inline)) {
+    /* Reach: the robot point count fixed at compile time (above) for every mode but far */
+    auto solve_w = [&](auto mode_c, auto k_c) __attribute__((always_inline)) {
         if constexpr (WROWS) {
-            if (n1w == 0) solve(IC<1>{}, IC<0>{});
-            else if (n1w <= 2) solve(IC<1>{}, IC<2>{});
-            else solve(IC<1>{}, IC<4>{});
+            if (n1w == 0) solve(mode_c, IC<0>{}, k_c);
+            else if (n1w <= 2) solve(mode_c, IC<2>{}, k_c);
+            else solve(mode_c, IC<4>{}, k_c);
         } else {
-            solve(IC<1>{}, IC<-1>{});
+            solve(mode_c, IC<-1>{}, k_c);
         }
     };
     if (__all(far)) {   /* (Reach: far implies no robot point in the wave) */
-        solve(IC<0>{}, IC<WROWS ? 0 : -1>{});
+        solve(IC<0>{}, IC<WROWS ? 0 : -1>{}, IC<0>{});
     } else {
         PGX_PROF_COUNT(10, 1);
         init_limit_rows();
         /* (not for the object tasks: a third copy of their 24-row sweep grows the kernel past
          * the instruction cache -- Push measured 1.6 -> 2.4 ms) */
-        if (!OBJ && __all(far_nc) && e.pgs_mode != 2) {
+        if (!OBJ && e.pgs_mode != 2) {
             float rl[NJ], ru[NJ];
 #pragma unroll
             for (int r = NJ; r < PGX_N_ROWS; r++) {
@@ -2009,11 +2103,68 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             }
             rl_c = pick_arm(rl, -1.0f);
             ru_c = pick_arm(ru, -1.0f);
+            const bool spec_all = __all(far_nc);
+            int nk = 0;
+            if (!spec_all) {   /* partial: the dofs the motor bound cannot clear, in any env */
+                const uint64_t bm = __ballot(arm && !ok_c);
+                dmask = __builtin_amdgcn_readfirstlane((unsigned)((bm | (bm >> 16) | (bm >> 32) | (bm >> 48)) & 0x7Fu));
+                nk = __builtin_popcount(dmask);
+            }
             const float gv0 = gv, gw0 = gw;
             float cl0[NPP];
 #pragma unroll
             for (int p = 0; p < NP; p++) cl0[p] = clam[p][0];
-            solve_spec();
+            if (PART && !spec_all && nk <= KMAX) {
+                PGX_PROF_COUNT(7, 1);
+                /* slots in the pairs' table order; slot lane NJ + S mirrors dof d_S */
+                int ds[2] = {0, 0};
+                int k = 0;
+                sfor<0, (PGX_N_ROWS - NJ) / 2>([&](auto pc) __attribute__((always_inline)) {
+                    constexpr int d = kPgxRowCode[NJ + 2 * decltype(pc)::value] & 15;
+                    if ((dmask >> d) & 1u) { if (k == 0) ds[0] = d; else ds[1] = d; k++; }
+                });
+                ds[0] = __builtin_amdgcn_readfirstlane(ds[0]);
+                ds[1] = __builtin_amdgcn_readfirstlane(ds[1]);
+                const int src = (int)(threadIdx.x & ~(unsigned)(GW - 1));
+                auto mirror = [&](float& x) __attribute__((always_inline)) {
+                    x = lane_sel<NJ>(__shfl(x, src + ds[0]), x);
+                    if (KMAX > 1 && nk > 1) x = lane_sel<NJ + 1>(__shfl(x, src + ds[1]), x);
+                };
+#pragma unroll
+                for (int d = 0; d < NJ; d++) mirror(mcs[d]);
+                mirror(gv);
+                if (g1_any) {
+#pragma unroll
+                    for (int p = 0; p < NP; p++)
+#pragma unroll
+                        for (int dir = 0; dir < 3; dir++) mirror(cR[p][dir]);
+                }
+                /* the slots' row data: dof d_S's entries, selected with uniform masks */
+#pragma unroll
+                for (int S = 0; S < KMAX; S++) {
+                    smcs[S] = mcs[0]; swms[S] = wms[0]; slhi[S] = lhi[0];
+                    srh[S][0] = rl[0]; srh[S][1] = ru[0];
+                    slam[S][0] = 0.0f; slam[S][1] = 0.0f;
+                    sfor<1, NJ>([&](auto dc) __attribute__((always_inline)) {
+                        constexpr int d = decltype(dc)::value;
+                        const bool hit = ds[S] == d;   /* wave-uniform */
+                        auto sel = [&](float a, float o) __attribute__((always_inline)) { return hit ? a : o; };
+                        smcs[S] = sel(mcs[d], smcs[S]); swms[S] = sel(wms[d], swms[S]);
+                        slhi[S] = sel(lhi[d], slhi[S]);
+                        srh[S][0] = sel(rl[d], srh[S][0]); srh[S][1] = sel(ru[d], srh[S][1]);
+                    });
+                }
+                /* the checks skip the running dofs and the slot lanes */
+                if (((dmask >> c) & 1u) || (c >= NJ && c < NJ + nk)) { rl_c = -3.0e38f; ru_c = -3.0e38f; }
+                PGX_PROF_COUNT(16, nk == 2 ? 1 : 0);
+                PGX_PROF_COUNT(18, any_contact ? 1 : 0);
+                if (KMAX == 1 || nk == 1) solve_w(IC<3>{}, IC<1>{});
+                else solve_w(IC<3>{}, IC<KMAX>{});
+            } else if (spec_all) {
+                solve_w(IC<1>{}, IC<0>{});
+            } else {
+                viol = true;   /* more than KMAX dofs: all rows */
+            }
             if (__any(row_any(viol)) || e.pgs_mode == 3) {
                 PGX_PROF_COUNT(12, 1);
                 gv = gv0;
@@ -2024,13 +2175,12 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                     clam[p][1] = 0.0f;
                     clam[p][2] = 0.0f;
                 }
-#pragma unroll
-                for (int r = 0; r < PGX_N_ROWS; r++) lam[r] = 0.0f;
-                solve(IC<2>{}, IC<-1>{});
+                init_bounds();
+                solve_w(IC<2>{}, IC<0>{});
             }
         } else {
             PGX_PROF_COUNT(13, 1);
-            solve(IC<2>{}, IC<-1>{});
+            solve_w(IC<2>{}, IC<0>{});
         }
     }
     PGX_PROF_SWEEPS_DONE();
@@ -2618,7 +2768,7 @@ __device__ __forceinline__ int xcd_block() {
 
 /* WIDE = 0: one env per lane (64 per wave); WIDE = 1: 16 lanes per env (4 per wave,
  * substep_g), the redundant lanes compute the same values and only the lead lane stores. */
-template <int CONTROL, int OBJ, int CONT, int AO, int WIDE>
+template <int CONTROL, int OBJ, int CONT, int AO, int WIDE, int PART = 1>
 __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, const PgxDevEnv& e,
                                           const PgxDevState& s, const float* __restrict__ action, const PgxDevOut& o) {
     using LT = ContactLdsT<WIDE ? EPW : 64>;
@@ -2650,8 +2800,9 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
         }
     }
 #ifdef PGX_PROF
-    if (threadIdx.x < 16) g_prof[threadIdx.x] = 0;
+    if (threadIdx.x < PGX_PROF_N) g_prof[threadIdx.x] = 0;
     g_prof_t = __builtin_amdgcn_s_memtime();
+    const unsigned long long prof_t0 = g_prof_t;
 #endif
     const MPtr mp = fresh((uint64_t)mdev);
     MRef m = *mp;
@@ -2699,7 +2850,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     const int n_substeps = m.n_substeps;
     bool collided = false;
     for (int st = 0; st < n_substeps; st++) {
-        if constexpr (WIDE) substep_g<OBJ, CONT>(mp, e, q, qd, tq, ob, L, ln, c, lk);
+        if constexpr (WIDE) substep_g<OBJ, CONT, PART>(mp, e, q, qd, tq, ob, L, ln, c, lk);
         else substep<OBJ, CONT>(mp, e, q, qd, tq, ob, L, ln);
         if constexpr (AO) {   /* ReachAO step_check_collision: check after every substep, stop on contact */
             ao_caps(*fresh(mp), q, *L, ln);
@@ -2800,8 +2951,14 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     s.episode[i] = episode;
 #ifdef PGX_PROF
     PGX_PROF_MARK(6);
-    if (threadIdx.x == 0)
-        for (int k = 0; k < 16; k++) atomicAdd(&pgx_prof_counters[k], g_prof[k]);
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < PGX_PROF_N; k++) atomicAdd(&pgx_prof_counters[k], g_prof[k]);
+        if (blockIdx.x < PGX_PROF_WAVES) {
+            unsigned long long* w = pgx_prof_wave[blockIdx.x];
+            w[0] = prof_t0; w[1] = g_prof_t; w[2] = g_prof[8]; w[3] = g_prof[10]; w[4] = g_prof[12]; w[5] = g_prof[13];
+            w[6] = g_prof[7]; w[7] = g_prof[4];
+        }
+    }
 #endif
 }
 
@@ -2819,7 +2976,7 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
 template <int CONTROL, int OBJ, int CONT, int AO, int WIDE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void step_kernel_o2(
     const PgxDevModel* __restrict__ mdev, PgxDevEnv e, PgxDevState s, const float* __restrict__ action, PgxDevOut o) {
-    step_body<CONTROL, OBJ, CONT, AO, WIDE>(mdev, e, s, action, o);
+    step_body<CONTROL, OBJ, CONT, AO, WIDE, 0>(mdev, e, s, action, o);
 }
 
 template <int OBJ, int AO>

@@ -19,7 +19,7 @@ NAMES = ["prologue+IK", "FK+detect", "dynamics", "row setup", "PGS sweeps", "int
 
 def run(env_id, n, contacts, launches=100, warm=50):
     lib = _native.load()
-    buf = (C.c_ulonglong * 16)()
+    buf = (C.c_ulonglong * 24)()
     venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=0, contacts=contacts)
     venv.reset_tensors()
     for t in range(warm):
@@ -36,8 +36,26 @@ def run(env_id, n, contacts, launches=100, warm=50):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / launches
     lib.pgx_prof_read(buf, 1)
-    waves = n // 64
-    per = [buf[k] / (waves * launches) for k in range(16)]
+    wide = venv._cfg.lanes_per_env == 16 or (venv._cfg.lanes_per_env == 0 and n <= 8192)
+    waves = n // (4 if wide else 64)
+    wv = (C.c_ulonglong * (8 * waves))()
+    lib.pgx_prof_wave_read(wv, waves)
+    import numpy as np
+    w = np.frombuffer(wv, dtype=np.uint64).reshape(waves, 8).astype(np.int64)
+    dur = w[:, 1] - w[:, 0]
+    start = w[:, 0] - w[:, 0].min()
+    end = w[:, 1] - w[:, 0].min()
+    top = np.argsort(dur)[-max(waves // 100, 1):]
+    wave_stats = {"waves": waves, "dur_mean": float(dur.mean()), "dur_p50": float(np.median(dur)),
+                  "dur_p99": float(np.percentile(dur, 99)), "dur_max": float(dur.max()),
+                  "start_max": float(start.max()), "end_max": float(end.max()),
+                  "sweeps_mean": float(w[:, 2].mean()), "sweeps_top1pct": float(w[top, 2].mean()),
+                  "nonfar_mean": float(w[:, 3].mean()), "nonfar_top1pct": float(w[top, 3].mean()),
+                  "redo_mean": float(w[:, 4].mean()), "redo_top1pct": float(w[top, 4].mean()),
+                  "allrows_mean": float(w[:, 5].mean()), "allrows_top1pct": float(w[top, 5].mean()),
+                  "partial_mean": float(w[:, 6].mean()), "partial_top1pct": float(w[top, 6].mean()),
+                  "pgs_cyc_mean": float(w[:, 7].mean()), "pgs_cyc_top1pct": float(w[top, 7].mean())}
+    per = [buf[k] / (waves * launches) for k in range(24)]
     tot = sum(per[:7]) + per[14] + per[15]
     out = {"env_id": env_id, "n": n, "contacts": contacts, "ms_per_step": ms,
            "cycles_per_wave_step": tot, "clock_ghz_est": tot / (ms * 1e6),
@@ -45,8 +63,9 @@ def run(env_id, n, contacts, launches=100, warm=50):
            "share": {NAMES[k]: round(per[k] / tot, 3) for k in range(7)},
            "sweeps_per_substep": per[8] / max(per[9], 1e-9), "nonfar_frac": per[10] / max(per[9], 1e-9),
            "contact_substep_frac": per[11] / max(per[9], 1e-9),
-           "speculation_redo_frac": per[12] / max(per[9], 1e-9), "all_rows_frac": per[13] / max(per[9], 1e-9),
-           "cycles_per_sweep": per[4] / max(per[8], 1e-9),
+           "speculation_redo_frac": per[12] / max(per[9], 1e-9), "partial_frac": per[7] / max(per[9], 1e-9),
+           "partial_k2_frac": per[16] / max(per[7], 1e-9), "partial_contact_frac": per[18] / max(per[7], 1e-9), "all_rows_frac": per[13] / max(per[9], 1e-9),
+           "cycles_per_sweep": per[4] / max(per[8], 1e-9), "last_launch_waves": wave_stats,
            "dynamics_split": {"newton_euler": round(per[14]), "crba_cholesky": round(per[15]),
                               "minv_and_rest": round(per[2])}}
     venv.close()
