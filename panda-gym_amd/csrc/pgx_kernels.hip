@@ -1911,7 +1911,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
 #pragma unroll
         for (int dir = 0; dir < 3; dir++) {
             rok[p][dir] = act[p] && cjinv[p][dir] != 0.0f;
-            fk[p][dir] = mu * cjinv[p][0] * cden[p][dir];
+            fk[p][dir] = rok[p][dir] ? mu * cjinv[p][0] * cden[p][dir] : 0.0f;   /* unusable row: bounds 0 */
             crhs[p][dir] *= cden[p][dir];
             clam[p][dir] *= cden[p][dir];
             cR[p][dir] *= cjinv[p][dir];
@@ -1935,11 +1935,12 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         float delta;
         if constexpr (WROWS) {
             float lo, hi;
-            if (fr) {
-                const bool idle = !rok[p][dir] || !(ln_n > 0.0f);
-                const f2 b = (f2){-fk[p][dir], fk[p][dir]} * ln_n - lm;
-                lo = idle ? 0.0f : b.x;
-                hi = idle ? 0.0f : b.y;
+            if (fr) {   /* idle while the normal impulse is 0: the bound pair times 0 (an unusable
+                         * row has fk = 0 and lambda' = 0, so its bounds are 0 as well) */
+                const float mk = ln_n > 0.0f ? 1.0f : 0.0f;
+                const f2 b = ((f2){-fk[p][dir], fk[p][dir]} * ln_n - lm) * mk;
+                lo = b.x;
+                hi = b.y;
             } else {
                 lo = -lm;
                 hi = chi[p];
@@ -1957,10 +1958,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         }
         gv += cR[p][dir] * delta;
         if constexpr (WROWS) gw += Wc[3 * p + dir] * delta;
-        /* a normal row sits alone between branches, where fmaxf costs a canonicalising max
-         * and an and; med3 against +big is the same maximum in one instruction */
-        if (fr || !WROWS) resid = fmaxf(resid, fabsf(delta));
-        else resid = __builtin_amdgcn_fmed3f(fabsf(delta), resid, 3.0e38f);
+        resid = fmaxf(resid, fabsf(delta));
     };
     /* the wave's largest robot-point count, a scalar: the per-point branches in the sweep
      * are s_cmp on it (a per-point bool there turns into a VALU mask round trip per row) */
