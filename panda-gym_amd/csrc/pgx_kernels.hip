@@ -509,9 +509,9 @@ struct ContactLdsT {
     /* ReachAO: obstacle centres, per collision link the closest distance and unit vector */
     float aoC[PGX_AO_OBSTACLES][3][W];
     float aoD[PGX_AO_LINKS][W], aoU[PGX_AO_LINKS][3][W];
-    /* wide layout (Reach): the robot contact rows' J and M^-1 J^T per env, row-major
-     * [row q][dof], so lane q reads its row back with two ds_read_b128 (a transpose) */
-    float4 wJ[W == 64 ? 1 : W][3 * CG][2], wR[W == 64 ? 1 : W][3 * CG][2];
+    /* wide layout: the contact rows' J (13 coordinates) and M^-1 J^T (arm part) per env,
+     * row-major [row q][coordinate], so lane q reads its row back with ds_read_b128 (a transpose) */
+    float4 wJ[W == 64 ? 1 : W][6 * CG][4], wR[W == 64 ? 1 : W][6 * CG][2];
 };
 using ContactLds = ContactLdsT<64>;   /* one env per lane */
 using ContactLdsG = ContactLdsT<EPW>;
@@ -1738,64 +1738,87 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         }
     }
 
-    /* ---- Reach: contact-row velocities in lanes.  Lane q = 3 point + dir holds w_q = J_q.dv
-     * (register gw) and the Delassus entries W[q][s] = J_q M^-1 J_s^T of every row s (Wm:
-     * motor / limit rows of dof d, = (M^-1 J_q^T)_d; Wc: contact rows), so a contact row
-     * reads its velocity with one broadcast, like a motor row, instead of a 16-lane
-     * reduction; every row's impulse also updates gw (one more off-chain fma). */
-    constexpr bool WROWS = CONT && !OBJ;
-    constexpr int NQ = WROWS ? 3 * CG : 1;
-    bool g1k_any[CG];
+    /* ---- contact-row velocities in lanes.  Lane q = 3 point + dir holds w_q = J_q.dv (register
+     * gw; the object tasks' rows 16..23 in a second register gw2, lanes 0..7) and the Delassus
+     * entries W[q][s] = J_q M^-1 J_s^T of every row s (Wm: motor / limit rows of dof d,
+     * = (M^-1 J_q^T)_d; Wc: contact rows), so a contact row reads its velocity with one
+     * broadcast, like a motor row, instead of a 16-lane reduction; every row's impulse also
+     * updates gw (one more off-chain fma; {gw, gw2} as one packed pair). */
+    constexpr bool WROWS = CONT;
+    constexpr int NQ = WROWS ? 3 * NP : 1;      /* 12 (Reach), 24 (object tasks) */
+    constexpr bool TWO = NQ > GW;
+    constexpr int NC = OBJ ? 13 : NJ;           /* generalized coordinates in lanes */
+    bool g1k_any[CG], g0k_any[CG];
 #pragma unroll
-    for (int k = 0; k < CG; k++) g1k_any[k] = CONT && __any(k < n1);
-    float gw = 0.0f, Wm[NJ], Wc[NQ];
+    for (int k = 0; k < CG; k++) {
+        g1k_any[k] = CONT && __any(k < n1);
+        g0k_any[k] = CONT && OBJ && __any(k < n0);
+    }
+    /* rows of point p live in the wave (slots fill from 0) */
+    auto row_live = [&](int pp) __attribute__((always_inline)) { return pp < P0 ? g0k_any[pp] : g1k_any[pp - P0]; };
+    float gw = 0.0f, gw2 = 0.0f, Wm[NJ], Wm2[NJ], Wc[NQ], Wc2[NQ];
 #pragma unroll
-    for (int d = 0; d < NJ; d++) Wm[d] = 0.0f;
+    for (int d = 0; d < NJ; d++) { Wm[d] = 0.0f; Wm2[d] = 0.0f; }
 #pragma unroll
-    for (int s2 = 0; s2 < NQ; s2++) Wc[s2] = 0.0f;
+    for (int s2 = 0; s2 < NQ; s2++) { Wc[s2] = 0.0f; Wc2[s2] = 0.0f; }
     if constexpr (WROWS) {
-        if (g1k_any[0]) {   /* any robot point in the wave (points fill from slot 0) */
-            /* transpose through LDS: lane c < 7 holds J_q[c], (M^-1 J_q^T)[c] of every row q; lane
-             * q reads row q back.  Rows of idle points are zero (their J and R are), so every row
-             * is written.  One wave per workgroup: LDS ops of the wave complete in order. */
+        if (g1k_any[0] || (OBJ && g0k_any[0])) {   /* any contact point in the wave (slots fill from 0) */
+            /* transpose through LDS: lane c < NC holds J_q[c], (M^-1 J_q^T)[c] of every row q; lane
+             * q reads row q back (and row 16 + q into the second register).  Rows of idle points
+             * are zero (their J and R are), so every row is written.  One wave per workgroup: LDS
+             * ops of the wave complete in order. */
             ContactLdsG& L = *Lp;
-            if (arm) {
+            if (c < NC) {
                 float* wj = &L.wJ[es][0][0].x;
                 float* wr = &L.wR[es][0][0].x;
                 sfor<0, NQ>([&](auto qc) __attribute__((always_inline)) {
                     constexpr int q = decltype(qc)::value;
-                    wj[8 * q + c] = cJ[q / 3][q % 3];
-                    wr[8 * q + c] = cR[q / 3][q % 3];
+                    wj[16 * q + c] = cJ[q / 3][q % 3];
+                    if (c < NJ) wr[8 * q + c] = cR[q / 3][q % 3];
                 });
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            const int qr = c < NQ ? c : NQ - 1;
-            const float4 ja = L.wJ[es][qr][0], jb = L.wJ[es][qr][1];
-            const float4 ra = L.wR[es][qr][0], rb = L.wR[es][qr][1];
-            const bool rl = c < NQ;
-            const float Jq[NJ] = {rl ? ja.x : 0.0f, rl ? ja.y : 0.0f, rl ? ja.z : 0.0f, rl ? ja.w : 0.0f,
-                                  rl ? jb.x : 0.0f, rl ? jb.y : 0.0f, rl ? jb.z : 0.0f};
-            Wm[0] = rl ? ra.x : 0.0f; Wm[1] = rl ? ra.y : 0.0f; Wm[2] = rl ? ra.z : 0.0f;
-            Wm[3] = rl ? ra.w : 0.0f; Wm[4] = rl ? rb.x : 0.0f; Wm[5] = rl ? rb.y : 0.0f;
-            Wm[6] = rl ? rb.z : 0.0f;
-            /* W[q][s] = J_q . (M^-1 J_s^T): lane q against the row broadcasts of column s */
-            sfor<0, NQ>([&](auto sc) __attribute__((always_inline)) {
-                constexpr int s2 = decltype(sc)::value;
-                if (g1k_any[s2 / 3]) {
-                    float w = Jq[0] * bcast16<0>(cR[s2 / 3][s2 % 3]);
-                    sfor<1, NJ>([&](auto lc) __attribute__((always_inline)) {
-                        constexpr int l = decltype(lc)::value;
-                        w = fmaf(Jq[l], bcast16<l>(cR[s2 / 3][s2 % 3]), w);
-                    });
-                    Wc[s2] = w;
+            auto build = [&](auto reg_c, float* Wmr, float* Wcr, float& gwr) __attribute__((always_inline)) {
+                constexpr int R0 = decltype(reg_c)::value * GW;   /* first row of this register */
+                const int qr = R0 + c < NQ ? R0 + c : NQ - 1;
+                const bool rl = R0 + c < NQ;
+                float Jq[NC];
+                const float4* jrow = &L.wJ[es][qr][0];
+#pragma unroll
+                for (int v4 = 0; v4 < (NC + 3) / 4; v4++) {
+                    const float4 t = jrow[v4];
+                    const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (4 * v4 + u < NC) Jq[4 * v4 + u] = rl ? tv[u] : 0.0f;
                 }
-            });
-            float w = Jq[0] * bcast16<0>(gv);
-            sfor<1, NJ>([&](auto lc) __attribute__((always_inline)) {
-                constexpr int l = decltype(lc)::value;
-                w = fmaf(Jq[l], bcast16<l>(gv), w);
-            });
-            gw = w;
+                const float4 ra = L.wR[es][qr][0], rb = L.wR[es][qr][1];
+                Wmr[0] = rl ? ra.x : 0.0f; Wmr[1] = rl ? ra.y : 0.0f; Wmr[2] = rl ? ra.z : 0.0f;
+                Wmr[3] = rl ? ra.w : 0.0f; Wmr[4] = rl ? rb.x : 0.0f; Wmr[5] = rl ? rb.y : 0.0f;
+                Wmr[6] = rl ? rb.z : 0.0f;
+                /* W[q][s] = J_q . (M^-1 J_s^T): lane q against the row broadcasts of column s
+                 * (object-scene rows have object coordinates only) */
+                sfor<0, NQ>([&](auto sc) __attribute__((always_inline)) {
+                    constexpr int s2 = decltype(sc)::value;
+                    constexpr int C0 = (s2 / 3 < P0) ? NJ : 0;
+                    if (row_live(s2 / 3)) {
+                        float w = Jq[C0] * bcast16<C0>(cR[s2 / 3][s2 % 3]);
+                        sfor<C0 + 1, NC>([&](auto lc) __attribute__((always_inline)) {
+                            constexpr int l = decltype(lc)::value;
+                            w = fmaf(Jq[l], bcast16<l>(cR[s2 / 3][s2 % 3]), w);
+                        });
+                        Wcr[s2] = w;
+                    }
+                });
+                float w = Jq[0] * bcast16<0>(gv);
+                sfor<1, NC>([&](auto lc) __attribute__((always_inline)) {
+                    constexpr int l = decltype(lc)::value;
+                    w = fmaf(Jq[l], bcast16<l>(gv), w);
+                });
+                gwr = w;
+            };
+            build(IC<0>{}, Wm, Wc, gw);
+            if constexpr (TWO) build(IC<1>{}, Wm2, Wc2, gw2);
         }
     }
 
@@ -1855,7 +1878,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
      * a sum formed off the chain; delta' = delta den is the residual Bullet tracks, and the
      * coordinate updates take the columns pre-multiplied by jinv.  Chain per row:
      * v_sub_dpp -> med3 -> fmac (the next broadcast's source). */
-    float mcs[NJ], wms[NJ];
+    float mcs[NJ], wms[NJ], wms2[NJ];
     /* motor rows: the shifted bound pair (lo' - lambda', hi' - lambda') tracked instead of
      * lambda', one v_pk_add_f32 per row update (lambda' itself is not needed after the solve:
      * joint rows are not warm-started); limit rows keep lambda' (fewer live registers) */
@@ -1865,6 +1888,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     for (int d = 0; d < NJ; d++) {
         mcs[d] = mcol[d] * jinv[d];
         wms[d] = Wm[d] * jinv[d];
+        wms2[d] = Wm2[d] * jinv[d];
         lhi[d] = m.limit_max_imp * den[d];
     }
     auto init_bounds = [&]() __attribute__((always_inline)) {
@@ -1893,6 +1917,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         const float sd = kind == 2 ? -delta : delta;
         gv += mcs[d] * sd;
         if constexpr (WROWS) gw += wms[d] * sd;
+        if constexpr (TWO) gw2 += wms2[d] * sd;
         resid = fmaxf(resid, fabsf(delta));
     };
     /* friction coefficient in a register: a model load inside the bound selects makes the
@@ -1918,7 +1943,10 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         }
     if constexpr (WROWS) {
 #pragma unroll
-        for (int q = 0; q < NQ; q++) Wc[q] *= cjinv[q / 3][q % 3];
+        for (int q = 0; q < NQ; q++) {
+            Wc[q] *= cjinv[q / 3][q % 3];
+            if (TWO) Wc2[q] *= cjinv[q / 3][q % 3];
+        }
     }
     /* shifted bounds as for the joint rows: delta' = clamp(rhs' - w, lo' - lambda', hi' - lambda').
      * A normal row's upper bound is +inf (0 with lambda' = 0 for an unusable row, below); a
@@ -1930,34 +1958,25 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         if (WROWS && !rok[p][0]) clam[p][0] = 0.0f;   /* already applied to gv; the cache stores lambda' jinv = 0 */
     }
     auto crow = [&](auto pc, auto dc, const bool fr, float& resid) __attribute__((always_inline)) {
-        constexpr int p = decltype(pc)::value, dir = decltype(dc)::value;
+        constexpr int p = decltype(pc)::value, dir = decltype(dc)::value, q = 3 * p + dir;
         const float ln_n = clam[p][0], lm = clam[p][dir];
-        float delta;
-        if constexpr (WROWS) {
-            float lo, hi;
-            if (fr) {   /* idle while the normal impulse is 0: the bound pair times 0 (an unusable
-                         * row has fk = 0 and lambda' = 0, so its bounds are 0 as well) */
-                const float mk = ln_n > 0.0f ? 1.0f : 0.0f;
-                const f2 b = ((f2){-fk[p][dir], fk[p][dir]} * ln_n - lm) * mk;
-                lo = b.x;
-                hi = b.y;
-            } else {
-                lo = -lm;
-                hi = chi[p];
-            }
-            delta = __builtin_amdgcn_fmed3f(crhs[p][dir] - bcast16<3 * p + dir>(gw), lo, hi);
-            clam[p][dir] = lm + delta;
-        } else {   /* the object tasks keep the clamped-sum form (measured faster there: Push
-                    * 1.61 vs 1.66 ms, the 16-lane reduction dominates their rows) */
-            const bool idle = !rok[p][dir] || (fr && !(ln_n > 0.0f));
-            const float lo = idle ? lm : (fr ? -fk[p][dir] * ln_n : 0.0f);
-            const float hi = idle ? lm : (fr ? fk[p][dir] * ln_n : 3.0e38f);
-            const float nl = __builtin_amdgcn_fmed3f((lm + crhs[p][dir]) - sum16(cJ[p][dir] * gv), lo, hi);
-            delta = nl - lm;
-            clam[p][dir] = nl;
+        float lo, hi;
+        if (fr) {   /* idle while the normal impulse is 0: the bound pair times 0 (an unusable
+                     * row has fk = 0 and lambda' = 0, so its bounds are 0 as well) */
+            const float mk = ln_n > 0.0f ? 1.0f : 0.0f;
+            const f2 b = ((f2){-fk[p][dir], fk[p][dir]} * ln_n - lm) * mk;
+            lo = b.x;
+            hi = b.y;
+        } else {
+            lo = -lm;
+            hi = chi[p];
         }
+        const float w = q < GW ? bcast16<q % GW>(gw) : bcast16<q % GW>(gw2);
+        const float delta = __builtin_amdgcn_fmed3f(crhs[p][dir] - w, lo, hi);
+        clam[p][dir] = lm + delta;
         gv += cR[p][dir] * delta;
-        if constexpr (WROWS) gw += Wc[3 * p + dir] * delta;
+        gw += Wc[q] * delta;
+        if constexpr (TWO) gw2 += Wc2[q] * delta;
         resid = fmaxf(resid, fabsf(delta));
     };
     /* the wave's largest robot-point count, a scalar: the per-point branches in the sweep
@@ -1985,7 +2004,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             if (NW < 0 && !g1_any) continue;
             sfor<0, (CONT ? (NW >= 0 ? NW : CG) : 0)>([&](auto kc) __attribute__((always_inline)) {
                 constexpr int k = decltype(kc)::value;
-                if (NW >= 0 || (WROWS ? k < n1w : g1k_any[k])) {   /* (the object tasks measured faster with the bool) */
+                if (NW >= 0 || k < n1w) {
                     if (fr) { crow(IC<P0 + k>{}, IC<1>{}, true, resid); crow(IC<P0 + k>{}, IC<2>{}, true, resid); }
                     else crow(IC<P0 + k>{}, IC<0>{}, false, resid);
                 }
@@ -2015,22 +2034,24 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
      * clear in some env of the wave (dmask, at most 2 of them) run, the others are checked as in
      * MODE 1 -- at the block's start and after every pair that runs, i.e. once per stretch of
      * constant velocity, which covers each skipped pair's own position.  The running pairs sit
-     * in slots: lane 7 + S (an idle coordinate lane of the arm tasks) mirrors dof d_S -- it gets
+     * in slots: lane SL0 + S (the first idle lane past the coordinates) mirrors dof d_S -- it gets
      * lane d_S's coefficients, so its velocity delta evolves bit for bit as lane d_S's -- and a
      * slot row reads it with a compile-time broadcast, so the sweep has no runtime branch (a
      * branch per pair measured slower than all 21 rows).  Same arithmetic as mrow: the result is
      * bitwise the all-rows solve's. */
     constexpr int KMAX = 1;
+    constexpr int SL0 = OBJ ? 13 : NJ;   /* first slot lane: the first lane past the coordinates */
     unsigned dmask = 0u;
-    float smcs[KMAX], swms[KMAX], srh[KMAX][2], slhi[KMAX], slam[KMAX][2];
+    float smcs[KMAX], swms[KMAX], swms2[KMAX], srh[KMAX][2], slhi[KMAX], slam[KMAX][2];
     auto srow = [&](auto sc, auto kc, float& resid) __attribute__((always_inline)) {
         constexpr int S = decltype(sc)::value, KIND = decltype(kc)::value;   /* 1 lower, 2 upper */
-        const float x = KIND == 2 ? srh[S][1] + bcast16<NJ + S>(gv) : srh[S][0] - bcast16<NJ + S>(gv);
+        const float x = KIND == 2 ? srh[S][1] + bcast16<SL0 + S>(gv) : srh[S][0] - bcast16<SL0 + S>(gv);
         const float delta = __builtin_amdgcn_fmed3f(x, -slam[S][KIND - 1], slhi[S] - slam[S][KIND - 1]);
         slam[S][KIND - 1] += delta;
         const float sd = KIND == 2 ? -delta : delta;
         gv += smcs[S] * sd;
         if constexpr (WROWS) gw += swms[S] * sd;
+        if constexpr (TWO) gw2 += swms2[S] * sd;
         resid = fmaxf(resid, fabsf(delta));
     };
     static_assert(limit_rows_paired(), "limit rows come as (lower, upper) pairs of one dof after the motor rows");
@@ -2053,7 +2074,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 constexpr int r = PGX_N_ROWS - 1 - decltype(i)::value;
                 if constexpr (MODE == 2 || (kPgxRowCode[r] >> 4) == 0) mrow(IC<r>{}, resid);
             });
-            if (CONT && (NW > 0 || (NW < 0 && any_contact))) contact_rows(nw_c, resid);
+            if (CONT && (OBJ || NW > 0 || (NW < 0 && any_contact))) contact_rows(nw_c, resid);
             PGX_PROF_SWEEP();
             if (resid <= m.residual_abs || it + 1 >= n_it) break;
             resid = 0.0f;
@@ -2069,7 +2090,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                     limit_check();
                 });
             }
-            if (CONT && (NW > 0 || (NW < 0 && any_contact))) contact_rows(nw_c, resid);
+            if (CONT && (OBJ || NW > 0 || (NW < 0 && any_contact))) contact_rows(nw_c, resid);
             PGX_PROF_SWEEP();
             if (resid <= m.residual_abs) break;
         }
@@ -2089,9 +2110,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     } else {
         PGX_PROF_COUNT(10, 1);
         init_limit_rows();
-        /* (not for the object tasks: a third copy of their 24-row sweep grows the kernel past
-         * the instruction cache -- Push measured 1.6 -> 2.4 ms) */
-        if (!OBJ && e.pgs_mode != 2) {
+        if (e.pgs_mode != 2) {
             float rl[NJ], ru[NJ];
 #pragma unroll
             for (int r = NJ; r < PGX_N_ROWS; r++) {
@@ -2099,8 +2118,8 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 if (kind == 1) rl[d] = rhs[r];
                 else ru[d] = rhs[r];
             }
-            rl_c = pick_arm(rl, -1.0f);
-            ru_c = pick_arm(ru, -1.0f);
+            rl_c = pick_arm(rl, -3.0e38f);   /* other lanes never flag (object coordinates) */
+            ru_c = pick_arm(ru, -3.0e38f);
             const bool spec_all = __all(far_nc);
             int nk = 0;
             if (!spec_all) {   /* partial: the dofs the motor bound cannot clear, in any env */
@@ -2108,13 +2127,13 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 dmask = __builtin_amdgcn_readfirstlane((unsigned)((bm | (bm >> 16) | (bm >> 32) | (bm >> 48)) & 0x7Fu));
                 nk = __builtin_popcount(dmask);
             }
-            const float gv0 = gv, gw0 = gw;
+            const float gv0 = gv, gw0 = gw, gw20 = gw2;
             float cl0[NPP];
 #pragma unroll
             for (int p = 0; p < NP; p++) cl0[p] = clam[p][0];
             if (PART && !spec_all && nk <= KMAX) {
                 PGX_PROF_COUNT(7, 1);
-                /* slots in the pairs' table order; slot lane NJ + S mirrors dof d_S */
+                /* slots in the pairs' table order; slot lane SL0 + S mirrors dof d_S */
                 int ds[2] = {0, 0};
                 int k = 0;
                 sfor<0, (PGX_N_ROWS - NJ) / 2>([&](auto pc) __attribute__((always_inline)) {
@@ -2125,8 +2144,8 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 ds[1] = __builtin_amdgcn_readfirstlane(ds[1]);
                 const int src = (int)(threadIdx.x & ~(unsigned)(GW - 1));
                 auto mirror = [&](float& x) __attribute__((always_inline)) {
-                    x = lane_sel<NJ>(__shfl(x, src + ds[0]), x);
-                    if (KMAX > 1 && nk > 1) x = lane_sel<NJ + 1>(__shfl(x, src + ds[1]), x);
+                    x = lane_sel<SL0>(__shfl(x, src + ds[0]), x);
+                    if (KMAX > 1 && nk > 1) x = lane_sel<SL0 + 1>(__shfl(x, src + ds[1]), x);
                 };
 #pragma unroll
                 for (int d = 0; d < NJ; d++) mirror(mcs[d]);
@@ -2140,7 +2159,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 /* the slots' row data: dof d_S's entries, selected with uniform masks */
 #pragma unroll
                 for (int S = 0; S < KMAX; S++) {
-                    smcs[S] = mcs[0]; swms[S] = wms[0]; slhi[S] = lhi[0];
+                    smcs[S] = mcs[0]; swms[S] = wms[0]; swms2[S] = wms2[0]; slhi[S] = lhi[0];
                     srh[S][0] = rl[0]; srh[S][1] = ru[0];
                     slam[S][0] = 0.0f; slam[S][1] = 0.0f;
                     sfor<1, NJ>([&](auto dc) __attribute__((always_inline)) {
@@ -2148,12 +2167,13 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                         const bool hit = ds[S] == d;   /* wave-uniform */
                         auto sel = [&](float a, float o) __attribute__((always_inline)) { return hit ? a : o; };
                         smcs[S] = sel(mcs[d], smcs[S]); swms[S] = sel(wms[d], swms[S]);
+                        swms2[S] = sel(wms2[d], swms2[S]);
                         slhi[S] = sel(lhi[d], slhi[S]);
                         srh[S][0] = sel(rl[d], srh[S][0]); srh[S][1] = sel(ru[d], srh[S][1]);
                     });
                 }
                 /* the checks skip the running dofs and the slot lanes */
-                if (((dmask >> c) & 1u) || (c >= NJ && c < NJ + nk)) { rl_c = -3.0e38f; ru_c = -3.0e38f; }
+                if ((dmask >> c) & 1u) { rl_c = -3.0e38f; ru_c = -3.0e38f; }
                 PGX_PROF_COUNT(16, nk == 2 ? 1 : 0);
                 PGX_PROF_COUNT(18, any_contact ? 1 : 0);
                 if (KMAX == 1 || nk == 1) solve_w(IC<3>{}, IC<1>{});
@@ -2167,6 +2187,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 PGX_PROF_COUNT(12, 1);
                 gv = gv0;
                 gw = gw0;
+                gw2 = gw20;
 #pragma unroll
                 for (int p = 0; p < NP; p++) {
                     clam[p][0] = cl0[p];
