@@ -50,4 +50,4 @@ def main(src=os.path.join(ROOT, "gpurun_out", "pmc"), round_tag="r01", num_envs=
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:2])
+    main(*sys.argv[1:3])
