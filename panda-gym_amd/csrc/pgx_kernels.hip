@@ -2995,7 +2995,7 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
 template <int CONTROL, int OBJ, int CONT, int AO, int WIDE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void step_kernel_o2(
     const PgxDevModel* __restrict__ mdev, PgxDevEnv e, PgxDevState s, const float* __restrict__ action, PgxDevOut o) {
-    step_body<CONTROL, OBJ, CONT, AO, WIDE, 0>(mdev, e, s, action, o);
+    step_body<CONTROL, OBJ, CONT, AO, WIDE, AO ? 0 : 1>(mdev, e, s, action, o);
 }
 
 template <int OBJ, int AO>

@@ -261,7 +261,7 @@ def test_speculative_limit_skip_is_exact(pg, monkeypatch, env_id):
 
 @pytest.mark.parametrize("env_id,contacts,n", [("PandaReach-v3", True, 4096), ("PandaReach-v3", False, 4096),
                                                ("PandaReach-v3", True, 8192), ("PandaReachAO-v3", True, 4096),
-                                               ("PandaPush-v3", True, 4096)])
+                                               ("PandaReachAO-v3", True, 8192), ("PandaPush-v3", True, 4096)])
 def test_partial_limit_rows_are_exact(pg, monkeypatch, env_id, contacts, n):
     """Waves holding an env near a joint limit solve with only that dof's limit pair (a slot
     lane mirrors the dof) and check the other pairs as the speculative solve does.  Under the
