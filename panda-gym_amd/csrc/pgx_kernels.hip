@@ -1051,15 +1051,32 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
     M3 Rc;
     if (OBJ) Rc = quat_mat(ob);
     if (CONT) { Lp->cnt[0][es] = 0; Lp->cnt[1][es] = 0; }
-    if (OBJ) { /* object vertices vs the box top under them */
+    if (OBJ) { /* object vertices vs the box top under them, lane v tests vertex v: the 4
+                * deepest by (depth, vertex) as g0_insert keeps them, in vertex (= id) order
+                * as sort_groups leaves them */
         const float h = e.obj_half;
-#pragma unroll
-        for (int vtx = 0; vtx < 8; vtx++) {
-            const V3 r = mul(Rc, v3((vtx & 1) ? h : -h, (vtx & 2) ? h : -h, (vtx & 4) ? h : -h));
-            const V3 P = ob.p + r;
-            const float d = P.z - ground_z(e, P.x, P.y);
-            if (d < m.contact_dist) g0_insert(*Lp, es, d, (float)vtx, r);
+        const int vtx = c & 7;
+        const V3 r = mul(Rc, v3((vtx & 1) ? h : -h, (vtx & 2) ? h : -h, (vtx & 4) ? h : -h));
+        const V3 P = ob.p + r;
+        const float d = P.z - ground_z(e, P.x, P.y);
+        const bool cand = c < 8 && d < m.contact_dist;
+        const float dd = cand ? d : 3.0e38f;
+        int rank = 0;
+        sfor<0, 8>([&](auto uc) __attribute__((always_inline)) {
+            constexpr int U = decltype(uc)::value;
+            const float du = bcast16<U>(dd);
+            rank += (du < dd || (du == dd && U < c)) ? 1 : 0;
+        });
+        const bool keep = cand && rank < CG;
+        const unsigned mk = row_ballot(keep);
+        const int sl = __builtin_popcount(mk & ((1u << (c & 15)) - 1u));
+        if (keep) {
+            Lp->g0d[sl][es] = d;
+            Lp->g0id[sl][es] = (float)vtx;
+            Lp->g0q[sl][0][es] = make_float4(r.x, r.y, r.z, 0.0f);
         }
+        Lp->cnt[0][es] = __builtin_popcount(mk);
+        PGX_PROF_MARK(19);
     }
     /* FK (redundant: constant-folded per link), capsule end points, and this lane's link */
     V3 (&z)[NJ] = D.z;
@@ -1096,8 +1113,29 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
         if constexpr (!OBJ) {
             robot_table_contacts_g(e, m.contact_dist, *Lp, es, c);
         } else {
-            robot_contacts<OBJ>(e, m.contact_dist, *Lp, es, ob, Rc);
-            sort_groups(*Lp, es);
+            PGX_PROF_MARK(20);
+            /* robot_contacts' object cull per capsule lane; without a capsule in reach of the
+             * object anywhere in the wave the robot group holds table candidates only, which
+             * robot_table_contacts_g finds lane-parallel (the same candidates, order and ids) */
+            const int cc = c < PGX_NCAP ? c : 0;
+            bool near = false;
+            if (c < PGX_NCAP && (kCapFlags[cc] & PGX_CAP_VS_OBJECT)) {
+                const V3 A = lds3(Lp->capA[cc], es), B = lds3(Lp->capB[cc], es);
+                const V3 ab = B - A;
+                const float l2 = dot(ab, ab);
+                float t = l2 > 0.0f ? dot(ob.p - A, ab) * fast_rcp(l2) : 0.0f;
+                t = fminf(fmaxf(t, 0.0f), 1.0f);
+                const V3 cp = A + t * ab - ob.p;
+                const float reach = kCapR[cc] + 1.7320508f * e.obj_half + m.contact_dist;
+                near = dot(cp, cp) < reach * reach;
+            }
+            if (__any(near)) {
+                robot_contacts<OBJ>(e, m.contact_dist, *Lp, es, ob, Rc);
+                PGX_PROF_MARK(21);
+                sort_groups(*Lp, es);
+            } else {
+                robot_table_contacts_g(e, m.contact_dist, *Lp, es, c);
+            }
         }
     }
     PGX_PROF_MARK(1);
