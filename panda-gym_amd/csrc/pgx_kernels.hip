@@ -34,9 +34,9 @@
 __device__ unsigned long long pgx_prof_counters[PGX_PROF_N];
 /* per wave of the last launch (block id): start / end s_memtime, sweeps, non-far, redo, all-rows */
 #define PGX_PROF_WAVES 16384
-__device__ unsigned long long pgx_prof_wave[PGX_PROF_WAVES][8];
+__device__ unsigned long long pgx_prof_wave[PGX_PROF_WAVES][10];
 extern "C" int pgx_prof_wave_read(unsigned long long* out, int n) {
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pgx_prof_wave), sizeof(unsigned long long) * 8 * (size_t)n);
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pgx_prof_wave), sizeof(unsigned long long) * 10 * (size_t)n);
 }
 extern "C" int pgx_prof_read(unsigned long long* out, int clear) {
     hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(pgx_prof_counters), sizeof(unsigned long long) * PGX_PROF_N);
@@ -2692,21 +2692,30 @@ __device__ __forceinline__ void ao_write_obs(float* dst, V3 pos, V3 vel, const f
 }
 
 /* whole-robot distance (every capsule) to a sphere (kind 0) / rounded cube (1) */
-template <class LT>
-__device__ __noinline__ float ao_robot_distance(LT& L, int ln, int kind, V3 C, float size) {
-    float best = 3.0e38f;
+/* Does the robot (the capsule set at the pose ao_caps left in LDS) come within thr of a sphere
+ * (kind 0) or a cuboid (kind 1) of half size `size` at C?  The reset's rejection tests
+ * (reach_ao.py get_distances(...) <= threshold): only the decision matters, so a capsule
+ * whose lower bound (axis distance - r - circumradius) already exceeds thr is skipped and the
+ * first capsule within thr decides.  PAR (wide layout): lane c tests capsule c, the row
+ * ballot ORs them. */
+template <bool PAR, class LT>
+__device__ __noinline__ bool ao_robot_hit(LT& L, int ln, int lane, int kind, V3 C, float size, float thr) {
     const V3 hc = v3(size, size, size);
-    for (int c = 0; c < PGX_NCAP; c++) {
-        const V3 A = lds3(L.capA[c], ln), B = lds3(L.capB[c], ln);
-        const float r = kCapR[c];
+    auto test = [&](int cp) __attribute__((always_inline)) {
+        const V3 A = lds3(L.capA[cp], ln), B = lds3(L.capB[cp], ln);
+        const float r = kCapR[cp];
         const float dc = norm(C - seg_closest(A, B, C)) - r;
-        float d;
-        if (kind == 0) d = dc - size;
-        else if (dc - 1.7320508f * size >= best) continue;
-        else d = capsule_box<false>(A, B, r, C, hc, nullptr);
-        best = fminf(best, d);
+        if (kind == 0) return dc - size <= thr;
+        if (dc - 1.7320508f * size > thr) return false;
+        return capsule_box<false>(A, B, r, C, hc, nullptr) <= thr;
+    };
+    if constexpr (PAR) {
+        return row_any(lane < PGX_NCAP && test(lane < PGX_NCAP ? lane : 0));
+    } else {
+        for (int cp = 0; cp < PGX_NCAP; cp++)
+            if (test(cp)) return true;
+        return false;
     }
-    return best;
 }
 
 struct AoDraw {
@@ -2733,8 +2742,8 @@ __device__ __noinline__ void ao_hollow_sphere(const PgxDevEnv& e, AoDraw& d, dou
 /* ReachAO.reset for reachao_rand (reach_ao.py:965-1082; oracle ao_reset_task): goal,
  * obstacles by rejection against robot / table / dummy sphere, 4-5 active.  Needs the
  * neutral-pose capsules in LDS; leaves the centres in L.aoC. */
-template <class LT>
-__device__ __noinline__ void ao_reset(const PgxDevEnv& e, LT& L, int ln, uint64_t env, uint32_t episode, V3 ee,
+template <bool PAR, class LT>
+__device__ __noinline__ void ao_reset(const PgxDevEnv& e, LT& L, int ln, int lane, uint64_t env, uint32_t episode, V3 ee,
                                       const double* inject_goal, const double* inject_obst, double* goal) {
     AoDraw d{env, episode, 0};
     const V3 tc = ao_table_c(e), th = ao_table_h(e);
@@ -2746,7 +2755,7 @@ __device__ __noinline__ void ao_reset(const PgxDevEnv& e, LT& L, int ln, uint64_
         const V3 g = v3((float)goal[0], (float)goal[1], (float)goal[2]);
         const bool coll = box_sd(g, tc, v3(th.x - kAoMargin, th.y - kAoMargin, th.z - kAoMargin)) - kAoMargin -
                                   kAoDummyR <= 0.1f ||
-                          ao_robot_distance(L, ln, 0, g, kAoDummyR) <= 0.1f;
+                          ao_robot_hit<PAR>(L, ln, lane, 0, g, kAoDummyR, 0.1f);
         if (!coll) break;
     }
     const V3 dm = v3((float)dummy[0], (float)dummy[1], (float)dummy[2]);
@@ -2769,7 +2778,7 @@ __device__ __noinline__ void ao_reset(const PgxDevEnv& e, LT& L, int ln, uint64_
                 ddum = box_sd(dm, Pf, v3(kAoSize - kAoMargin, kAoSize - kAoMargin, kAoSize - kAoMargin)) - kAoMargin -
                        kAoDummyR;
             }
-            const bool coll = dtab <= 0.03f || ddum <= 0.03f || ao_robot_distance(L, ln, o < 3 ? 0 : 1, Pf, kAoSize) <= 0.03f;
+            const bool coll = dtab <= 0.03f || ddum <= 0.03f || ao_robot_hit<PAR>(L, ln, lane, o < 3 ? 0 : 1, Pf, kAoSize, 0.03f);
             if (!coll) break;
         }
         L.aoC[o][0][ln] = (float)P[0]; L.aoC[o][1][ln] = (float)P[1]; L.aoC[o][2][ln] = (float)P[2];
@@ -2966,7 +2975,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
             for (int j = 0; j < NJ; j++) { q[j] = mr.neutral_q[j]; qd[j] = 0.0f; }
             ee_state(mr, q, qd, pos, vel);
             ao_caps(mr, q, *L, ln);
-            ao_reset(e, *L, ln, e.env_id_offset + (uint64_t)i, episode, pos, nullptr, nullptr, goal);
+            ao_reset<WIDE != 0>(e, *L, ln, c, e.env_id_offset + (uint64_t)i, episode, pos, nullptr, nullptr, goal);
             episode += 1;
             if constexpr (WIDE) ao_link_obs_g(*L, ln, c);
             else ao_link_obs(*L, ln);
@@ -3013,7 +3022,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
         if (blockIdx.x < PGX_PROF_WAVES) {
             unsigned long long* w = pgx_prof_wave[blockIdx.x];
             w[0] = prof_t0; w[1] = g_prof_t; w[2] = g_prof[8]; w[3] = g_prof[10]; w[4] = g_prof[12]; w[5] = g_prof[13];
-            w[6] = g_prof[7]; w[7] = g_prof[4];
+            w[6] = g_prof[7]; w[7] = g_prof[4]; w[8] = g_prof[1]; w[9] = g_prof[6];
         }
     }
 #endif
@@ -3062,7 +3071,7 @@ __global__ __launch_bounds__(64) void reset_kernel(const PgxDevModel* __restrict
         for (int j = 0; j < NJ; j++) { q[j] = m.neutral_q[j]; qd[j] = 0.0f; }
         ee_state(m, q, qd, pos, vel);
         ao_caps(m, q, *L, ln);
-        ao_reset(e, *L, ln, e.env_id_offset + (uint64_t)i, episode, pos,
+        ao_reset<false>(e, *L, ln, 0, e.env_id_offset + (uint64_t)i, episode, pos,
                  inject_goal ? inject_goal + 3 * (size_t)i : nullptr,
                  inject_obj ? inject_obj + 3 * AO_N * (size_t)i : nullptr, goal);
         episode += 1;

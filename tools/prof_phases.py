@@ -38,10 +38,10 @@ def run(env_id, n, contacts, launches=100, warm=50):
     lib.pgx_prof_read(buf, 1)
     wide = venv._cfg.lanes_per_env == 16 or (venv._cfg.lanes_per_env == 0 and n <= 8192)
     waves = n // (4 if wide else 64)
-    wv = (C.c_ulonglong * (8 * waves))()
+    wv = (C.c_ulonglong * (10 * waves))()
     lib.pgx_prof_wave_read(wv, waves)
     import numpy as np
-    w = np.frombuffer(wv, dtype=np.uint64).reshape(waves, 8).astype(np.int64)
+    w = np.frombuffer(wv, dtype=np.uint64).reshape(waves, 10).astype(np.int64)
     dur = w[:, 1] - w[:, 0]
     start = w[:, 0] - w[:, 0].min()
     end = w[:, 1] - w[:, 0].min()
@@ -54,7 +54,9 @@ def run(env_id, n, contacts, launches=100, warm=50):
                   "redo_mean": float(w[:, 4].mean()), "redo_top1pct": float(w[top, 4].mean()),
                   "allrows_mean": float(w[:, 5].mean()), "allrows_top1pct": float(w[top, 5].mean()),
                   "partial_mean": float(w[:, 6].mean()), "partial_top1pct": float(w[top, 6].mean()),
-                  "pgs_cyc_mean": float(w[:, 7].mean()), "pgs_cyc_top1pct": float(w[top, 7].mean())}
+                  "pgs_cyc_mean": float(w[:, 7].mean()), "pgs_cyc_top1pct": float(w[top, 7].mean()),
+                  "detect_cyc_mean": float(w[:, 8].mean()), "detect_cyc_top1pct": float(w[top, 8].mean()),
+                  "epilogue_cyc_mean": float(w[:, 9].mean()), "epilogue_cyc_top1pct": float(w[top, 9].mean())}
     per = [buf[k] / (waves * launches) for k in range(24)]
     tot = sum(per[:7]) + per[14] + per[15]
     out = {"env_id": env_id, "n": n, "contacts": contacts, "ms_per_step": ms,
