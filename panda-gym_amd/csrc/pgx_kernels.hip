@@ -2495,6 +2495,48 @@ __device__ __forceinline__ float capsule_box(V3 A, V3 B, float r, V3 c, V3 hf, V
     return d;
 }
 
+/* capsule_box(...) <= thr as a decision: the same golden-section search, stopped as soon as a
+ * sample is within r + margin of the inner box (the minimum can only be lower) or the best
+ * sample minus |AB| times the bracket width (f is |AB|-Lipschitz in t; the minimiser stays in
+ * the bracket of a convex f) is farther than that (the minimum cannot reach it); the
+ * undecided rest ends as capsule_box does. */
+__device__ __forceinline__ bool capsule_box_hit(V3 A, V3 B, float r, V3 c, V3 hf, float thr = 0.0f) {
+    const V3 h = v3(hf.x - kAoMargin, hf.y - kAoMargin, hf.z - kAoMargin);
+    const V3 ab = B - A;
+    const float lim = kAoMargin + r + thr;
+    if (!(dot(ab, ab) > 0.0f)) return box_sd(A, c, h) - kAoMargin - r <= thr;
+    const float len = norm(ab);
+    const float gr = 0.61803398875f;
+    float lo = 0.0f, hi = 1.0f;
+    float t1 = hi - gr * (hi - lo), t2 = lo + gr * (hi - lo);
+    float f1 = box_sd(A + t1 * ab, c, h), f2 = box_sd(A + t2 * ab, c, h);
+    for (int it = 0; it < 34; it++) {
+        const float fb = fminf(f1, f2);
+        if (fb <= lim) return true;
+        if (fb - len * (hi - lo) > lim) return false;
+        if (f1 <= f2) {
+            hi = t2; t2 = t1; f2 = f1;
+            t1 = hi - gr * (hi - lo);
+            f1 = box_sd(A + t1 * ab, c, h);
+        } else {
+            lo = t1; t1 = t2; f1 = f2;
+            t2 = lo + gr * (hi - lo);
+            f2 = box_sd(A + t2 * ab, c, h);
+        }
+    }
+    V3 P = A + 0.5f * (lo + hi) * ab;
+    float sd = box_sd(P, c, h);
+    if (sd > 0.0f) {
+        for (int it = 0; it < 2; it++) {
+            const V3 q = v3(fminf(fmaxf(P.x, c.x - h.x), c.x + h.x), fminf(fmaxf(P.y, c.y - h.y), c.y + h.y),
+                            fminf(fmaxf(P.z, c.z - h.z), c.z + h.z));
+            P = seg_closest(A, B, q);
+        }
+        sd = box_sd(P, c, h);
+    }
+    return sd - kAoMargin - r <= thr;
+}
+
 /* world end points of every capsule at q (base capsule included) into LDS */
 template <int C = 0, class LT>
 __device__ __forceinline__ void ao_caps_walk(const Chain& k, MRef m, LT& L, int ln) {
@@ -2540,12 +2582,12 @@ __device__ __forceinline__ bool ao_collided(const PgxDevEnv& e, LT& L, int ln) {
             const V3 P = seg_closest(A, B, C);
             const float dc = norm(C - P) - r;
             if (o < 3) hit = hit || dc - kAoSize <= 0.0f;
-            else if (dc - kAoCubeBound <= 0.0f) hit = hit || capsule_box<false>(A, B, r, C, hcube, nullptr) <= 0.0f;
+            else if (dc - kAoCubeBound <= 0.0f) hit = hit || capsule_box_hit(A, B, r, C, hcube);
         }
         if (slot >= 1) {
             /* box_sd is 1-Lipschitz: min over the segment >= min(ends) - |AB| / 2 */
             const float lb = fminf(box_sd(A, tc, thi), box_sd(B, tc, thi)) - 0.5f * norm(B - A) - kAoMargin - r;
-            if (lb <= 0.0f) hit = hit || capsule_box<false>(A, B, r, tc, th, nullptr) <= 0.0f;
+            if (lb <= 0.0f) hit = hit || capsule_box_hit(A, B, r, tc, th);
         }
     }
     return hit;
@@ -2611,11 +2653,11 @@ __device__ __forceinline__ bool ao_collided_g(const PgxDevEnv& e, LT& L, int es,
             const V3 P = seg_closest(A, B, C);
             const float dc = norm(C - P) - r;
             if (o < 3) hit = hit || dc - kAoSize <= 0.0f;
-            else if (dc - kAoCubeBound <= 0.0f) hit = hit || capsule_box<false>(A, B, r, C, hcube, nullptr) <= 0.0f;
+            else if (dc - kAoCubeBound <= 0.0f) hit = hit || capsule_box_hit(A, B, r, C, hcube);
         }
         if (slot >= 1) {
             const float lb = fminf(box_sd(A, tc, thi), box_sd(B, tc, thi)) - 0.5f * norm(B - A) - kAoMargin - r;
-            if (lb <= 0.0f) hit = hit || capsule_box<false>(A, B, r, tc, th, nullptr) <= 0.0f;
+            if (lb <= 0.0f) hit = hit || capsule_box_hit(A, B, r, tc, th);
         }
     }
     return row_any(hit);
@@ -2707,7 +2749,7 @@ __device__ __noinline__ bool ao_robot_hit(LT& L, int ln, int lane, int kind, V3 
         const float dc = norm(C - seg_closest(A, B, C)) - r;
         if (kind == 0) return dc - size <= thr;
         if (dc - 1.7320508f * size > thr) return false;
-        return capsule_box<false>(A, B, r, C, hc, nullptr) <= thr;
+        return capsule_box_hit(A, B, r, C, hc, thr);
     };
     if constexpr (PAR) {
         return row_any(lane < PGX_NCAP && test(lane < PGX_NCAP ? lane : 0));
