@@ -17,7 +17,7 @@ from panda_gym_amd import _native  # noqa: E402
 NAMES = ["prologue+IK", "FK+detect", "dynamics", "row setup", "PGS sweeps", "integrate", "epilogue"]
 
 
-def run(env_id, n, contacts, launches=100, warm=50):
+def run(env_id, n, contacts, launches=100, warm=26):
     lib = _native.load()
     buf = (C.c_ulonglong * 24)()
     venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=0, contacts=contacts)
