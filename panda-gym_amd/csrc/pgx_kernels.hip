@@ -577,6 +577,21 @@ __device__ __forceinline__ void g1_insert(LT& L, int ln, float d, float id, int 
     L.g1n[pos][0][ln] = n.x; L.g1n[pos][1][ln] = n.y; L.g1n[pos][2][ln] = n.z;
     L.g1rb[pos][0][ln] = rb.x; L.g1rb[pos][1][ln] = rb.y; L.g1rb[pos][2][ln] = rb.z;
 }
+/* group 1 by depth (stable insertion sort of <= 4 entries) */
+template <class LT>
+__device__ __forceinline__ void sort_g1_by_depth(LT& L, int ln) {
+    const int c1 = L.cnt[1][ln];
+    for (int i = 1; i < c1; i++)
+        for (int j = i; j > 0 && L.g1d[j][ln] < L.g1d[j - 1][ln]; j--) {
+            float d = L.g1d[j][ln], id = L.g1id[j][ln];
+            int jj = L.g1j[j][ln];
+            float p[3], n[3], rb[3];
+            for (int k = 0; k < 3; k++) { p[k] = L.g1p[j][k][ln]; n[k] = L.g1n[j][k][ln]; rb[k] = L.g1rb[j][k][ln]; }
+            g1_copy(L, ln, j, j - 1);
+            L.g1d[j - 1][ln] = d; L.g1id[j - 1][ln] = id; L.g1j[j - 1][ln] = jj;
+            for (int k = 0; k < 3; k++) { L.g1p[j - 1][k][ln] = p[k]; L.g1n[j - 1][k][ln] = n[k]; L.g1rb[j - 1][k][ln] = rb[k]; }
+        }
+}
 /* rows are ordered by feature id (insertion sort of <= 4 entries, via a spare slot-free swap) */
 template <class LT>
 __device__ __forceinline__ void sort_groups(LT& L, int ln) {
@@ -612,6 +627,59 @@ __device__ __forceinline__ V3 mul_t(const M3& A, V3 v) {
               A.m[2] * v.x + A.m[5] * v.y + A.m[8] * v.z);
 }
 
+/* capsule c's spheres against the object (robot_contacts' object branch): the cull (segment
+ * farther from the object centre than r + h sqrt(3) + tau) unless the caller already did it */
+template <class LT>
+__device__ __forceinline__ void object_candidates(const PgxDevEnv& e, float tau, LT& L, int ln, const ObjState& ob,
+                                                  const M3& Rc, int c, bool cull) {
+    const V3 A = v3(L.capA[c][0][ln], L.capA[c][1][ln], L.capA[c][2][ln]);
+    const V3 B = v3(L.capB[c][0][ln], L.capB[c][1][ln], L.capB[c][2][ln]);
+    const float r = kCapR[c];
+    const int jc = kCapJ[c], ns = kCapNs[c];
+    const float h = e.obj_half;
+    const V3 ab = B - A;
+    if (cull) {
+        const float l2 = dot(ab, ab);
+        float t = l2 > 0.0f ? dot(ob.p - A, ab) * fast_rcp(l2) : 0.0f;
+        t = fminf(fmaxf(t, 0.0f), 1.0f);
+        const V3 cp = A + t * ab - ob.p;
+        const float reach = r + 1.7320508f * h + tau;
+        if (!(dot(cp, cp) < reach * reach)) return;
+    }
+    const float inv_n = ns > 1 ? 1.0f / (float)(ns - 1) : 0.0f;
+    for (int s = 0; s < ns; s++) {
+        const V3 C = A + ((float)s * inv_n) * ab;
+        const V3 cl = mul_t(Rc, C - ob.p);
+        V3 qb = v3(fminf(fmaxf(cl.x, -h), h), fminf(fmaxf(cl.y, -h), h), fminf(fmaxf(cl.z, -h), h));
+        const V3 diff = cl - qb;
+        const float d2 = dot(diff, diff);
+        V3 nl;
+        float depth;
+        if (d2 > 1e-24f) {
+            const float dist = fast_sqrt(d2);
+            nl = fast_rcp(dist) * diff;
+            depth = dist - r;
+        } else { /* centre inside the box: out through the nearest face */
+            const float bx = h - fabsf(cl.x), by = h - fabsf(cl.y), bz = h - fabsf(cl.z);
+            int ax = 0;
+            float best = bx;
+            if (by < best) { best = by; ax = 1; }
+            if (bz < best) { best = bz; ax = 2; }
+            const float sx = cl.x < 0.0f ? -1.0f : 1.0f, sy = cl.y < 0.0f ? -1.0f : 1.0f,
+                        sz = cl.z < 0.0f ? -1.0f : 1.0f;
+            nl = v3(ax == 0 ? sx : 0.0f, ax == 1 ? sy : 0.0f, ax == 2 ? sz : 0.0f);
+            if (ax == 0) qb.x = sx * h;
+            if (ax == 1) qb.y = sy * h;
+            if (ax == 2) qb.z = sz * h;
+            depth = -best - r;
+        }
+        if (depth < tau) {
+            const V3 n = mul(Rc, nl);
+            g1_insert(L, ln, depth, (float)(32 + 16 * c + s), jc, C - r * n, n, mul(Rc, qb));
+        }
+    }
+}
+
 /* Robot capsules against the table/plane (end spheres) and the object (spheres sampled
  * along the axis), from the world end points the FK pass left in LDS.  A runtime loop
  * over the capsule table (wave-uniform index: scalar loads) keeps the code compact. */
@@ -632,50 +700,7 @@ __device__ __forceinline__ void robot_contacts(const PgxDevEnv& e, float tau, LT
                                        v3(0.0f, 0.0f, 0.0f));
             }
         }
-        if (OBJ && (flags & PGX_CAP_VS_OBJECT)) {
-            const float h = e.obj_half;
-            /* cull: segment farther from the object centre than r + h*sqrt(3) + tau */
-            const V3 ab = B - A;
-            const float l2 = dot(ab, ab);
-            float t = l2 > 0.0f ? dot(ob.p - A, ab) * fast_rcp(l2) : 0.0f;
-            t = fminf(fmaxf(t, 0.0f), 1.0f);
-            const V3 cp = A + t * ab - ob.p;
-            const float reach = r + 1.7320508f * h + tau;
-            if (dot(cp, cp) < reach * reach) {
-                const float inv_n = ns > 1 ? 1.0f / (float)(ns - 1) : 0.0f;
-                for (int s = 0; s < ns; s++) {
-                    const V3 C = A + ((float)s * inv_n) * ab;
-                    const V3 cl = mul_t(Rc, C - ob.p);
-                    V3 qb = v3(fminf(fmaxf(cl.x, -h), h), fminf(fmaxf(cl.y, -h), h), fminf(fmaxf(cl.z, -h), h));
-                    const V3 diff = cl - qb;
-                    const float d2 = dot(diff, diff);
-                    V3 nl;
-                    float depth;
-                    if (d2 > 1e-24f) {
-                        const float dist = fast_sqrt(d2);
-                        nl = fast_rcp(dist) * diff;
-                        depth = dist - r;
-                    } else { /* centre inside the box: out through the nearest face */
-                        const float bx = h - fabsf(cl.x), by = h - fabsf(cl.y), bz = h - fabsf(cl.z);
-                        int ax = 0;
-                        float best = bx;
-                        if (by < best) { best = by; ax = 1; }
-                        if (bz < best) { best = bz; ax = 2; }
-                        const float sx = cl.x < 0.0f ? -1.0f : 1.0f, sy = cl.y < 0.0f ? -1.0f : 1.0f,
-                                    sz = cl.z < 0.0f ? -1.0f : 1.0f;
-                        nl = v3(ax == 0 ? sx : 0.0f, ax == 1 ? sy : 0.0f, ax == 2 ? sz : 0.0f);
-                        if (ax == 0) qb.x = sx * h;
-                        if (ax == 1) qb.y = sy * h;
-                        if (ax == 2) qb.z = sz * h;
-                        depth = -best - r;
-                    }
-                    if (depth < tau) {
-                        const V3 n = mul(Rc, nl);
-                        g1_insert(L, ln, depth, (float)(32 + 16 * c + s), jc, C - r * n, n, mul(Rc, qb));
-                    }
-                }
-            }
-        }
+        if (OBJ && (flags & PGX_CAP_VS_OBJECT)) object_candidates(e, tau, L, ln, ob, Rc, c, true);
     }
 }
 
@@ -1129,12 +1154,24 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                 const float reach = kCapR[cc] + 1.7320508f * e.obj_half + m.contact_dist;
                 near = dot(cp, cp) < reach * reach;
             }
-            if (__any(near)) {
-                robot_contacts<OBJ>(e, m.contact_dist, *Lp, es, ob, Rc);
+            /* table candidates lane-parallel (id-ordered, so re-sorted by depth: ids grow with
+             * discovery among them), then the near capsules' object spheres inserted by depth
+             * (g1_insert), then id order; only exact depth ties between a table and an object
+             * candidate could order differently from robot_contacts' discovery order */
+            robot_table_contacts_g(e, m.contact_dist, *Lp, es, c);
+            const uint64_t bn = __ballot(near);
+            unsigned wm = (unsigned)((bn | (bn >> 16) | (bn >> 32) | (bn >> 48)) & 0xFFFFu);
+            if (wm) {
+                const unsigned rm = row_ballot(near);
+                sort_g1_by_depth(*Lp, es);
+                wm = __builtin_amdgcn_readfirstlane(wm);
+                while (wm) {
+                    const int cn = __builtin_ctz(wm);
+                    wm &= wm - 1u;
+                    if ((rm >> cn) & 1u) object_candidates(e, m.contact_dist, *Lp, es, ob, Rc, cn, false);
+                }
                 PGX_PROF_MARK(21);
                 sort_groups(*Lp, es);
-            } else {
-                robot_table_contacts_g(e, m.contact_dist, *Lp, es, c);
             }
         }
     }
