@@ -425,6 +425,7 @@ __device__ __forceinline__ void ik(MPtr mp, const float* q0, V3 target, const fl
     const float residual = mp->ik_residual;
     for (int it = 0; it < max_iters; it++) {
         if (!(diff > residual)) break;
+        PGX_PROF_COUNT(17, 1);
         MRef m = *fresh(mp);
         Chain k;
         fk_chain<PAR>(m, qs, k);

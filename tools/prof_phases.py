@@ -68,6 +68,7 @@ def run(env_id, n, contacts, launches=100, warm=26):
            "speculation_redo_frac": per[12] / max(per[9], 1e-9), "partial_frac": per[7] / max(per[9], 1e-9),
            "partial_k2_frac": per[16] / max(per[7], 1e-9), "partial_contact_frac": per[18] / max(per[7], 1e-9), "all_rows_frac": per[13] / max(per[9], 1e-9),
            "cycles_per_sweep": per[4] / max(per[8], 1e-9), "last_launch_waves": wave_stats,
+           "ik_iterations_per_wave_step": per[17],
            "detect_split": {"g0_vertices": round(per[19]), "fk": round(per[20]), "robot_contacts": round(per[21])},
            "dynamics_split": {"newton_euler": round(per[14]), "crba_cholesky": round(per[15]),
                               "minv_and_rest": round(per[2])}}
