@@ -2102,9 +2102,11 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
      * oracle under the random policy) is solved again from the same start with the limit
      * rows.  Otherwise all 21 joint rows run. */
     float rl_c = -1.0f, ru_c = -1.0f;
-    bool viol = false;
+    /* the smallest margin seen, min(gv - rl, -(ru + gv)): a row would compute x' > 0 (a
+     * violation) exactly when its margin is negative; one v_min3 per check, no compare */
+    float lmargin = 3.0e38f;
     auto limit_check = [&]() __attribute__((always_inline)) {
-        viol = viol || (rl_c - gv > 0.0f) || (ru_c + gv > 0.0f);
+        lmargin = fminf(lmargin, fminf(gv - rl_c, -(ru_c + gv)));
     };
     /* MODE 3 (partial, arm tasks): the limit pairs of the dofs the motor-impulse bound cannot
      * clear in some env of the wave (dmask, at most 2 of them) run, the others are checked as in
@@ -2257,8 +2259,9 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             } else if (spec_all) {
                 solve_w(IC<1>{}, IC<0>{});
             } else {
-                viol = true;   /* more than KMAX dofs: all rows */
+                lmargin = -1.0f;   /* more than KMAX dofs: all rows */
             }
+            const bool viol = lmargin < 0.0f;
             if (__any(row_any(viol)) || e.pgs_mode == 3) {
                 PGX_PROF_COUNT(12, 1);
                 gv = gv0;
