@@ -4,10 +4,12 @@ Writes profiles/pmc_step_kernel.json (read by bench.py for roofline.traffic and
 roofline_valu) and copies the per-pass CSVs under profiles/<round>/pmc/.
 
 Units: FETCH_SIZE / WRITE_SIZE are KB per dispatch (TCC_EA0_RDREQ/WRREQ based).
-MI355X_MICROARCH.md §HBM: FETCH_SIZE reads 1/2 of the bytes of *16-B-per-lane*
-streaming loads on gfx950; the step kernel's loads are 4-B (dword) per lane,
-for which the guide has no calibration, so the raw value is reported as is
-(`fetch_correction` = 1) and the write side is exact for dword stores.
+MI355X_MICROARCH.md §HBM: FETCH_SIZE reads 1/2 of the bytes of 16-B-per-lane streaming
+loads on gfx950 and other widths are uncalibrated there.  tools/calib (profiles/r02/calib)
+calibrates the widths and the pattern of the step kernel: dword, dwordx2 and 16-B streaming
+copies of 512 MiB and the step kernel's SoA pattern (4 envs per wave, one dword per row from
+the lead lane, XCD block mapping, 40 rows x 4096 envs, repeated launches) all report FETCH_SIZE
+= 1/2 of the bytes read and WRITE_SIZE = the bytes written, so `fetch_correction` = 2.
 """
 import csv
 import glob
@@ -35,8 +37,11 @@ def main(src=os.path.join(ROOT, "gpurun_out", "pmc"), round_tag="r01", num_envs=
         "valu_lane_ops_per_launch": mean.get("SQ_INSTS_VALU", 0.0) * 64,
         "valu_instr_per_env_step": mean.get("SQ_INSTS_VALU", 0.0) * 64 / num_envs,
         "salu_instr_per_wave": mean.get("SQ_INSTS_SALU", 0.0) / waves if waves else None,
-        "fetch_kb": mean.get("FETCH_SIZE"), "write_kb": mean.get("WRITE_SIZE"), "fetch_correction": 1.0,
-        "hbm_bytes_per_launch": (mean.get("FETCH_SIZE", 0.0) + mean.get("WRITE_SIZE", 0.0)) * 1024.0,
+        "fetch_kb": mean.get("FETCH_SIZE"), "write_kb": mean.get("WRITE_SIZE"), "fetch_correction": 2.0,
+        "fetch_correction_source": "profiles/r02/calib (tools/calib/run.sh)",
+        "hbm_bytes_per_launch": (2.0 * mean.get("FETCH_SIZE", 0.0) + mean.get("WRITE_SIZE", 0.0)) * 1024.0,
+        "read_bytes_per_launch": 2.0 * mean.get("FETCH_SIZE", 0.0) * 1024.0,
+        "write_bytes_per_launch": mean.get("WRITE_SIZE", 0.0) * 1024.0,
         "alg_bytes_per_launch": 199.0 * num_envs,
         "source": "tools/profile_pmc.sh (rocprofv3 --pmc, one counter group per run) on MI355X",
     }
