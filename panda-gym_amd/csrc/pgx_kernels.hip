@@ -1600,6 +1600,10 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
      * loop body holds one even (reverse) and one odd (forward) sweep, so no value has to
      * be merged from two branch arms (that cost ~35 v_mov per sweep). */
     const int n_it = m.num_iterations;
+    /* the exit threshold in an SGPR before the sweeps: read from the model inside the loop it
+     * costs a scalar load and its s_waitcnt on every sweep */
+    float res_thr = m.residual_abs;
+    asm("" : "+s"(res_thr));
     PGX_PROF_MARK(3);
     PGX_PROF_COUNT(9, 1);
     PGX_PROF_SWEEPS_DECL;
@@ -1611,14 +1615,14 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
                 if ((kPgxRowCode[r] >> 4) == 0) row(r, resid);
             if (CONT && any_contact) contact_rows(resid);
             PGX_PROF_SWEEP();
-            if (resid <= m.residual_abs || it + 1 >= n_it) break;
+            if (resid <= res_thr || it + 1 >= n_it) break;
             resid = 0.0f;
 #pragma unroll
             for (int r = 0; r < PGX_N_ROWS; r++)
                 if ((kPgxRowCode[r] >> 4) == 0) row(r, resid);
             if (CONT && any_contact) contact_rows(resid);
             PGX_PROF_SWEEP();
-            if (resid <= m.residual_abs) break;
+            if (resid <= res_thr) break;
         }
     } else {
         PGX_PROF_COUNT(10, 1);
@@ -1629,13 +1633,13 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
             for (int r = PGX_N_ROWS - 1; r >= 0; r--) row(r, resid);
             if (CONT && any_contact) contact_rows(resid);
             PGX_PROF_SWEEP();
-            if (resid <= m.residual_abs || it + 1 >= n_it) break;
+            if (resid <= res_thr || it + 1 >= n_it) break;
             resid = 0.0f;
 #pragma unroll
             for (int r = 0; r < PGX_N_ROWS; r++) row(r, resid);
             if (CONT && any_contact) contact_rows(resid);
             PGX_PROF_SWEEP();
-            if (resid <= m.residual_abs) break;
+            if (resid <= res_thr) break;
         }
     }
 #undef MINV
@@ -2089,6 +2093,10 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     };
     const bool any_contact = CONT && __any(n0 > 0 || n1 > 0);
     const int n_it = m.num_iterations;
+    /* the exit threshold in an SGPR before the sweeps: read from the model inside the loop it
+     * costs a scalar load and its s_waitcnt on every sweep */
+    float res_thr = m.residual_abs;
+    asm("" : "+s"(res_thr));
     PGX_PROF_MARK(3);
     PGX_PROF_COUNT(9, 1);
     PGX_PROF_SWEEPS_DECL;
@@ -2154,7 +2162,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             });
             if (CONT && (OBJ || NW > 0 || (NW < 0 && any_contact))) contact_rows(nw_c, resid);
             PGX_PROF_SWEEP();
-            if (resid <= m.residual_abs || it + 1 >= n_it) break;
+            if (resid <= res_thr || it + 1 >= n_it) break;
             resid = 0.0f;
             sfor<0, PGX_N_ROWS>([&](auto i) __attribute__((always_inline)) {
                 constexpr int r = decltype(i)::value;
@@ -2170,7 +2178,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             }
             if (CONT && (OBJ || NW > 0 || (NW < 0 && any_contact))) contact_rows(nw_c, resid);
             PGX_PROF_SWEEP();
-            if (resid <= m.residual_abs) break;
+            if (resid <= res_thr) break;
         }
     };
     /* Reach: the robot point count fixed at compile time (above) for every mode but far */
