@@ -2067,10 +2067,11 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     n1w = __builtin_amdgcn_readfirstlane(n1w);
     const bool g0_any = CONT && OBJ && __any(n0 > 0);
     const bool g1_any = CONT && __any(n1 > 0);
-    /* NW (Reach, WROWS): the robot points the sweep runs, a compile-time count chosen per wave
-     * outside the sweep loop (2 or 4, n1w rounded up): the rows of points n1w..NW-1 are idle
-     * (bounds [lambda', lambda'] with lambda' = 0 -> delta' = 0, bit for bit), so no per-point
-     * branch sits inside the sweep.  NW < 0: the per-point branches (rare all-rows solve). */
+    /* NW: the robot points the sweep runs, a compile-time count chosen per wave outside the
+     * sweep loop (0, 2 or 4, n1w rounded up): the rows of points n1w..NW-1 are idle (bounds
+     * [lambda', lambda'] with lambda' = 0 -> delta' = 0, bit for bit), so no per-point branch
+     * sits inside the sweep.  The object-scene rows (P0 points, a resting cube has 4) run in
+     * every sweep of the object tasks, idle points predicated the same way. */
     auto contact_rows = [&](auto nw_c, float& resid) __attribute__((always_inline)) {
         constexpr int NW = decltype(nw_c)::value;
 #pragma unroll
@@ -2181,7 +2182,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             if (resid <= res_thr) break;
         }
     };
-    /* Reach: the robot point count fixed at compile time (above) for every mode but far */
+    /* the robot point count fixed at compile time (above) for every mode but far */
     auto solve_w = [&](auto mode_c, auto k_c) __attribute__((always_inline)) {
         if constexpr (WROWS) {
             if (n1w == 0) solve(mode_c, IC<0>{}, k_c);
@@ -2191,8 +2192,8 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             solve(mode_c, IC<-1>{}, k_c);
         }
     };
-    if (__all(far)) {   /* (Reach: far implies no robot point in the wave) */
-        solve(IC<0>{}, IC<WROWS ? 0 : -1>{}, IC<0>{});
+    if (__all(far)) {   /* (far implies no robot point in the wave) */
+        solve(IC<0>{}, IC<0>{}, IC<0>{});
     } else {
         PGX_PROF_COUNT(10, 1);
         init_limit_rows();
