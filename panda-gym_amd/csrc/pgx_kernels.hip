@@ -2126,7 +2126,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
      * slot row reads it with a compile-time broadcast, so the sweep has no runtime branch (a
      * branch per pair measured slower than all 21 rows).  Same arithmetic as mrow: the result is
      * bitwise the all-rows solve's. */
-    constexpr int KMAX = 1;
+    constexpr int KMAX = CONT ? 1 : 2;   /* two slots measured -1.2 % without the table, +1 % with it */
     constexpr int SL0 = OBJ ? 13 : NJ;   /* first slot lane: the first lane past the coordinates */
     unsigned dmask = 0u;
     float smcs[KMAX], swms[KMAX], swms2[KMAX], srh[KMAX][2], slhi[KMAX], slam[KMAX][2];
