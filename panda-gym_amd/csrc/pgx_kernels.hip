@@ -1818,6 +1818,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         }
     }
 
+    PGX_PROF_MARK(22);
     /* ---- contact-row velocities in lanes.  Lane q = 3 point + dir holds w_q = J_q.dv (register
      * gw; the object tasks' rows 16..23 in a second register gw2, lanes 0..7) and the Delassus
      * entries W[q][s] = J_q M^-1 J_s^T of every row s (Wm: motor / limit rows of dof d,
@@ -1901,6 +1902,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             if constexpr (TWO) build(IC<1>{}, Wm2, Wc2, gw2);
         }
     }
+    PGX_PROF_MARK(23);
 
     /* ---- motor / limit rows (as substep()): per row rhs and lambda, per dof jinv / den */
     float den[NJ], jinv[NJ];

@@ -58,7 +58,7 @@ def run(env_id, n, contacts, launches=100, warm=26):
                   "detect_cyc_mean": float(w[:, 8].mean()), "detect_cyc_top1pct": float(w[top, 8].mean()),
                   "epilogue_cyc_mean": float(w[:, 9].mean()), "epilogue_cyc_top1pct": float(w[top, 9].mean())}
     per = [buf[k] / (waves * launches) for k in range(24)]
-    tot = sum(per[:7]) + per[14] + per[15]
+    tot = sum(per[:7]) + per[14] + per[15] + sum(per[19:24])
     out = {"env_id": env_id, "n": n, "contacts": contacts, "ms_per_step": ms,
            "cycles_per_wave_step": tot, "clock_ghz_est": tot / (ms * 1e6),
            "phases": {NAMES[k]: round(per[k]) for k in range(7)},
@@ -70,6 +70,8 @@ def run(env_id, n, contacts, launches=100, warm=26):
            "cycles_per_sweep": per[4] / max(per[8], 1e-9), "last_launch_waves": wave_stats,
            "ik_iterations_per_wave_step": per[17],
            "detect_split": {"g0_vertices": round(per[19]), "fk": round(per[20]), "robot_contacts": round(per[21])},
+           "row_setup_split": {"contact_points": round(per[22]), "delassus_lanes": round(per[23]),
+                               "joint_rows": round(per[3])},
            "dynamics_split": {"newton_euler": round(per[14]), "crba_cholesky": round(per[15]),
                               "minv_and_rest": round(per[2])}}
     venv.close()
