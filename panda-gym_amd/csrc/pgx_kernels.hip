@@ -1899,7 +1899,9 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 gwr = w;
             };
             build(IC<0>{}, Wm, Wc, gw);
-            if constexpr (TWO) build(IC<1>{}, Wm2, Wc2, gw2);
+            /* rows 16..23 belong to robot points 1..3 (slots fill from 0): idle in every env of
+             * the wave while point 1 is, and an idle row reads 0 (bounds [0, 0]) */
+            if constexpr (TWO) { if (g1k_any[1]) build(IC<1>{}, Wm2, Wc2, gw2); }
         }
     }
     PGX_PROF_MARK(23);
