@@ -193,6 +193,30 @@ def task_leg(dev, env_id: str, n: int, steps: int, contacts: bool = True):
             "policy": "device Philox random actions (sample_actions + step per step)"}
 
 
+def host_path_leg(dev, env_id: str, n: int, steps: int):
+    """The SB3-facing path (PCIe-inclusive, never ``value``): numpy actions in through
+    ``step_async`` (pinned H2D), ``step_wait`` returns numpy obs / rewards / dones and the
+    per-env infos list SB3's VecEnv protocol requires (D2H of every output + Python dicts).
+    The actions are drawn on the host by numpy, as a policy's would arrive."""
+    import panda_gym_amd as pg
+
+    venv = pg.PandaVecEnv(env_id, num_envs=n, device=dev, seed=2)
+    venv.reset()
+    rng = np.random.default_rng(0)
+    acts = rng.uniform(-1.0, 1.0, (steps + 10, n, venv.action_dim)).astype(np.float32)
+    for t in range(10):
+        venv.step(acts[t])
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for t in range(steps):
+        venv.step(acts[10 + t])
+    el = time.perf_counter() - t0
+    venv.close()
+    return {"env_id": env_id, "envs": n, "value": n * steps / el, "unit": "env-steps/s",
+            "ms_per_step": el / steps * 1e3, "steps": steps,
+            "path": "VecEnv.step_async/step_wait with numpy in and out (pinned H2D / D2H, SB3 infos list)"}
+
+
 def sharded_leg(dev, env_id: str, n: int, steps: int, warmup: int, dist, rank: int, world: int):
     """Every rank steps its own shard of ``n`` envs (global ids [rank*n, (rank+1)*n)); the timed
     region is barrier-bracketed and the max over ranks is taken, like the headline leg.  Used for
@@ -354,6 +378,7 @@ def main():
             line["tasks"] = [task_leg(dev, "PandaPush-v3", 4096, args.task_steps),               # configs[2]
                              task_leg(dev, "PandaPickAndPlace-v3", 16384, args.task_steps),      # configs[3]
                              task_leg(dev, args.env_id, E, args.task_steps, contacts=False)]     # no table
+            line["sb3_host_path"] = host_path_leg(dev, args.env_id, E, 100)
         print(json.dumps(line), flush=True)
     venv.close()
     if dist is not None:

@@ -308,29 +308,69 @@ class PandaVecEnv:
         self._pending_seed = seed
         return [None if seed is None else seed + i for i in range(self.num_envs)]
 
+    def _host_stage(self):
+        """Pinned host mirrors of the step outputs (allocated on first use): the SB3 path
+        copies every output with one async DMA each on the env's stream and waits once,
+        instead of a blocking pageable copy (and a stream sync) per tensor."""
+        if getattr(self, "_hs", None) is None:
+            n, od, ad = self.num_envs, self.obs_dim, self.action_dim
+            pin = dict(dtype=torch.float32, pin_memory=True)
+            self._hs = {
+                "act": torch.empty((n, ad), **pin), "act_dev": torch.empty((n, ad), dtype=torch.float32,
+                                                                           device=self.device),
+                "observation": torch.empty((n, od), **pin), "achieved_goal": torch.empty((n, 3), **pin),
+                "desired_goal": torch.empty((n, 3), **pin), "reward": torch.empty(n, **pin),
+                "flags": torch.empty((3, n), dtype=torch.uint8, pin_memory=True),
+                "flags_dev": torch.empty((3, n), dtype=torch.uint8, device=self.device),
+                "t_observation": torch.empty((n, od), **pin), "t_achieved_goal": torch.empty((n, 3), **pin),
+                "t_desired_goal": torch.empty((n, 3), **pin),
+            }
+        return self._hs
+
     def step_async(self, actions) -> None:
-        self._pending = torch.as_tensor(np.asarray(actions, dtype=np.float32) if not torch.is_tensor(actions)
-                                        else actions)
+        if torch.is_tensor(actions) and actions.device == self.device:
+            self._pending = actions
+            return
+        hs = self._host_stage()
+        a = np.asarray(actions.cpu() if torch.is_tensor(actions) else actions, dtype=np.float32)
+        if a.shape != (self.num_envs, self.action_dim):
+            raise ValueError(f"actions must be [{self.num_envs}, {self.action_dim}], got {a.shape}")
+        # the previous step's H2D copy has completed: step_wait synchronised the stream
+        hs["act"].numpy()[...] = a
+        hs["act_dev"].copy_(hs["act"], non_blocking=True)
+        self._pending = hs["act_dev"]
 
     def step_wait(self):
+        """SB3 VecEnv.step_wait: (obs dict, rewards, dones, infos) as numpy, with auto-reset
+        ``terminal_observation`` / ``TimeLimit.truncated`` infos (SB3 DummyVecEnv semantics).
+        Host-facing path: PCIe-inclusive (bench.py ``sb3_host_path`` times it)."""
         obs, rew, term, trunc, succ = self.step_tensors(self._pending)
         self._pending = None
-        dones = (term | trunc).bool()
-        o = self._numpy_obs()
-        r = rew.cpu().numpy()
-        d = dones.cpu().numpy()
-        tr = trunc.bool().cpu().numpy()
-        te = term.bool().cpu().numpy()
-        sc = succ.bool().cpu().numpy()
+        hs = self._host_stage()
+        stream = torch.cuda.current_stream(self.device)
+        fd = hs["flags_dev"]
+        fd[0].copy_(term)
+        fd[1].copy_(trunc)
+        fd[2].copy_(succ)
+        for k, src in (("observation", obs["observation"]), ("achieved_goal", obs["achieved_goal"]),
+                       ("desired_goal", obs["desired_goal"]), ("reward", rew), ("flags", fd),
+                       ("t_observation", self.terminal_obs), ("t_achieved_goal", self.terminal_ag),
+                       ("t_desired_goal", self.terminal_dg)):
+            hs[k].copy_(src, non_blocking=True)
+        stream.synchronize()
+        # copies: the pinned mirrors are overwritten by the next step
+        o = {k: hs[k].numpy().copy() for k in ("observation", "achieved_goal", "desired_goal")}
+        r = hs["reward"].numpy().copy()
+        fl = hs["flags"].numpy() != 0
+        te, tr, sc = fl[0].copy(), fl[1].copy(), fl[2]
+        d = te | tr
         col = self.task_truncated(r)
-        infos: List[Dict[str, Any]] = [{"is_success": bool(sc[i]), "is_truncated": bool(col[i])}
-                                       for i in range(self.num_envs)]
+        infos: List[Dict[str, Any]] = [{"is_success": s, "is_truncated": c}
+                                       for s, c in zip(sc.tolist(), np.broadcast_to(col, sc.shape).tolist())]
         idx = np.nonzero(d)[0]
         if len(idx):
-            tobs = self.terminal_obs.cpu().numpy()
-            tag = self.terminal_ag.cpu().numpy()
-            tdg = self.terminal_dg.cpu().numpy()
-            for i in idx:
+            tobs, tag, tdg = hs["t_observation"].numpy(), hs["t_achieved_goal"].numpy(), hs["t_desired_goal"].numpy()
+            for i in idx.tolist():
                 infos[i]["terminal_observation"] = {"observation": tobs[i].copy(), "achieved_goal": tag[i].copy(),
                                                     "desired_goal": tdg[i].copy()}
                 infos[i]["TimeLimit.truncated"] = bool(tr[i] and not te[i])

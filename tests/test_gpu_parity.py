@@ -237,6 +237,39 @@ def test_sb3_vecenv_protocol(pg):
     venv.close()
 
 
+@pytest.mark.parametrize("env_id", ["PandaReach-v3", "PandaPush-v3"])
+def test_sb3_host_path_matches_device_path(pg, env_id):
+    """step_async/step_wait (pinned staging, one sync) returns exactly the device path's
+    outputs, including the terminal observations of the auto-reset at the time limit."""
+    n, T = 64, 7
+    a_env = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=5, max_episode_steps=3)
+    b_env = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=5, max_episode_steps=3)
+    a_env.reset_tensors()
+    b_env.reset()
+    rng = np.random.default_rng(1)
+    for t in range(T):
+        act = rng.uniform(-1, 1, (n, a_env.action_dim)).astype(np.float32)
+        obs, rew, term, trunc, succ = a_env.step_tensors(torch.as_tensor(act, device="cuda:0"))
+        want = {k: v.cpu().numpy() for k, v in obs.items()}
+        done = (term | trunc).bool().cpu().numpy()
+        tobs = a_env.terminal_obs.cpu().numpy()
+        o, r, d, infos = b_env.step(act)
+        for k in want:
+            assert np.array_equal(o[k], want[k]), (t, k)
+        assert np.array_equal(r, rew.cpu().numpy())
+        assert np.array_equal(d, done)
+        assert [i["is_success"] for i in infos] == succ.bool().cpu().tolist()
+        for i in np.nonzero(done)[0]:
+            assert np.array_equal(infos[i]["terminal_observation"]["observation"], tobs[i])
+            assert infos[i]["TimeLimit.truncated"] is True
+        assert done.any() == ((t + 1) % 3 == 0)
+    # device actions go straight through step_async
+    o, *_ = b_env.step(torch.zeros((n, b_env.action_dim), device="cuda:0"))
+    assert o["observation"].shape == (n, b_env.obs_dim)
+    a_env.close()
+    b_env.close()
+
+
 def test_vecenv_seed_applies_to_next_reset(pg):
     """SB3 protocol: VecEnv.seed(s) then reset() seeds env i with s + i (as reset(seed=s))."""
     venv = pg.PandaVecEnv("PandaReach-v3", num_envs=8, device="cuda:0")
