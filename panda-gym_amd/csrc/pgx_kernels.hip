@@ -513,6 +513,8 @@ struct ContactLdsT {
     /* wide layout: the contact rows' J (13 coordinates) and M^-1 J^T (arm part) per env,
      * row-major [row q][coordinate], so lane q reads its row back with ds_read_b128 (a transpose) */
     float4 wJ[W == 64 ? 1 : W][6 * CG][4], wR[W == 64 ? 1 : W][6 * CG][2];
+    /* one-lane speculative solve: the sweep's start velocities (dv, dvl, dvw) for a redo */
+    float spec0[W == 64 ? NJ + 6 : 1][W == 64 ? W : 1];
 };
 using ContactLds = ContactLdsT<64>;   /* one env per lane */
 using ContactLdsG = ContactLdsT<EPW>;
@@ -1487,7 +1489,7 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
      * during the sweep (by induction), every evaluation of them clamps to delta = 0,
      * and dropping them changes no bit of the result or of the exit iteration.  Robot
      * contact impulses are unbounded, so the skip needs an env without robot contacts. */
-    bool far = n1 == 0;
+    bool far_nc = true;   /* the motor-impulse bound alone keeps every limit row idle */
 #pragma unroll
     for (int d = 0; d < NJ; d++) {
         float B = 0.0f;
@@ -1495,8 +1497,10 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
         for (int k = 0; k < NJ; k++) B += fabsf(MINV(d, k)) * m.max_impulse[k];
         B = B * 1.001f + 1e-6f;
         const float penl = q[d] - kLower[d], penu = kUpper[d] - q[d];
-        far = far && penl > 0.0f && penu > 0.0f && (vu[d] - B) > -penl * m.inv_dt && (vu[d] + B) < penu * m.inv_dt;
+        far_nc = far_nc && penl > 0.0f && penu > 0.0f && (vu[d] - B) > -penl * m.inv_dt &&
+                 (vu[d] + B) < penu * m.inv_dt;
     }
+    const bool far = far_nc && n1 == 0;
     /* resolveSingleConstraintRowGeneric, branch-free: clamp the accumulated impulse,
      * apply the clamped delta through the unit response M^-1 J^T (a column of M^-1). */
     auto row = [&](const int r, float& resid) {
@@ -1627,7 +1631,75 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
     } else {
         PGX_PROF_COUNT(10, 1);
         init_limit_rows();
-        for (int it = 0; it < n_it; it += 2) {
+        /* Speculative solve (as substep_g's MODE 1): when the motor-impulse bound alone keeps
+         * every limit row idle in every env of the wave (only robot-contact impulses, which
+         * are unbounded, stand in the way of the far solve), sweep without the 14 limit rows
+         * and check, at each position the limit block takes in the order (the head of the
+         * reversed sweep, after the motor rows of the forward one), that each of them would
+         * compute delta = fma(-v, jinv, rhs) <= 0 there: with lambda = 0 that row clamps to
+         * 0 and leaves dv, lambda and the residual bit for bit unchanged, and a block of
+         * no-ops leaves dv constant across it, so one check per position covers all 14.  A
+         * wave where any env fails is solved again from the same start with every row. */
+        bool redo = true;
+        if (CONT && e.pgs_mode != 2 && __all(far_nc)) {
+            float rl[NJ], ru[NJ];
+#pragma unroll
+            for (int r = NJ; r < PGX_N_ROWS; r++) {
+                const int kind = kPgxRowCode[r] >> 4, d = kPgxRowCode[r] & 15;
+                if (kind == 1) rl[d] = rhs[r];
+                else ru[d] = rhs[r];
+            }
+            ContactLds& L = *Lp;
+#pragma unroll
+            for (int j = 0; j < NJ; j++) L.spec0[j][ln] = dv[j];
+            L.spec0[NJ][ln] = dvl.x; L.spec0[NJ + 1][ln] = dvl.y; L.spec0[NJ + 2][ln] = dvl.z;
+            L.spec0[NJ + 3][ln] = dvw.x; L.spec0[NJ + 4][ln] = dvw.y; L.spec0[NJ + 5][ln] = dvw.z;
+            /* the smallest -delta seen: a limit row would act exactly when it is negative */
+            float lmargin = 3.0e38f;
+            auto limit_check = [&]() {
+#pragma unroll
+                for (int d = 0; d < NJ; d++)
+                    lmargin = fminf(lmargin, fminf(-fmaf(-dv[d], jinv[d], rl[d]), -fmaf(dv[d], jinv[d], ru[d])));
+            };
+            for (int it = 0; it < n_it; it += 2) {
+                float resid = 0.0f;
+                limit_check();
+#pragma unroll
+                for (int r = PGX_N_ROWS - 1; r >= 0; r--)
+                    if ((kPgxRowCode[r] >> 4) == 0) row(r, resid);
+                if (CONT && any_contact) contact_rows(resid);
+                PGX_PROF_SWEEP();
+                if (resid <= res_thr || it + 1 >= n_it) break;
+                resid = 0.0f;
+#pragma unroll
+                for (int r = 0; r < PGX_N_ROWS; r++)
+                    if ((kPgxRowCode[r] >> 4) == 0) row(r, resid);
+                limit_check();
+                if (CONT && any_contact) contact_rows(resid);
+                PGX_PROF_SWEEP();
+                if (resid <= res_thr) break;
+            }
+            redo = __any(lmargin < 0.0f) || e.pgs_mode == 3;
+            if (redo) {   /* back to the start: velocities, impulses (warm starts from the records) */
+                PGX_PROF_COUNT(12, 1);
+#pragma unroll
+                for (int j = 0; j < NJ; j++) dv[j] = L.spec0[j][ln];
+                dvl = v3(L.spec0[NJ][ln], L.spec0[NJ + 1][ln], L.spec0[NJ + 2][ln]);
+                dvw = v3(L.spec0[NJ + 3][ln], L.spec0[NJ + 4][ln], L.spec0[NJ + 5][ln]);
+#pragma unroll
+                for (int r = 0; r < PGX_N_ROWS; r++) lam[r] = 0.0f;
+#pragma unroll
+                for (int k = 0; k < CG; k++)
+#pragma unroll
+                    for (int dir = 0; dir < 3; dir++) {
+                        lam0[k][dir] = (CONT && OBJ && k < n0) ? L.g0q[k][1 + dir][ln].w : 0.0f;
+                        lam1[k][dir] = (CONT && k < n1) ? L.g1q[k][dir][5][ln].w : 0.0f;
+                    }
+            }
+        } else {
+            PGX_PROF_COUNT(13, 1);
+        }
+        for (int it = 0; redo && it < n_it; it += 2) {
             float resid = 0.0f;
 #pragma unroll
             for (int r = PGX_N_ROWS - 1; r >= 0; r--) row(r, resid);

@@ -233,22 +233,24 @@ def test_layouts_agree_per_step(pg, env_id):
     b.close()
 
 
-@pytest.mark.parametrize("env_id", ["PandaReach-v3", "PandaPush-v3"])
-def test_speculative_limit_skip_is_exact(pg, monkeypatch, env_id):
-    """substep_g solves contact substeps without the joint-limit rows when the motor-impulse
-    bound alone keeps them idle, checks at every limit-block position that they would have
-    computed a zero impulse, and redoes the solve with them otherwise.  The claim is bit-exact
-    equality with the all-rows solve: compared here against PGX_PGS_MODE=2 (never speculate)
-    and PGX_PGS_MODE=3 (always redo), on table-contact Reach and Push steps from the same states."""
+@pytest.mark.parametrize("env_id,lanes", [("PandaReach-v3", 16), ("PandaPush-v3", 16), ("PandaReach-v3", 1),
+                                          ("PandaPush-v3", 1), ("PandaPickAndPlace-v3", 1)])
+def test_speculative_limit_skip_is_exact(pg, monkeypatch, env_id, lanes):
+    """Both layouts (substep_g, substep) solve contact substeps without the joint-limit rows
+    when the motor-impulse bound alone keeps them idle, check at every limit-block position
+    that they would have computed a zero impulse, and redo the solve with them otherwise.  The
+    claim is bit-exact equality with the all-rows solve: compared here against PGX_PGS_MODE=2
+    (never speculate) and PGX_PGS_MODE=3 (always redo), on table-contact steps from the same
+    states."""
     n = 256
     runs = {}
     for mode in ("0", "2", "3"):
         monkeypatch.setenv("PGX_PGS_MODE", mode)
-        v = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=9, lanes_per_env=16)
+        v = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=9, lanes_per_env=lanes)
         v.reset_tensors(seed=9)
         outs = []
         for t in range(25):
-            a = torch.zeros((n, 3), device="cuda:0")
+            a = torch.zeros((n, v.action_dim), device="cuda:0")
             a[:, 2] = -1.0                          # press the tool bar onto the table
             a[:, :2] = v.sample_actions(t)[:, :2]
             v.step_tensors(a)
@@ -257,6 +259,24 @@ def test_speculative_limit_skip_is_exact(pg, monkeypatch, env_id):
         v.close()
     assert np.array_equal(runs["0"], runs["2"])
     assert np.array_equal(runs["0"], runs["3"])
+
+
+@pytest.mark.parametrize("env_id,n", [("PandaPickAndPlace-v3", 16384), ("PandaReach-v3", 16384)])
+def test_one_lane_speculative_solve_exact_at_full_size(pg, monkeypatch, env_id, n):
+    """The one-lane layout's speculative limit-row solve at its benchmark batch, random policy:
+    every step bit-identical to the all-rows solve (PGX_PGS_MODE=2)."""
+    runs = {}
+    for mode in ("0", "2"):
+        monkeypatch.setenv("PGX_PGS_MODE", mode)
+        v = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=4, lanes_per_env=1)
+        v.reset_tensors()
+        outs = []
+        for t in range(12):
+            v.step_tensors(v.sample_actions(t))
+            outs.append(torch.cat([v.obs, v.state()["qd"].T], 1).cpu().numpy().copy())
+        runs[mode] = np.stack(outs)
+        v.close()
+    assert np.array_equal(runs["0"], runs["2"])
 
 
 @pytest.mark.parametrize("env_id,contacts,n", [("PandaReach-v3", True, 4096), ("PandaReach-v3", False, 4096),
