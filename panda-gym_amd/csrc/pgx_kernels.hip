@@ -1544,19 +1544,25 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
                         const float ln_n = lam0[k][0];
 #pragma unroll
                         for (int dir = fr ? 1 : 0; dir < (fr ? 3 : 1); dir++) {
-                            const V3 lin = dir == 0 ? v3(0, 0, 1) : (dir == 1 ? v3(0, -1, 0) : v3(1, 0, 0));
-                            const V3 ang = dir == 0 ? v3(r.y, -r.x, 0) : (dir == 1 ? v3(r.z, 0, -r.x) : v3(0, r.z, -r.y));
+                            /* u = +z, -y, +x and ang = r x u written out by component: as V3 products
+                             * the zero entries would cost an fma each (x + s * 0 does not fold) */
                             const float4 rw = L.g0q[k][1 + dir][ln];
                             const float jv = rw.x, dn = rw.y, rh = rw.z, lm = lam0[k][dir];
                             const float lo = fr ? -mu * ln_n : 0.0f;
                             const float hi = fr ? mu * ln_n : 1e10f;
-                            float delta = rh - (dot(lin, dvl) + dot(ang, dvw)) * jv;
+                            float jdv;
+                            if (dir == 0) jdv = dvl.z + (r.y * dvw.x - r.x * dvw.y);
+                            else if (dir == 1) jdv = (r.z * dvw.x - r.x * dvw.z) - dvl.y;
+                            else jdv = dvl.x + (r.z * dvw.y - r.y * dvw.z);
+                            float delta = rh - jdv * jv;
                             const float nl = __builtin_amdgcn_fmed3f(lm + delta, lo, hi);
                             /* a friction row waits for a positive normal impulse */
                             delta = (!act || (fr && !(ln_n > 0.0f))) ? 0.0f : nl - lm;
                             lam0[k][dir] = lm + delta;
-                            dvl = dvl + (delta * inv_m) * lin;
-                            dvw = dvw + (delta * inv_i) * ang;
+                            const float sm = delta * inv_m, si = delta * inv_i;
+                            if (dir == 0) { dvl.z += sm; dvw.x += si * r.y; dvw.y -= si * r.x; }
+                            else if (dir == 1) { dvl.y -= sm; dvw.x += si * r.z; dvw.z -= si * r.x; }
+                            else { dvl.x += sm; dvw.y += si * r.z; dvw.z -= si * r.y; }
                             resid = fmaxf(resid, fabsf(delta * dn));
                         }
                     }
