@@ -336,12 +336,12 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     e.terminate_on_success = cfg->terminate_on_success ? 1 : 0;
     e.no_auto_reset = cfg->no_auto_reset ? 1 : 0;
     e.collision_reward = cfg->collision_reward;
-    /* Step layout (pgx_kernels.hip): 16 lanes per env up to 8192 envs (4096 x 16 lanes = 1024
-     * waves = one per SIMD; at 8192, two), one lane per env beyond, where the one-lane waves
-     * fill enough SIMDs (tools/time_layouts.py, profiles/r01/time_layouts_v11.json: Reach at
-     * 8192 envs 1.21 ms wide vs 1.32 one-lane, PickAndPlace 2.99 vs 3.52; at 16384 the
-     * one-lane layout wins, 1.33 vs 2.27 and 3.54 vs 5.49).  cfg->lanes_per_env (0 = this
-     * rule, 1, 16) chooses; PGX_LANES_PER_ENV=1|16 overrides both (A/B timing). */
+    /* Step layout (pgx_kernels.hip): 16 lanes per env (4096 x 16 lanes = 1024 waves = one per
+     * SIMD; beyond, several per SIMD) or one lane per env.  Round 1 measured the one-lane layout
+     * ahead at 16384 envs (profiles/r01/time_layouts_v11.json: 1.33 vs 2.27 ms Reach, 3.54 vs
+     * 5.49 PickAndPlace); the round-2 wide kernels reversed that for the contact tasks (below).
+     * cfg->lanes_per_env (0 = this rule, 1, 16) chooses; PGX_LANES_PER_ENV=1|16 overrides both
+     * (A/B timing). */
     if (cfg->lanes_per_env != 0 && cfg->lanes_per_env != 1 && cfg->lanes_per_env != 16) {
         delete h;
         return fail(PGX_E_INVALID, "lanes_per_env must be 0, 1 or 16, got %d", cfg->lanes_per_env);
@@ -349,8 +349,14 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     /* test hook for the exactness of the speculative limit-row skip (substep_g) */
     e.pgs_mode = 0;
     if (const char* pm = std::getenv("PGX_PGS_MODE")) e.pgs_mode = std::atoi(pm);
+    /* Round-2 measurements (tools/time_layouts.py, profiles/r02/time_layouts_r02.json): with
+     * contacts the wide layout now wins at every batch -- Reach 16384 0.99 vs 1.29 ms, 65536
+     * 3.43 vs 4.78; ReachAO 16384 0.78 vs 1.19; PickAndPlace 16384 3.10 vs 3.29 -- so it is
+     * the default there; without contacts (Reach's contact-free kernel) the two layouts tie
+     * beyond 8192 envs (16384: 0.56 vs 0.54 ms) and the one-lane layout stays. */
     const int wide_max = 8192;
-    e.lanes_per_env = cfg->lanes_per_env ? cfg->lanes_per_env : (cfg->n_envs <= wide_max ? 16 : 1);
+    e.lanes_per_env = cfg->lanes_per_env ? cfg->lanes_per_env
+                                         : ((cfg->n_envs <= wide_max || cfg->contacts) ? 16 : 1);
     if (const char* lpe = std::getenv("PGX_LANES_PER_ENV")) {
         const int v = std::atoi(lpe);
         if (v != 1 && v != 16) { delete h; return fail(PGX_E_INVALID, "PGX_LANES_PER_ENV must be 1 or 16, got %s", lpe); }

@@ -146,7 +146,7 @@ class PandaVecEnv:
     ``lanes_per_env`` picks the kernel layout (results agree to fp32 rounding): 16 gives
     each env a 16-lane DPP row (the solver's coordinates split over the lanes; fastest
     while the batch is too small to fill the chip one lane per env), 1 one env per lane,
-    0 (default) chooses by batch size (16 up to 8192 envs)."""
+    0 (default) chooses: 16 with contacts at every batch size, and up to 8192 envs without)."""
 
     def __init__(self, env_id: str = "PandaReach-v3", num_envs: int = 4096, device: Any = "cuda:0", seed: int = 0,
                  env_id_offset: int = 0, max_episode_steps: Optional[int] = None, auto_reset: bool = True,

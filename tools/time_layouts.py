@@ -36,6 +36,8 @@ def run(env_id, n, contacts, launches):
 
 if __name__ == "__main__":
     launches = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+    if os.environ.get("TL_CASES"):   # e.g. TL_CASES="PandaReach-v3:16384:1,PandaPush-v3:16384:1"
+        CASES = [(a, int(b), bool(int(c))) for a, b, c in (x.split(":") for x in os.environ["TL_CASES"].split(","))]
     for env_id, n, contacts in CASES:
         row = {"env_id": env_id, "n": n, "contacts": contacts}
         for lanes in (16, 1):
