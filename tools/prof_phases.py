@@ -36,7 +36,8 @@ def run(env_id, n, contacts, launches=100, warm=26):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / launches
     lib.pgx_prof_read(buf, 1)
-    wide = venv._cfg.lanes_per_env == 16 or (venv._cfg.lanes_per_env == 0 and n <= 8192)
+    # libpgx's default rule (pgx_api.cpp): 16 lanes with contacts at any batch, else up to 8192 envs
+    wide = venv._cfg.lanes_per_env == 16 or (venv._cfg.lanes_per_env == 0 and (n <= 8192 or contacts))
     waves = n // (4 if wide else 64)
     wv = (C.c_ulonglong * (10 * waves))()
     lib.pgx_prof_wave_read(wv, waves)
