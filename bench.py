@@ -29,6 +29,24 @@ HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (8.0 TB/s spec
 VALU_PEAK_TFLOPS = 157.3         # FP32 vector peak (spec)
 ALG_BYTES_PER_ENV_STEP = 199.0   # read 84 + write 115 B per Reach env-step
 PROFILE_JSON = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
+# algorithmic FLOPs per env-step, op-counted in the oracle and frozen (oracle/count_flops.py)
+FLOPS_JSON = os.path.join(ROOT, "tests", "golden", "flops_per_env_step.json")
+
+
+def alg_flops() -> dict:
+    """config key -> algorithmic FLOPs per env-step (tests/golden/flops_per_env_step.json)."""
+    with open(FLOPS_JSON) as f:
+        doc = json.load(f)
+    return {k: v["flops_per_env_step"] for k, v in doc["configs"].items()}
+
+
+def valu_roofline(key: str, env_steps_per_s: float, what: str) -> dict:
+    """rate x algorithmic FLOPs per env-step / the FP32 vector peak."""
+    fl = alg_flops()[key]
+    ach = env_steps_per_s * fl / 1e12
+    return {"bound": "valu", "achieved": ach, "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / VALU_PEAK_TFLOPS,
+            "alg_flops_per_env_step": fl, "rate": what,
+            "source": os.path.relpath(FLOPS_JSON, ROOT) + f" [{key}] (fp64 oracle op-count, oracle/count_flops.py)"}
 
 
 def parse():
@@ -48,6 +66,9 @@ def parse():
     ap.add_argument("--task-steps", type=int, default=200)
     ap.add_argument("--no-ao", action="store_true", help="skip the sharded ReachAO leg (configs[4])")
     ap.add_argument("--ao-envs", type=int, default=8192, help="ReachAO envs per GPU (65536 over 8 GPUs)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group for N > 1 (gloo: collective tensors on the host, so several ranks "
+                         "can share one GPU for a rehearsal of the multi-GPU path)")
     return ap.parse_args()
 
 
@@ -169,7 +190,7 @@ def her_leg(dev, calls: int, with_cpu: bool):
     return res
 
 
-def task_leg(dev, env_id: str, n: int, steps: int, contacts: bool = True):
+def task_leg(dev, env_id: str, n: int, steps: int, contacts: bool = True, flops_key: str = ""):
     """env-steps/s of one more task config on this GPU (device random policy, in-kernel
     auto-reset), timed like the main leg: barrier-free single GPU, HIP events bracketing."""
     import panda_gym_amd as pg
@@ -188,9 +209,12 @@ def task_leg(dev, env_id: str, n: int, steps: int, contacts: bool = True):
     torch.cuda.synchronize(dev)
     ms = e0.elapsed_time(e1) / steps
     venv.close()
-    return {"env_id": env_id, "envs": n, "contacts": contacts, "value": n / (ms * 1e-3), "unit": "env-steps/s",
-            "ms_per_step": ms, "steps": steps,
-            "policy": "device Philox random actions (sample_actions + step per step)"}
+    res = {"env_id": env_id, "envs": n, "contacts": contacts, "value": n / (ms * 1e-3), "unit": "env-steps/s",
+           "ms_per_step": ms, "steps": steps,
+           "policy": "device Philox random actions (sample_actions + step per step)"}
+    if flops_key:
+        res["roofline_valu"] = valu_roofline(flops_key, res["value"], "env-steps/s of this leg (sample + step)")
+    return res
 
 
 def host_path_leg(dev, env_id: str, n: int, steps: int):
@@ -217,7 +241,22 @@ def host_path_leg(dev, env_id: str, n: int, steps: int):
             "path": "VecEnv.step_async/step_wait with numpy in and out (pinned H2D / D2H, SB3 infos list)"}
 
 
-def sharded_leg(dev, env_id: str, n: int, steps: int, warmup: int, dist, rank: int, world: int):
+def state_digest(venv, dist, world: int) -> str:
+    """sha256 over every env's final observation bits in global env order: per env the sum of the
+    int32 views of its obs row (order-independent and exact), gathered from every rank.  A sharded
+    run and one handle holding all the envs give the same digest iff they agree env for env."""
+    import hashlib
+
+    per_env = venv.obs.contiguous().view(torch.int32).to(torch.int64).sum(1).cpu()
+    if dist is not None and world > 1:
+        parts = [None] * world
+        dist.all_gather_object(parts, per_env.numpy())
+        per_env = torch.from_numpy(np.concatenate(parts))
+    return hashlib.sha256(per_env.numpy().astype("<i8").tobytes()).hexdigest()
+
+
+def sharded_leg(dev, env_id: str, n: int, steps: int, warmup: int, dist, rank: int, world: int,
+                coll_dev=None):
     """Every rank steps its own shard of ``n`` envs (global ids [rank*n, (rank+1)*n)); the timed
     region is barrier-bracketed and the max over ranks is taken, like the headline leg.  Used for
     BASELINE configs[4] (ReachAO, 65536 envs as 8192 per GPU on 8 GPUs)."""
@@ -240,12 +279,16 @@ def sharded_leg(dev, env_id: str, n: int, steps: int, warmup: int, dist, rank: i
         venv.step_tensors(venv.sample_actions())
     torch.cuda.synchronize(dev)
     barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0, dist, dev)
+    elapsed = max_over_ranks(time.perf_counter() - t0, dist, coll_dev)
+    digest = state_digest(venv, dist, world)
     venv.close()
+    value = world * n * steps / elapsed
     return {"env_id": env_id, "envs_per_gpu": n, "global_envs": world * n, "n_gpus": world,
-            "value": world * n * steps / elapsed, "unit": "env-steps/s", "ms_per_step": elapsed / steps * 1e3,
+            "value": value, "unit": "env-steps/s", "ms_per_step": elapsed / steps * 1e3,
             "steps": steps, "warmup": warmup, "scaling": "weak",
-            "policy": "device Philox random actions, in-kernel collision / success / TimeLimit auto-reset"}
+            "policy": "device Philox random actions, in-kernel collision / success / TimeLimit auto-reset",
+            "obs_digest": digest,
+            "roofline_valu": valu_roofline("reach_ao", value / world, "env-steps/s per GPU of this leg")}
 
 
 def launch_ranks(n: int) -> int:
@@ -273,13 +316,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # gloo rehearsal on one box: ranks share the GPUs there are (device_count does not initialise HIP)
+    local_dev = local if args.dist_backend == "nccl" else local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(local_dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
+        else:
+            dist.init_process_group("gloo")
+    dev = torch.device("cuda", local_dev)
     torch.cuda.set_device(dev)
+    coll_dev = dev if args.dist_backend == "nccl" else None   # where the collective tensors live
 
     import panda_gym_amd as pg
     from panda_gym_amd.shard import gather_stats, max_over_ranks, shard_offset
@@ -302,10 +351,10 @@ def main():
         venv.step_tensors(venv.sample_actions())
     torch.cuda.synchronize(dev)
     barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0, dist, dev)
+    elapsed = max_over_ranks(time.perf_counter() - t0, dist, coll_dev)
     # episode statistics all-gather (outside the timed region; 16 B per rank over xGMI)
     stats = gather_stats([float(venv.truncated.sum()), float(venv.success.sum()), float(venv.reward.sum()),
-                          float(args.steps)], dist, dev).sum(0)
+                          float(args.steps)], dist, coll_dev).sum(0)
     total = world * E * args.steps
     value = total / elapsed
 
@@ -327,24 +376,33 @@ def main():
     kernel_ms = ev0.elapsed_time(ev1) / args.kernel_launches
     # configs[4]: ReachAO sharded over every rank (collective timing: all ranks take part)
     ao = None if args.no_ao else sharded_leg(dev, "PandaReachAO-v3", args.ao_envs, args.task_steps, 20, dist, rank,
-                                            world)
+                                            world, coll_dev)
 
     if rank == 0:
         alg_bytes = ALG_BYTES_PER_ENV_STEP * E
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
         traffic = None
+        # the binding roofline: algorithmic FLOPs (op-counted in the oracle, frozen) over the
+        # kernel's own launch time (HIP events on the launch stream)
+        fkey = {"PandaReach-v3": "reach_table", "PandaPush-v3": "push", "PandaPickAndPlace-v3": "pick_and_place",
+                "PandaReachAO-v3": "reach_ao"}.get(args.env_id)
         valu = None
+        if fkey:
+            valu = valu_roofline(fkey, E / (kernel_ms * 1e-3), "env-steps/s of the step kernel alone (kernel_ms)")
+            valu["binding"] = True
         if os.path.exists(PROFILE_JSON):
             with open(PROFILE_JSON) as f:
                 prof = json.load(f)
             if prof.get("num_envs") == E:
                 traffic = prof.get("hbm_bytes_per_launch")
                 ins = prof.get("valu_lane_ops_per_launch")
-                if ins:
-                    valu = {"bound": "valu", "binding": True, "achieved": ins / (kernel_ms * 1e-3) / 1e12 * 2.0,
-                            "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s-equiv (2 x VALU lane-ops)",
-                            "source": os.path.relpath(PROFILE_JSON, ROOT)}
-                    valu["frac"] = valu["achieved"] / VALU_PEAK_TFLOPS
+                if ins and valu:
+                    # what the hardware issued (PMC SQ_INSTS_VALU x 64 lanes, the redundant lanes
+                    # of the 16-lane rows included), next to the algorithmic count
+                    valu["issued"] = {"lane_ops_per_env_step": ins / E,
+                                      "tflops_equiv": 2.0 * ins / (kernel_ms * 1e-3) / 1e12,
+                                      "redundancy": ins / E / valu["alg_flops_per_env_step"],
+                                      "source": os.path.relpath(PROFILE_JSON, ROOT)}
         line = {
             "metric": "aggregate env-steps/s, PandaReach 4096 envs @1 GPU; 1/2/4/8-GPU scaling",
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -375,9 +433,11 @@ def main():
         if world == 1 and not args.no_her:
             line["her_relabel"] = her_leg(dev, args.her_calls, not args.no_cpu_baseline)
         if world == 1 and not args.no_tasks:
-            line["tasks"] = [task_leg(dev, "PandaPush-v3", 4096, args.task_steps),               # configs[2]
-                             task_leg(dev, "PandaPickAndPlace-v3", 16384, args.task_steps),      # configs[3]
-                             task_leg(dev, args.env_id, E, args.task_steps, contacts=False)]     # no table
+            line["tasks"] = [task_leg(dev, "PandaPush-v3", 4096, args.task_steps, flops_key="push"),   # configs[2]
+                             task_leg(dev, "PandaPickAndPlace-v3", 16384, args.task_steps,            # configs[3]
+                                      flops_key="pick_and_place"),
+                             task_leg(dev, args.env_id, E, args.task_steps, contacts=False,           # no table
+                                      flops_key="reach_no_table")]
             line["sb3_host_path"] = host_path_leg(dev, args.env_id, E, 100)
         print(json.dumps(line), flush=True)
     venv.close()

@@ -16,8 +16,8 @@
  *                       panda_gym/__init__.py:23-91 (max_episode_steps)
  *   pgx_reset           RobotTaskEnv.reset core.py:298-308 -> Panda.reset
  *                       panda.py:290-298, Reach.reset reach.py:63-78,
- *                       Push.reset push.py:158-176, PickAndPlace.reset
- *                       pick_and_place.py:252-272
+ *                       Push.reset push.py:69-87, PickAndPlace.reset
+ *                       pick_and_place.py:65-85
  *   pgx_step            RobotTaskEnv.step core.py:352-368 -> Panda.set_action
  *                       panda.py:120-172 (IK: pybullet.py:465-493), PyBullet.step
  *                       pybullet.py:68-71 (20 x stepSimulation), _get_obs
@@ -25,8 +25,8 @@
  *                       reach.py:80-89, + gymnasium TimeLimit and SB3 VecEnv
  *                       auto-reset (terminal_observation)
  *   pgx_compute_reward  Task.compute_reward bound as env.compute_reward
- *                       (core.py:282; reach.py:84-89, push.py:182-187,
- *                       pick_and_place.py:278-283) over a batch (HER relabel)
+ *                       (core.py:282; reach.py:84-89, push.py:93-98,
+ *                       pick_and_place.py:91-96) over a batch (HER relabel)
  *   pgx_get_state /     PyBullet.get_joint_angles / get_joint_velocities /
  *   pgx_set_state       set_joint_angles pybullet.py:313-348,416-435 and
  *                       RobotTaskEnv.save_state/restore_state core.py:310-336
@@ -178,8 +178,9 @@ typedef struct pgx_config {
     const pgx_sim_params* params;
     /* scene (Task._create_scene, push.py:31-47; pybullet.py:759-817) */
     int32_t contacts;             /* 1: robot/table/object contacts (the reference's scene) */
-    int32_t lanes_per_env;        /* step layout: 0 auto (16 up to 8192 envs, else 1), 1 = one env
-                                     per lane, 16 = one env per 16-lane DPP row; ReachAO: 1 */
+    int32_t lanes_per_env;        /* step layout: 0 auto (16 with contacts -- every object task
+                                     and ReachAO -- at any batch, and up to 8192 envs without),
+                                     1 = one env per lane, 16 = one env per 16-lane DPP row */
     double goal_offset[3];        /* goal = offset + uniform(goal_low, goal_high): (0,0,0.02) Push/PnP */
     double goal_z_zero_prob;      /* PickAndPlace: noise z = 0 with probability 0.3 */
     double obj_low[3];            /* object = obj_offset + uniform(obj_low, obj_high) */
@@ -216,6 +217,9 @@ typedef struct pgx_step_out {
     float* terminal_obs;
     float* terminal_achieved_goal;
     float* terminal_desired_goal;
+    uint8_t* task_truncated;      /* [N] u8 Task.is_truncated of the step (ReachAO: is_collided,
+                                     reach_ao.py:1263-1264; 0 for the other tasks, reach.py:53-54),
+                                     i.e. info["is_truncated"], without the TimeLimit part */
 } pgx_step_out;
 
 /* Device-resident state views (SoA, env-minor: x[k*N + env]). */
@@ -270,7 +274,7 @@ int pgx_restore_state(pgx_handle h, const void* src_device, void* stream);
  * training uses (SB3 HerReplayBuffer / the fork's VecHerReplayBuffer,
  * training/utils/setup_training.py:176-179; classes/train_config.py:15),
  * "future" strategy, relabelled rewards from Task.compute_reward
- * (reach.py:84-89 / pick_and_place.py:278-283) in float32.
+ * (reach.py:84-89 / pick_and_place.py:91-96) in float32.
  *
  * Storage is [capacity][n_envs] slot-major like SB3's (buffer_size, n_envs)
  * arrays, one padded record per transition so a sampled transition is one

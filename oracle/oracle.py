@@ -14,8 +14,10 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "libpgx_oracle.so")
+FLOPS_LIB_PATH = os.path.join(HERE, "_build", "libpgx_oracle_flops.so")   # operation-counting build
 
 _lib = None
+_flops_lib = None
 
 
 def build() -> str:
@@ -35,6 +37,36 @@ def lib():
         _lib.pgxo_vec_step.restype = C.c_int
         _lib.pgxo_vec_reset.restype = C.c_int
     return _lib
+
+
+def flops_lib():
+    """The operation-counting build of the same oracle (oracle/flops_count.cpp)."""
+    global _flops_lib
+    if _flops_lib is None:
+        if not os.path.exists(FLOPS_LIB_PATH):
+            build()
+        _flops_lib = C.CDLL(FLOPS_LIB_PATH)
+        for f in ("pgxo_vec_step", "pgxo_vec_reset", "pgxo_flops_nphase"):
+            getattr(_flops_lib, f).restype = C.c_int
+    return _flops_lib
+
+
+class PgxoFlops(C.Structure):
+    _fields_ = [(k, C.c_int64) for k in ("add", "mul", "div", "sqrt", "trans", "cmp")]
+
+
+FLOP_PHASES = ("action_ik", "detection", "dynamics", "row_setup", "pgs_sweeps", "integrate", "obs_reward",
+               "reset", "ao_collision_check")
+
+
+def read_flops(clear: bool = True) -> dict:
+    """Per-phase operation counters of the counting build since the last clear."""
+    lb = flops_lib()
+    n = lb.pgxo_flops_nphase()
+    assert n == len(FLOP_PHASES), n
+    arr = (PgxoFlops * n)()
+    lb.pgxo_flops_read(arr, int(clear))
+    return {FLOP_PHASES[i]: {k: int(getattr(arr[i], k)) for k, _ in PgxoFlops._fields_} for i in range(n)}
 
 
 class PgxoMotor(C.Structure):
@@ -175,7 +207,9 @@ def philox(ctr, key):
 class OracleVecEnv:
     """Host-side fp64 mirror of one libpgx handle (AoS state), same vec-env semantics."""
 
-    def __init__(self, cfg, n: int):
+    def __init__(self, cfg, n: int, counting: bool = False):
+        """``counting``: run on the operation-counting build (read_flops) instead."""
+        self._lib = flops_lib() if counting else lib()
         self.cfg = cfg
         self.n = n
         self.nd = cfg.model.contents.n_dofs
@@ -206,7 +240,7 @@ class OracleVecEnv:
         m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
         g = None if inject_goal is None else _d(inject_goal)
         io = None if inject_obj is None else _d(inject_obj)
-        rc = lib().pgxo_vec_reset(C.byref(self.cfg), C.c_int64(self.n), None if m is None else _p(m),
+        rc = self._lib.pgxo_vec_reset(C.byref(self.cfg), C.c_int64(self.n), None if m is None else _p(m),
                                   None if g is None else _p(g), None if io is None else _p(io), _p(self.q),
                                   _p(self.qd), _p(self.goal),
                                   _p(self.obj), _p(self.elapsed), _p(self.episode), _p(b["obs"]), _p(b["ag"]),
@@ -220,7 +254,7 @@ class OracleVecEnv:
         n = self.n
         b.update(reward=np.zeros(n, np.float32), success=np.zeros(n, np.uint8), terminated=np.zeros(n, np.uint8),
                  truncated=np.zeros(n, np.uint8), terminal_obs=np.zeros((n, self.od), np.float32))
-        rc = lib().pgxo_vec_step(C.byref(self.cfg), C.c_int64(n), _p(self.q), _p(self.qd), _p(self.goal),
+        rc = self._lib.pgxo_vec_step(C.byref(self.cfg), C.c_int64(n), _p(self.q), _p(self.qd), _p(self.goal),
                                  _p(self.obj), _p(self.elapsed), _p(self.episode), _p(a), _p(b["obs"]), _p(b["ag"]),
                                  _p(b["dg"]), _p(b["reward"]), _p(b["success"]), _p(b["terminated"]),
                                  _p(b["truncated"]), _p(b["terminal_obs"]))
@@ -238,5 +272,5 @@ class OracleVecEnv:
 
     def sample_actions(self, step: int) -> np.ndarray:
         a = np.zeros((self.n, self.ad), np.float32)
-        lib().pgxo_sample_actions(C.byref(self.cfg), C.c_int64(self.n), C.c_uint64(step), _p(a))
+        self._lib.pgxo_sample_actions(C.byref(self.cfg), C.c_int64(self.n), C.c_uint64(step), _p(a))
         return a

@@ -21,6 +21,15 @@
 #define L PGX_MAX_LINKS
 #define D PGX_MAX_DOFS
 
+/* phase marks for the operation-counting build (oracle/flops_count.cpp); no-ops here:
+ * 0 action + IK, 1 contact detection, 2 dynamics (FK, M, bias, Cholesky, M^-1, free
+ * velocities), 3 constraint-row setup, 4 PGS sweeps, 5 integration + contact cache,
+ * 6 observation / success / reward, 7 reset (draws, rejection sampling, reset obs),
+ * 8 ReachAO per-substep collision check */
+#ifndef PGXO_PHASE
+#define PGXO_PHASE(k) ((void)0)
+#endif
+
 /* ----------------------------------------------------------------- small vec */
 /* diagnostics (tools/diag_iterations.py): histograms of PGS sweeps [0,64), contact
  * points per substep [64,80), IK iterations [80,112), substeps ending with a joint-limit
@@ -515,9 +524,12 @@ static void substep_impl(const pgx_model* m, const pgx_sim_params* p, const doub
     int nd = m->n_dofs;
     double dt = p->dt;
     kin_t k;
+    PGXO_PHASE(2);
     fk(m, base, q, &k);
     contact_t con[NC_MAX];
+    PGXO_PHASE(1);
     int ncon = W ? detect(m, p, W, &k, obj, con) : 0;
+    PGXO_PHASE(2);
     double M[D * D], Lm[D * D], b[D], qdd[D], Minv[D * D];
     mass_matrix(m, &k, M);
     bias(m, p, &k, qd, 1, 1, b);
@@ -548,6 +560,7 @@ static void substep_impl(const pgx_model* m, const pgx_sim_params* p, const doub
     }
 
     /* --- joint rows */
+    PGXO_PHASE(3);
     int nr = 0;
     double rhs[PGX_MAX_ROWS], lo[PGX_MAX_ROWS], hi[PGX_MAX_ROWS], inv[PGX_MAX_ROWS], sgn[PGX_MAX_ROWS],
         lam[PGX_MAX_ROWS];
@@ -648,6 +661,7 @@ static void substep_impl(const pgx_model* m, const pgx_sim_params* p, const doub
     }
 
     int it_used = 0;
+    PGXO_PHASE(4);
     for (int it = 0; it < p->num_iterations; it++) {
         double resid = 0.0;
         for (int j = 0; j < nr; j++) {
@@ -700,6 +714,7 @@ static void substep_impl(const pgx_model* m, const pgx_sim_params* p, const doub
         for (int c2 = 0; c2 < ncon; c2++) rob |= con[c2].grp != 0;
         pgxo_diag_hist[112] += lim; pgxo_diag_hist[113] += rob; pgxo_diag_hist[114] += lim && rob;
     }
+    PGXO_PHASE(5);
     double vn[D];
     for (int d = 0; d < nd; d++) vn[d] = clampd(vu[d] + dv[d], -p->max_coord_vel, p->max_coord_vel);
     if (p->flags & PGX_FLAG_CONSTRAINT_PASS_BIAS) {
@@ -870,7 +885,8 @@ int pgxo_ik(const pgx_model* m, const pgx_sim_params* p, const double base[3], c
         if (mx > p->ik_max_angle)
             for (int a = 0; a < nd; a++) dth[a] *= p->ik_max_angle / mx;
         for (int a = 0; a < nd; a++) q_out[a] = qs[a] + dth[a];
-        diff = v3_norm((double[3]){pos[0] - tgt[0], pos[1] - tgt[1], pos[2] - tgt[2]});
+        const double res3[3] = {pos[0] - tgt[0], pos[1] - tgt[1], pos[2] - tgt[2]};
+        diff = v3_norm(res3);
         memcpy(qs, q_out, sizeof(double) * nd);
     }
     if (it == 0) memcpy(q_out, q_start, sizeof(double) * nd);
@@ -1048,6 +1064,7 @@ int pgxo_vec_reset(const pgx_config* c, int64_t n, const uint8_t* mask, const do
                    const double* inject_obj, double* q, double* qd, double* goal, double* obj, int32_t* elapsed,
                    uint32_t* episode, float* obs, float* ag, float* dg) {
     int nd = c->model->n_dofs, od = obs_dim(c);
+    PGXO_PHASE(7);
     for (int64_t e = 0; e < n; e++) {
         if (mask && !mask[e]) continue;
         double* oe = obj ? obj + OBJ_N * e : NULL;
@@ -1209,15 +1226,41 @@ static double ao_link_distances(const pgx_config* c, const kin_t* k, const doubl
     return dtable;
 }
 
-/* check_collided (reach_ao.py:896-900) */
+/* check_collided (reach_ao.py:896-900): min over the collision links of the obstacle
+ * distance <= 0, or of the table distance of links 2..ee.  Only the decision is needed, so a
+ * pair whose lower bound is already > 0 is not measured (the decision is the same as with
+ * every distance computed, which ao_obs does): capsule vs obstacle -- the distance from the
+ * capsule axis to the obstacle centre minus the radius / the rounded cube's circumradius and
+ * the capsule radius; capsule vs table -- the signed distance of the rounded box is
+ * 1-Lipschitz, so along the axis it is >= min(sd(A), sd(B)) - |AB| / 2. */
 static int ao_collided(const pgx_config* c, const double* q, const double* obst) {
+    const pgx_model* m = c->model;
     kin_t k;
-    fk(c->model, c->base_pos, q, &k);
-    double dist[PGX_AO_LINKS], pa[PGX_AO_LINKS][3], pb[PGX_AO_LINKS][3];
-    double dt = ao_link_distances(c, &k, obst, dist, pa, pb);
-    double mn = dist[0];
-    for (int l = 1; l < PGX_AO_LINKS; l++) if (dist[l] < mn) mn = dist[l];
-    return mn <= 0.0 || dt <= 0.0;
+    fk(m, c->base_pos, q, &k);
+    double tc[3], th[3];
+    table_box(c, tc, th);
+    const double circum = AO_SIZE * 1.7320508075688772;   /* sqrt(3) * half extent */
+    for (int l = 0; l < PGX_AO_LINKS; l++) {
+        for (int ci = 0; ci < m->n_capsules; ci++) {
+            if (m->cap_link[ci] != kAoLinks[l]) continue;
+            double A[3], B[3];
+            capsule_world(m, &k, c->base_pos, ci, A, B);
+            const double r = m->cap_radius[ci];
+            for (int o = 0; o < PGX_AO_OBSTACLES; o++) {
+                const double* C = obst + 3 * o;
+                const cdist_t axis = capsule_sphere(A, B, 0.0, C, 0.0);   /* axis to centre */
+                if (axis.d - r - (kAoKind[o] == 0 ? AO_SIZE : circum) > 0.0) continue;
+                if (capsule_obstacle(A, B, r, kAoKind[o], C).d <= 0.0) return 1;
+            }
+            if (kAoLinks[l] >= 1) {
+                double ab[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]};
+                double sa = rbox_sd(A, tc, th), sb = rbox_sd(B, tc, th);
+                if ((sa < sb ? sa : sb) - 0.5 * v3_norm(ab) - r > 0.0) continue;
+                if (capsule_box(A, B, r, tc, th).d <= 0.0) return 1;
+            }
+        }
+    }
+    return 0;
 }
 
 /* whole-robot (every capsule incl. base and hand) distance to a sphere (kind 0) / box (1) */
@@ -1391,6 +1434,7 @@ int pgxo_vec_step(const pgx_config* c, int64_t n, double* q, double* qd, double*
         double* qde = qd + nd * e;
         double* ge = goal + 3 * e;
         double* oe = obj + OBJ_N * e;
+        PGXO_PHASE(0);
         /* Panda.set_action (panda.py:120-172): clip to the action space (float32) */
         float a[8];
         for (int i = 0; i < A; i++) {
@@ -1427,8 +1471,10 @@ int pgxo_vec_step(const pgx_config* c, int64_t n, double* q, double* qd, double*
         for (int s = 0; s < p->n_substeps; s++) {
             pgxo_world_substep(c, qe, qde, oe, mot, NULL);
             /* ReachAO step_check_collision (reach_ao.py:182-188) */
+            PGXO_PHASE(8);
             if (ao && ao_collided(c, qe, oe + OBJ_AO)) { collided = 1; break; }
         }
+        PGXO_PHASE(6);
 
         float o[64], agv[3], dgv[3];
         env_obs(c, qe, qde, ge, oe, o, agv, dgv);
@@ -1454,6 +1500,7 @@ int pgxo_vec_step(const pgx_config* c, int64_t n, double* q, double* qd, double*
             if (terminal_obs) memcpy(terminal_obs + od * e, o, sizeof(float) * od);
         }
         if ((trunc || term) && !c->no_auto_reset) {
+            PGXO_PHASE(7);
             reset_one(c, e, NULL, NULL, qe, qde, ge, oe, elapsed + e, episode + e);
             env_obs(c, qe, qde, ge, oe, o, agv, dgv);
         }

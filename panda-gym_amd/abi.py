@@ -90,7 +90,7 @@ class PgxStepOut(C.Structure):
         ("obs", C.c_void_p), ("achieved_goal", C.c_void_p), ("desired_goal", C.c_void_p),
         ("reward", C.c_void_p), ("success", C.c_void_p), ("terminated", C.c_void_p),
         ("truncated", C.c_void_p), ("terminal_obs", C.c_void_p), ("terminal_achieved_goal", C.c_void_p),
-        ("terminal_desired_goal", C.c_void_p),
+        ("terminal_desired_goal", C.c_void_p), ("task_truncated", C.c_void_p),
     ]
 
 
@@ -210,6 +210,7 @@ class EnvSpec:
     base_pos: Sequence[float] = (-0.6, 0.0, 0.0)       # panda_tasks.py:49,66,85
     distance_threshold: float = 0.05                   # reach.py:15
     goal_range: float = 0.3                            # reach.py:16
+    collision_reward: float = -100.0                   # ReachAO only: train_config.py:33
 
     @classmethod
     def reach_ao(cls, max_episode_steps: int = 50) -> "EnvSpec":
@@ -222,16 +223,16 @@ class EnvSpec:
                    distance_threshold=float(np.float32(0.05)))
 
     def obj_bounds(self):
-        """push.py:26-27 / pick_and_place.py:28-29: noise ranges of the object position."""
+        """push.py:24-25 / pick_and_place.py:26-27: noise ranges of the object position."""
         return [-0.15, -0.15, 0.0], [0.15, 0.15, 0.0]
 
     def goal_bounds(self):
         if self.task == TASK_REACH:   # reach.py:24-25
             g = self.goal_range
             return [-g / 2, -g / 2, 0.0], [g / 2, g / 2, g]
-        if self.task == TASK_PUSH:    # push.py:111-112 (+ z offset object_size/2 added at sample)
+        if self.task == TASK_PUSH:    # push.py:22-23 (+ z offset object_size/2 added at sample)
             return [-0.15, -0.15, 0.0], [0.15, 0.15, 0.0]
-        return [-0.15, -0.15, 0.0], [0.15, 0.15, 0.2]  # pick_and_place.py:211-212
+        return [-0.15, -0.15, 0.0], [0.15, 0.15, 0.2]  # pick_and_place.py:24-25
 
     @property
     def obs_dim(self) -> int:
@@ -270,14 +271,14 @@ def make_config(spec: EnvSpec, n_envs: int, model: PgxModel, params: PgxSimParam
     c.contacts = 1 if contacts else 0
     half = OBJECT_SIZE / 2
     if spec.task != TASK_REACH:
-        c.goal_offset[2] = half                   # push.py:71 / pick_and_place.py:68 (cube centre)
+        c.goal_offset[2] = half                   # push.py:77 / pick_and_place.py:73 (cube centre)
         c.obj_offset[2] = half
         olo, ohi = spec.obj_bounds()
         for i in range(3):
             c.obj_low[i], c.obj_high[i] = olo[i], ohi[i]
-    c.goal_z_zero_prob = 0.3 if spec.task == TASK_PICK_AND_PLACE else 0.0   # pick_and_place.py:73
+    c.goal_z_zero_prob = 0.3 if spec.task == TASK_PICK_AND_PLACE else 0.0   # pick_and_place.py:75-76
     c.object_half = half
-    c.object_mass = 1.0                           # push.py:37
+    c.object_mass = 1.0                           # push.py:36
     c.object_inertia = box_inertia(OBJECT_MASS, half)
     ao = spec.task == TASK_REACH_AO
     for i in range(3):  # create_table(1.1, 0.7, 0.4, x_offset=-0.3); ReachAO create_table(2.0, 1.3, 0.4) (reach_ao.py:272)
@@ -285,11 +286,11 @@ def make_config(spec: EnvSpec, n_envs: int, model: PgxModel, params: PgxSimParam
         c.table_half[i] = ((1.0, 0.65, 0.2) if ao else (0.55, 0.35, 0.2))[i]
     c.plane_z = -0.4                              # create_plane(z_offset=-0.4): box top
     c.terminate_on_success = 1 if ao else 0       # core.py:265 / train_config.py:28
-    c.collision_reward = -100.0 if ao else 0.0    # train_config.py:33
+    c.collision_reward = spec.collision_reward if ao else 0.0    # train_config.py:33
     return c
 
 
-OBJECT_SIZE = 0.04     # push.py:23
+OBJECT_SIZE = 0.04     # push.py:21
 OBJECT_MASS = 1.0
 
 

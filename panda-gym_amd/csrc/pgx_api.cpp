@@ -244,15 +244,24 @@ static int build_dev_model(const pgx_config* cfg, PgxDevModel* dm) {
     dm->lin_damp = (float)p->lin_damping;
     dm->ang_damp = (float)p->ang_damping;
     dm->max_vel = (float)p->max_coord_vel;
+    if (std::isnan(p->residual_threshold))
+        return fail(PGX_E_INVALID, "residual_threshold is NaN");
     dm->residual_thr = (float)p->residual_threshold;
-    {   /* fl(t * t) is monotone in t, so {t >= 0 : fl(t * t) <= thr} = [0, residual_abs] */
+    if (!(dm->residual_thr > 0.0f)) {
+        dm->residual_abs = 0.0f;           /* thr <= 0: only an exact zero residual exits */
+    } else if (!std::isfinite(dm->residual_thr)) {
+        dm->residual_abs = INFINITY;       /* +inf (or > FLT_MAX): every sweep exits */
+    } else {
+        /* fl(t * t) is monotone in t, so {t >= 0 : fl(t * t) <= thr} = [0, residual_abs];
+         * sqrtf is within an ulp or two of that bound, so a bounded walk settles it */
         volatile float thr = dm->residual_thr, t = std::sqrt(thr);
-        while (t > 0.0f && (float)(t * t) > thr) t = std::nextafter((float)t, 0.0f);
-        for (;;) {
+        for (int i = 0; i < 8 && t > 0.0f && (float)(t * t) > thr; i++) t = std::nextafter((float)t, 0.0f);
+        for (int i = 0; i < 8; i++) {
             volatile float u = std::nextafter((float)t, INFINITY);
             if (!((float)(u * u) <= thr)) break;
             t = u;
         }
+        if ((float)(t * t) > thr) return fail(PGX_E_INVALID, "residual_threshold %g: no float bound", (double)thr);
         dm->residual_abs = t;
     }
     dm->erp = (float)p->erp;
@@ -435,6 +444,7 @@ static PgxDevOut to_dev_out(const pgx_step_out* o) {
     d.terminal_obs = o->terminal_obs;
     d.terminal_ag = o->terminal_achieved_goal;
     d.terminal_dg = o->terminal_desired_goal;
+    d.task_truncated = o->task_truncated;
     return d;
 }
 

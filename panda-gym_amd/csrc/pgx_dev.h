@@ -88,6 +88,7 @@ struct PgxDevOut {
     float* terminal_obs;
     float* terminal_ag;
     float* terminal_dg;
+    uint8_t* task_truncated;   /* ReachAO is_collided (pgx_step_out.task_truncated) */
 };
 
 /* launchers (pgx_kernels.hip); return hipError_t as int */

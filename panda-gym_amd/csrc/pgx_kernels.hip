@@ -2438,7 +2438,7 @@ __device__ double distance_f32_f64(V3 ag, const double* gl) {
     double d = sqrt(s);
     return rint(d * 1e6) / 1e6;
 }
-/* goal = offset + noise (push.py:71-74), unfused */
+/* goal = offset + noise (push.py:77-79), unfused */
 __device__ double goal_add(double a, double b) { return a + b; }
 /* numpy Generator.uniform: low + (high - low) * u, unfused */
 __device__ double uniform_draw(double low, double high, double u) {
@@ -3122,6 +3122,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
         if (o.success) o.success[i] = succ;
         if (o.terminated) o.terminated[i] = term;
         if (o.truncated) o.truncated[i] = trunc;
+        if (o.task_truncated) o.task_truncated[i] = collided;
     }
     if constexpr (AO) {
         if constexpr (WIDE) ao_link_obs_g(*L, ln, c);

@@ -117,8 +117,8 @@ def _ao_geometry(base_pos: tuple) -> "reach_ao.RobotGeometry":
 def seeded_reset(env_spec: abi.EnvSpec, seed: Optional[int]) -> Optional[Tuple[np.ndarray, Optional[np.ndarray]]]:
     """(goal, object position) of RobotTaskEnv.reset(seed): a fresh PCG64(SeedSequence(seed))
     (core.py:302), then the task's draws in its own order -- Reach reach.py:75-78; Push
-    push.py:158-176 (goal noise, object noise, both around the cube centre height);
-    PickAndPlace pick_and_place.py:258-272 (goal noise, random() < 0.3 zeroes its z, object)."""
+    push.py:69-87 (goal noise, object noise, both around the cube centre height);
+    PickAndPlace pick_and_place.py:65-85 (goal noise, random() < 0.3 zeroes its z, object)."""
     if seed is None:
         return None
     if env_spec.task == abi.TASK_REACH_AO:   # (goal, obstacle centres [6, 3])
@@ -190,11 +190,14 @@ class PandaVecEnv:
         self.terminal_obs = torch.zeros((n, od), dtype=torch.float32, **kw)
         self.terminal_ag = torch.zeros((n, 3), dtype=torch.float32, **kw)
         self.terminal_dg = torch.zeros((n, 3), dtype=torch.float32, **kw)
+        # Task.is_truncated (ReachAO is_collided): written by the kernel; zero for the other tasks
+        self.task_trunc = torch.zeros(n, dtype=torch.uint8, **kw)
         self._actions = torch.zeros((n, self.action_dim), dtype=torch.float32, **kw)
         self._out = abi.PgxStepOut(self.obs.data_ptr(), self.achieved_goal.data_ptr(), self.desired_goal.data_ptr(),
                                    self.reward.data_ptr(), self.success.data_ptr(), self.terminated.data_ptr(),
                                    self.truncated.data_ptr(), self.terminal_obs.data_ptr(), self.terminal_ag.data_ptr(),
-                                   self.terminal_dg.data_ptr())
+                                   self.terminal_dg.data_ptr(),
+                                   self.task_trunc.data_ptr() if self.spec.task == abi.TASK_REACH_AO else None)
         self.observation_space = DictSpace(observation=Box(-10.0, 10.0, (od,)), desired_goal=Box(-10.0, 10.0, (3,)),
                                            achieved_goal=Box(-10.0, 10.0, (3,)))
         self.action_space = Box(-1.0, 1.0, (self.action_dim,))
@@ -320,8 +323,8 @@ class PandaVecEnv:
                                                                            device=self.device),
                 "observation": torch.empty((n, od), **pin), "achieved_goal": torch.empty((n, 3), **pin),
                 "desired_goal": torch.empty((n, 3), **pin), "reward": torch.empty(n, **pin),
-                "flags": torch.empty((3, n), dtype=torch.uint8, pin_memory=True),
-                "flags_dev": torch.empty((3, n), dtype=torch.uint8, device=self.device),
+                "flags": torch.empty((4, n), dtype=torch.uint8, pin_memory=True),
+                "flags_dev": torch.empty((4, n), dtype=torch.uint8, device=self.device),
                 "t_observation": torch.empty((n, od), **pin), "t_achieved_goal": torch.empty((n, 3), **pin),
                 "t_desired_goal": torch.empty((n, 3), **pin),
             }
@@ -352,6 +355,7 @@ class PandaVecEnv:
         fd[0].copy_(term)
         fd[1].copy_(trunc)
         fd[2].copy_(succ)
+        fd[3].copy_(self.task_trunc)
         for k, src in (("observation", obs["observation"]), ("achieved_goal", obs["achieved_goal"]),
                        ("desired_goal", obs["desired_goal"]), ("reward", rew), ("flags", fd),
                        ("t_observation", self.terminal_obs), ("t_achieved_goal", self.terminal_ag),
@@ -362,11 +366,10 @@ class PandaVecEnv:
         o = {k: hs[k].numpy().copy() for k in ("observation", "achieved_goal", "desired_goal")}
         r = hs["reward"].numpy().copy()
         fl = hs["flags"].numpy() != 0
-        te, tr, sc = fl[0].copy(), fl[1].copy(), fl[2]
+        te, tr, sc, col = fl[0].copy(), fl[1].copy(), fl[2], fl[3]
         d = te | tr
-        col = self.task_truncated(r)
         infos: List[Dict[str, Any]] = [{"is_success": s, "is_truncated": c}
-                                       for s, c in zip(sc.tolist(), np.broadcast_to(col, sc.shape).tolist())]
+                                       for s, c in zip(sc.tolist(), col.tolist())]
         idx = np.nonzero(d)[0]
         if len(idx):
             tobs, tag, tdg = hs["t_observation"].numpy(), hs["t_achieved_goal"].numpy(), hs["t_desired_goal"].numpy()
@@ -380,13 +383,11 @@ class PandaVecEnv:
         self.step_async(actions)
         return self.step_wait()
 
-    def task_truncated(self, reward):
-        """Task.is_truncated of the step that returned ``reward``: False for Reach / Push /
-        PickAndPlace (reach.py:53-54); ReachAO's is_collided (reach_ao.py:1263-1264), which is
-        exactly the steps whose sparse reward carries collision_reward (-1 - 100 vs -1 / +0)."""
-        col = np.asarray(reward) < 0.5 * self._cfg.collision_reward if self.spec.task == abi.TASK_REACH_AO \
-            else np.zeros(np.shape(reward), dtype=bool)
-        return col if np.ndim(col) else bool(col)
+    def task_truncated(self) -> np.ndarray:
+        """Task.is_truncated of the last step per env: False for Reach / Push / PickAndPlace
+        (reach.py:53-54); ReachAO's is_collided (reach_ao.py:1263-1264), the kernel's own
+        collision flag (pgx_step_out.task_truncated), whatever collision_reward is."""
+        return self.task_trunc.cpu().numpy() != 0
 
     def _numpy_obs(self) -> Dict[str, np.ndarray]:
         return {k: v.cpu().numpy().copy() for k, v in self._obs_dict().items()}
@@ -488,7 +489,7 @@ class PandaEnv:
         r = float(rew[0].item())
         # the kernel's truncated flag = Task.is_truncated (ReachAO collision) or the TimeLimit
         # (gymnasium TimeLimit.step ORs them); info carries the task's own flag (core.py:363-365)
-        info = {"is_success": bool(succ[0].item()), "is_truncated": self._vec.task_truncated(r)}
+        info = {"is_success": bool(succ[0].item()), "is_truncated": bool(self._vec.task_truncated()[0])}
         return o, r, bool(term[0].item()), bool(trunc[0].item()), info
 
     def compute_reward(self, achieved_goal, desired_goal, info=None):

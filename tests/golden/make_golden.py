@@ -11,7 +11,7 @@ Run in the build container only (the reference tree is not on the GPU box):
   HER call (float32 vs float32), random pairs plus rounding and threshold edges.
 * Goal/object draws of ``RobotTaskEnv.reset(seed)`` (core.py:302: a fresh
   ``np.random.Generator(PCG64(SeedSequence(seed)))`` per reset) for the task
-  samplers (reach.py:75-78, push.py:164-176, pick_and_place.py:258-272),
+  samplers (reach.py:75-78, push.py:69-87, pick_and_place.py:65-85),
   reproduced with numpy's PCG64 (gymnasium 0.29 seeding.np_random).
 """
 import importlib.util

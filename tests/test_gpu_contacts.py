@@ -137,21 +137,23 @@ def test_reach_with_table_contacts(pg, oracle, lanes):
 
 @pytest.mark.parametrize("env_id", ["PandaPush-v3", "PandaPickAndPlaceJoints-v3"])
 def test_random_policy_one_step_parity(pg, oracle, env_id, lanes):
-    """p99 <= 1e-5 and p99.9 <= 1e-4; every sample above 1e-3 must sit at a contact
-    bifurcation: the oracle itself, from its input perturbed by 1e-7 relative, moves by at
-    least a quarter of the device's deviation there (max over 16 trials)."""
+    """p99 <= 1e-5 and p99.9 <= 1e-4 in both layouts.  One lane per env: max <= 1e-3.  The
+    16-lane layout (lane-parallel bias / CRBA: a different summation order) may exceed 1e-3 only
+    at a contact bifurcation, and only where the oracle itself, from its input perturbed by 1e-7
+    relative (the fp32 rounding scale), moves by at least the device's deviation (max over 32
+    trials); at most one such sample per 2000."""
     outl = []
     ee, ag, final = _one_step_errors(pg, oracle, env_id, 256, 50, 21, lanes=lanes, outliers=outl)
     cfg, _keep = outl.pop()
     for name, e in (("ee", ee), ("object", ag)):
         assert np.percentile(e, 99) <= 1e-5, (name, np.percentile(e, 99))
         assert np.percentile(e, 99.9) <= 1e-4, (name, np.percentile(e, 99.9))
-        assert e.max() <= 1e-2, (name, e.max())
-    assert len(outl) <= ee.size // 500, len(outl)
+        assert e.max() <= (1e-2 if lanes == 16 else OUTLIER), (name, e.max())
+    assert len(outl) <= ee.size // 2000, len(outl)
     for rec in outl:
-        s_ee, s_ag = _self_sensitivity(oracle, cfg, rec)
-        assert rec["err_ee"] <= OUTLIER or s_ee >= 0.25 * rec["err_ee"], (rec["t"], rec["env"], rec["err_ee"], s_ee)
-        assert rec["err_ag"] <= OUTLIER or s_ag >= 0.25 * rec["err_ag"], (rec["t"], rec["env"], rec["err_ag"], s_ag)
+        s_ee, s_ag = _self_sensitivity(oracle, cfg, rec, trials=32)
+        assert rec["err_ee"] <= OUTLIER or s_ee >= rec["err_ee"], (rec["t"], rec["env"], rec["err_ee"], s_ee)
+        assert rec["err_ag"] <= OUTLIER or s_ag >= rec["err_ag"], (rec["t"], rec["env"], rec["err_ag"], s_ag)
     cube = final["object"].cpu().numpy()
     assert cube[2].min() > -0.4
 

@@ -258,3 +258,35 @@ def test_vec_env_infos_is_truncated_on_collision(pg):
     assert [i["is_truncated"] for i in infos] == [True, False, True, False]
     assert infos[0]["TimeLimit.truncated"] is True and "terminal_observation" in infos[0]
     venv.close()
+
+
+@pytest.mark.parametrize("collision_reward", [-1.0, 0.0])
+def test_is_truncated_is_the_collision_flag_for_any_collision_reward(pg, collision_reward):
+    """info["is_truncated"] is the kernel's collision flag (pgx_step_out.task_truncated), not a
+    reward threshold: with collision_reward -1 or 0 a non-colliding, unsuccessful step still
+    reports False and the colliding one True (reach_ao.py:1263-1264)."""
+    from dataclasses import replace
+
+    from oracle.oracle import fk
+
+    env_id = f"PandaReachAOcr{int(collision_reward)}-v3"
+    pg.envs._REGISTRY[env_id] = replace(pg.spec(ENV), collision_reward=collision_reward)
+    n = 4
+    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=1)
+    com, _, _ = fk(venv._cfg.model.contents, np.array(pg.abi.NEUTRAL_Q[:7]))
+    ee = com[11]
+    obst = np.array([[ee[0], ee[1] + 0.14, ee[2]]] + [[99.9, 99.9, -99.9]] * 5)
+    far = np.array([[99.9, 99.9, -99.9]] * 6)
+    venv.reset_tensors(goals=np.tile([[0.5, 0.3, 0.3]], (n, 1)), objects=np.stack([obst, far, obst, far]))
+    a = np.zeros((n, 7), np.float32)
+    a[:, 0] = 1.0
+    for _ in range(10):
+        _, rew, dones, infos = venv.step(a)
+        if dones.any():
+            break
+        assert [i["is_truncated"] for i in infos] == [False] * n
+    assert dones.tolist() == [True, False, True, False]
+    assert [i["is_truncated"] for i in infos] == [True, False, True, False]
+    assert rew.tolist() == [-1.0 + collision_reward, -1.0, -1.0 + collision_reward, -1.0]
+    venv.close()
+    del pg.envs._REGISTRY[env_id]
