@@ -232,7 +232,15 @@ typedef struct pgx_state_view {
     float* obstacles;   /* [4*PGX_AO_OBSTACLES][N] ReachAO obstacle centres (x,y,z) then active flags */
     int32_t* elapsed;   /* [N] steps in the current episode */
     uint32_t* episode;  /* [N] episodes finished (RNG counter) */
+    uint32_t* errors;   /* [1] sticky PGX_ERR_* bits set by the kernels; the host clears them */
 } pgx_state_view;
+
+/* errors word (pgx_state_view.errors): a device-side reset that cannot complete the way the
+ * reference's would.  PGX_ERR_AO_OBSTACLE: ReachAO.set_coll_free_obs drew 10000 obstacle
+ * positions without a collision-free one, where the reference raises StopIteration
+ * ("Couldn't find collision free obstacle!", reach_ao.py:1143-1145); the env keeps the last
+ * draw and the host raises PgxError when it reads the bit. */
+#define PGX_ERR_AO_OBSTACLE 1u
 
 const char* pgx_version(void);
 const char* pgx_last_error(void);

@@ -270,6 +270,11 @@ class OracleVecEnv:
     def active(self) -> np.ndarray:
         return self.obj[:, OBJ_AO + 18:OBJ_AO + 24]
 
+    def take_errors(self) -> int:
+        """PGX_ERR_* bits the resets set since the last call (the device errors word)."""
+        self._lib.pgxo_take_errors.restype = C.c_uint32
+        return int(self._lib.pgxo_take_errors())
+
     def sample_actions(self, step: int) -> np.ndarray:
         a = np.zeros((self.n, self.ad), np.float32)
         self._lib.pgxo_sample_actions(C.byref(self.cfg), C.c_int64(self.n), C.c_uint64(step), _p(a))

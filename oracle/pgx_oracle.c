@@ -365,7 +365,15 @@ typedef struct {
     int contacts, has_object;
     double half, mass, inertia;
     double tc[3], th[3], plane_z;
+    const double* obst;   /* ReachAO: obstacle centres [6][3] (static colliders), else NULL */
 } world_t;
+
+/* closest pair of a capsule and an obstacle (ReachAO section below): signed distance d,
+ * point on the capsule pa, on the obstacle pb, n the unit direction from the capsule axis
+ * towards the obstacle (pb - pa = d n away from contact) */
+typedef struct { double d, pa[3], pb[3], n[3]; } cdist_t;
+static cdist_t ao_capsule_obstacle(const double* A, const double* B, double r, int o, const double* obst);
+static double ao_pair_lower_bound(const double* A, const double* B, double r, int o, const double* obst);
 
 static void quat_to_mat(const double* q, double* R) {
     double x = q[0], y = q[1], z = q[2], w = q[3];
@@ -476,6 +484,24 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
                     m3_v(Rc, nl, c.n);
                     m3_v(Rc, qb, c.pb);
                     for (int i = 0; i < 3; i++) { c.pb[i] += obj[i]; c.pa[i] = C[i] - r * c.n[i]; }
+                    keep4(g1, &n1, &c);
+                }
+            }
+        }
+        /* ReachAO: the obstacles are static colliders (create_obstacle_sphere / _cuboid,
+         * reach_ao.py:819-860: mass 0, not ghosts), so Bullet resolves robot contacts with
+         * them inside stepSimulation like the table's: per capsule and obstacle the closest
+         * pair (one point, as the convex-convex query returns it) within the processing
+         * threshold, the normal from the obstacle to the robot, a static body B */
+        if (W->obst) {
+            for (int o = 0; o < PGX_AO_OBSTACLES; o++) {
+                /* the axis-to-centre distance minus the radii bounds the pair from below: a pair
+                 * that cannot be within tau is not measured (the same candidates) */
+                if (ao_pair_lower_bound(A, B, r, o, W->obst) >= tau) continue;
+                const cdist_t cd = ao_capsule_obstacle(A, B, r, o, W->obst);
+                if (cd.d < tau) {
+                    contact_t c = {1, 32 + 6 * ci + o, li, {-cd.n[0], -cd.n[1], -cd.n[2]},
+                                   {cd.pa[0], cd.pa[1], cd.pa[2]}, {cd.pb[0], cd.pb[1], cd.pb[2]}, cd.d};
                     keep4(g1, &n1, &c);
                 }
             }
@@ -773,12 +799,14 @@ static void world_of(const pgx_config* c, world_t* W) {
     W->inertia = c->object_inertia;
     for (int i = 0; i < 3; i++) { W->tc[i] = c->table_center[i]; W->th[i] = c->table_half[i]; }
     W->plane_z = c->plane_z;
+    W->obst = NULL;
 }
 
 void pgxo_world_substep(const pgx_config* c, double* q, double* qd, double* obj, const pgxo_motor* motors,
                         pgxo_stats* st) {
     world_t W;
     world_of(c, &W);
+    W.obst = c->task == PGX_TASK_REACH_AO ? obj + OBJ_AO : NULL;
     substep_impl(c->model, c->params, c->base_pos, q, qd, motors, st, &W, obj);
 }
 
@@ -1086,14 +1114,18 @@ int pgxo_vec_reset(const pgx_config* c, int64_t n, const uint8_t* mask, const do
  * (Model.capsules, the URDF's cylinder+sphere unions) against sphere / box
  * obstacles: signed distances (negative when penetrating), closest point pairs. */
 static const int kAoKind[PGX_AO_OBSTACLES] = {0, 0, 0, 1, 1, 1};   /* 3 spheres, then 3 cuboids */
+static uint32_t pgxo_errors;   /* PGX_ERR_* of the device errors word, set by the resets */
+uint32_t pgxo_take_errors(void) {
+    uint32_t e = pgxo_errors;
+    pgxo_errors = 0;
+    return e;
+}
 #define AO_SIZE 0.05          /* sphere radius / cuboid half extent (create_scenario_reachao3/_rand) */
 #define AO_DUMMY_R 0.05       /* the goal's dummy sphere (reach_ao.py:281-287) */
 #define AO_MARGIN 0.001       /* btBoxShape collision margin of createCollisionShape boxes: the
                                  box is its inner box (h - m) swept by a sphere of radius m */
 #define AO_PI 3.14159265358979323846
 static const int kAoLinks[PGX_AO_LINKS] = {0, 1, 2, 3, 4, 5, 6, 7, 9};  /* link1..8, panda_ee */
-
-typedef struct { double d, pa[3], pb[3]; } cdist_t;
 
 /* signed distance of P to the axis-aligned box (c, h): negative inside */
 static double box_sd(const double* P, const double* c, const double* h) {
@@ -1114,7 +1146,7 @@ static cdist_t capsule_sphere(const double* A, const double* B, double r, const 
     if (len > 0) for (int i = 0; i < 3; i++) n[i] = v[i] / len;
     cdist_t o;
     o.d = len - r - R;
-    for (int i = 0; i < 3; i++) { o.pa[i] = P[i] + r * n[i]; o.pb[i] = C[i] - R * n[i]; }
+    for (int i = 0; i < 3; i++) { o.pa[i] = P[i] + r * n[i]; o.pb[i] = C[i] - R * n[i]; o.n[i] = n[i]; }
     return o;
 }
 
@@ -1171,7 +1203,7 @@ static cdist_t capsule_box(const double* A, const double* B, double r, const dou
     }
     cdist_t o;
     o.d = sd - AO_MARGIN - r;
-    for (int i = 0; i < 3; i++) { o.pa[i] = P[i] + r * n[i]; o.pb[i] = q[i] - AO_MARGIN * n[i]; }
+    for (int i = 0; i < 3; i++) { o.pa[i] = P[i] + r * n[i]; o.pb[i] = q[i] - AO_MARGIN * n[i]; o.n[i] = n[i]; }
     return o;
 }
 
@@ -1190,6 +1222,16 @@ static cdist_t capsule_obstacle(const double* A, const double* B, double r, int 
     if (kind == 0) return capsule_sphere(A, B, r, C, AO_SIZE);
     const double h[3] = {AO_SIZE, AO_SIZE, AO_SIZE};
     return capsule_box(A, B, r, C, h);
+}
+
+static cdist_t ao_capsule_obstacle(const double* A, const double* B, double r, int o, const double* obst) {
+    return capsule_obstacle(A, B, r, kAoKind[o], obst + 3 * o);
+}
+/* capsule axis to obstacle centre, minus the capsule radius and the sphere radius / the
+ * rounded cube's circumradius: <= the pair's distance */
+static double ao_pair_lower_bound(const double* A, const double* B, double r, int o, const double* obst) {
+    const cdist_t axis = capsule_sphere(A, B, 0.0, obst + 3 * o, 0.0);
+    return axis.d - r - (kAoKind[o] == 0 ? AO_SIZE : AO_SIZE * 1.7320508075688772);
 }
 
 static void table_box(const pgx_config* c, double* tc, double* th) {
@@ -1318,6 +1360,7 @@ static void ao_reset_task(const pgx_config* c, int64_t e, uint32_t episode, cons
     }
     for (int o = 0; o < PGX_AO_OBSTACLES; o++) {
         double* P = obst + 3 * o;
+        int placed = 0;
         for (int it = 0; it < 10000; it++) {
             double rnd = ao_draw(&d), s[3];
             hollow_sphere(&d, 0.1, 0.5, 0, s);
@@ -1337,8 +1380,11 @@ static void ao_reset_task(const pgx_config* c, int64_t e, uint32_t episode, cons
                 ddum = rbox_sd(dummy, P, h) - AO_DUMMY_R;
             }
             int coll = ao_robot_distance(c, &k, kAoKind[o], P, AO_SIZE) <= 0.03 || dtab <= 0.03 || ddum <= 0.03;
-            if (!coll) break;
+            if (!coll) { placed = 1; break; }
         }
+        /* set_coll_free_obs raises StopIteration on the 10001st attempt (reach_ao.py:1143-1145):
+         * the last draw stays, the sticky error word records it (pgxo_take_errors) */
+        if (!placed) pgxo_errors |= PGX_ERR_AO_OBSTACLE;
         active[o] = 1.0;
     }
     int n_active = 4 + (int)(ao_draw(&d) * 2.0);           /* integers(4, 6) */

@@ -81,6 +81,8 @@ int pgxo_vec_reset(const pgx_config* cfg, int64_t n, const uint8_t* mask, const 
                    const double* inject_obj, double* q, double* qd, double* goal, double* obj,
                    int32_t* elapsed, uint32_t* episode, float* obs, float* ag, float* dg);
 void pgxo_sample_actions(const pgx_config* cfg, int64_t n, uint64_t step, float* action);
+/* sticky PGX_ERR_* bits set by the resets since the last call (cleared by it) */
+uint32_t pgxo_take_errors(void);
 
 #ifdef __cplusplus
 }

@@ -85,6 +85,9 @@ class PgxConfig(C.Structure):
     ]
 
 
+ERR_AO_OBSTACLE = 1   # PGX_ERR_AO_OBSTACLE (include/pgx.h): pgx_state_view.errors bit
+
+
 class PgxStepOut(C.Structure):
     _fields_ = [
         ("obs", C.c_void_p), ("achieved_goal", C.c_void_p), ("desired_goal", C.c_void_p),
@@ -98,6 +101,7 @@ class PgxStateView(C.Structure):
     _fields_ = [
         ("q", C.c_void_p), ("qd", C.c_void_p), ("goal", C.c_void_p), ("object", C.c_void_p),
         ("contacts", C.c_void_p), ("obstacles", C.c_void_p), ("elapsed", C.c_void_p), ("episode", C.c_void_p),
+        ("errors", C.c_void_p),
     ]
 
 

@@ -380,7 +380,7 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
            off_obj = align(off_qd + PGX_NJ * N * 4), off_ct = align(off_obj + 13 * N * 4),
            off_ao = align(off_ct + 2 * PGX_CONTACT_SLOTS * N * 4),
            off_el = align(off_ao + (e.ao ? 4 * PGX_AO_OBSTACLES * N * 4 : 0)), off_ep = align(off_el + N * 4),
-           total = align(off_ep + N * 4);
+           off_err = align(off_ep + N * 4), total = align(off_err + 4);
     rc = hip_check(hipMalloc(&h->blob, total), "hipMalloc(state)");
     if (rc) { delete h; return rc; }
     h->blob_bytes = total;
@@ -393,6 +393,7 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     h->ds.obstacles = e.ao ? (float*)(b + off_ao) : nullptr;
     h->ds.elapsed = (int32_t*)(b + off_el);
     h->ds.episode = (uint32_t*)(b + off_ep);
+    h->ds.errors = (uint32_t*)(b + off_err);
     h->dm_dev = (PgxDevModel*)b;
     rc = hip_check(hipMemset(h->blob, 0, total), "hipMemset(state)");
     if (!rc) rc = hip_check(hipMemcpy(h->dm_dev, &h->dm, sizeof(PgxDevModel), hipMemcpyHostToDevice), "model copy");
@@ -427,6 +428,7 @@ int pgx_get_state(pgx_handle h, pgx_state_view* out) {
     out->obstacles = h->ds.obstacles;
     out->elapsed = h->ds.elapsed;
     out->episode = h->ds.episode;
+    out->errors = h->ds.errors;
     return PGX_OK;
 }
 

@@ -75,6 +75,7 @@ struct PgxDevState {
     float* obstacles;  /* [4*PGX_AO_OBSTACLES][N] ReachAO centres (o, xyz) then active flags */
     int32_t* elapsed;  /* [N] */
     uint32_t* episode; /* [N] */
+    uint32_t* errors;  /* [1] sticky PGX_ERR_* bits (pgx_state_view.errors) */
 };
 
 struct PgxDevOut {

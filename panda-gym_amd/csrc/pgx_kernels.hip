@@ -477,6 +477,151 @@ __device__ __forceinline__ void ik(MPtr mp, const float* q0, V3 target, const fl
 }
 
 /* --------------------------------------------------------------- physics */
+/* ------------------------------------------------ ReachAO geometry (shared) */
+constexpr int AO_N = PGX_AO_OBSTACLES;
+constexpr float kAoSize = 0.05f, kAoMargin = 0.001f, kAoDummyR = 0.05f;
+constexpr float kAoCubeBound = 0.0866025404f;   /* 0.05 * sqrt(3): cuboid circumradius */
+
+/* AO collision-link slot of each capsule (-1: base, hand) */
+__host__ __device__ constexpr int ao_slot(int c) {
+    return kCapLink[c] < 0 ? -1 : (kCapLink[c] <= 7 ? kCapLink[c] : (kCapLink[c] == 9 ? 8 : -1));
+}
+__device__ constexpr int kAoSlot[PGX_NCAP] = {ao_slot(0), ao_slot(1), ao_slot(2), ao_slot(3), ao_slot(4),
+                                              ao_slot(5), ao_slot(6), ao_slot(7), ao_slot(8), ao_slot(9),
+                                              ao_slot(10), ao_slot(11), ao_slot(12), ao_slot(13)};
+static_assert(PGX_NCAP == 14, "kAoSlot table");
+
+
+/* signed distance to the axis-aligned box (c, h) */
+__device__ __forceinline__ float box_sd(V3 P, V3 c, V3 h) {
+    const float dx = fabsf(P.x - c.x) - h.x, dy = fabsf(P.y - c.y) - h.y, dz = fabsf(P.z - c.z) - h.z;
+    const float ox = fmaxf(dx, 0.0f), oy = fmaxf(dy, 0.0f), oz = fmaxf(dz, 0.0f);
+    return fast_sqrt(ox * ox + oy * oy + oz * oz) + fminf(fmaxf(dx, fmaxf(dy, dz)), 0.0f);
+}
+
+/* closest point of segment AB to C */
+__device__ __forceinline__ V3 seg_closest(V3 A, V3 B, V3 C) {
+    const V3 ab = B - A;
+    const float l2 = dot(ab, ab);
+    float t = l2 > 0.0f ? dot(C - A, ab) / l2 : 0.0f;
+    t = fminf(fmaxf(t, 0.0f), 1.0f);
+    return A + t * ab;
+}
+
+/* capsule (A, B, r) vs rounded box (c, full half extents hf): a golden-section search
+ * on the inner box's signed distance along the axis, the signed distance returned; with NV
+ * also the closest axis point P and the unit direction n from it towards the box (into the
+ * box through the nearest face when P is inside the inner box) */
+template <bool NV>
+__device__ __forceinline__ float capsule_box_pair(V3 A, V3 B, float r, V3 c, V3 hf, V3* Pout, V3* nout) {
+    const V3 h = v3(hf.x - kAoMargin, hf.y - kAoMargin, hf.z - kAoMargin);
+    const V3 ab = B - A;
+    float lo = 0.0f, hi = 1.0f;
+    const bool seg = dot(ab, ab) > 0.0f;
+    if (seg) {
+        /* golden-section search of the convex box_sd along the axis: one evaluation per step,
+         * 34 steps shrink [0, 1] to 0.618^34 = 8e-8 (the ternary search's 40 steps of two
+         * evaluations reach 9e-8) */
+        const float gr = 0.61803398875f;
+        float t1 = hi - gr * (hi - lo), t2 = lo + gr * (hi - lo);
+        float f1 = box_sd(A + t1 * ab, c, h), f2 = box_sd(A + t2 * ab, c, h);
+        for (int it = 0; it < 34; it++) {
+            if (f1 <= f2) {
+                hi = t2; t2 = t1; f2 = f1;
+                t1 = hi - gr * (hi - lo);
+                f1 = box_sd(A + t1 * ab, c, h);
+            } else {
+                lo = t1; t1 = t2; f1 = f2;
+                t2 = lo + gr * (hi - lo);
+                f2 = box_sd(A + t2 * ab, c, h);
+            }
+        }
+    }
+    V3 P = A + (seg ? 0.5f * (lo + hi) : 0.0f) * ab;
+    float sd = box_sd(P, c, h);
+    if (seg && sd > 0.0f) {
+        /* two alternating projections (box -> segment): the search cannot resolve t where
+         * the distance is flat to second order (a segment passing an edge or a corner);
+         * each can only shorten the pair and pins it */
+        for (int it = 0; it < 2; it++) {
+            const V3 q = v3(fminf(fmaxf(P.x, c.x - h.x), c.x + h.x), fminf(fmaxf(P.y, c.y - h.y), c.y + h.y),
+                            fminf(fmaxf(P.z, c.z - h.z), c.z + h.z));
+            P = seg_closest(A, B, q);
+        }
+        sd = box_sd(P, c, h);
+    }
+    const float d = sd - kAoMargin - r;
+    if (NV) {
+        V3 n;
+        if (sd > 0.0f) {
+            const V3 q = v3(fminf(fmaxf(P.x, c.x - h.x), c.x + h.x), fminf(fmaxf(P.y, c.y - h.y), c.y + h.y),
+                            fminf(fmaxf(P.z, c.z - h.z), c.z + h.z));
+            const V3 v = q - P;
+            const float len = norm(v);
+            n = len > 0.0f ? fast_rcp(len) * v : v3(0.0f, 0.0f, 0.0f);
+        } else {   /* inside the inner box: out through the nearest face */
+            const float bx = fabsf(P.x - c.x) - h.x, by = fabsf(P.y - c.y) - h.y, bz = fabsf(P.z - c.z) - h.z;
+            const int ax = (bx >= by && bx >= bz) ? 0 : (by >= bz ? 1 : 2);
+            const float sx = P.x < c.x ? 1.0f : -1.0f, sy = P.y < c.y ? 1.0f : -1.0f, sz = P.z < c.z ? 1.0f : -1.0f;
+            n = v3(ax == 0 ? sx : 0.0f, ax == 1 ? sy : 0.0f, ax == 2 ? sz : 0.0f);
+        }
+        *Pout = P;
+        *nout = n;
+    }
+    return d;
+}
+/* the distance, and with VEC the unit vector from the capsule's closest point to the box's
+ * (utils.unit_vector: pb - pa = d n) */
+template <bool VEC>
+__device__ __forceinline__ float capsule_box(V3 A, V3 B, float r, V3 c, V3 hf, V3* u) {
+    V3 P, n;
+    const float d = capsule_box_pair<VEC>(A, B, r, c, hf, &P, &n);
+    if (VEC) *u = d > 0.0f ? n : (d < 0.0f ? (-1.0f) * n : v3(0.0f, 0.0f, 0.0f));
+    return d;
+}
+
+/* capsule_box(...) <= thr as a decision: the same golden-section search, stopped as soon as a
+ * sample is within r + margin of the inner box (the minimum can only be lower) or the best
+ * sample minus |AB| times the bracket width (f is |AB|-Lipschitz in t; the minimiser stays in
+ * the bracket of a convex f) is farther than that (the minimum cannot reach it); the
+ * undecided rest ends as capsule_box does. */
+__device__ __forceinline__ bool capsule_box_hit(V3 A, V3 B, float r, V3 c, V3 hf, float thr = 0.0f) {
+    const V3 h = v3(hf.x - kAoMargin, hf.y - kAoMargin, hf.z - kAoMargin);
+    const V3 ab = B - A;
+    const float lim = kAoMargin + r + thr;
+    if (!(dot(ab, ab) > 0.0f)) return box_sd(A, c, h) - kAoMargin - r <= thr;
+    const float len = norm(ab);
+    const float gr = 0.61803398875f;
+    float lo = 0.0f, hi = 1.0f;
+    float t1 = hi - gr * (hi - lo), t2 = lo + gr * (hi - lo);
+    float f1 = box_sd(A + t1 * ab, c, h), f2 = box_sd(A + t2 * ab, c, h);
+    for (int it = 0; it < 34; it++) {
+        const float fb = fminf(f1, f2);
+        if (fb <= lim) return true;
+        if (fb - len * (hi - lo) > lim) return false;
+        if (f1 <= f2) {
+            hi = t2; t2 = t1; f2 = f1;
+            t1 = hi - gr * (hi - lo);
+            f1 = box_sd(A + t1 * ab, c, h);
+        } else {
+            lo = t1; t1 = t2; f1 = f2;
+            t2 = lo + gr * (hi - lo);
+            f2 = box_sd(A + t2 * ab, c, h);
+        }
+    }
+    V3 P = A + 0.5f * (lo + hi) * ab;
+    float sd = box_sd(P, c, h);
+    if (sd > 0.0f) {
+        for (int it = 0; it < 2; it++) {
+            const V3 q = v3(fminf(fmaxf(P.x, c.x - h.x), c.x + h.x), fminf(fmaxf(P.y, c.y - h.y), c.y + h.y),
+                            fminf(fmaxf(P.z, c.z - h.z), c.z + h.z));
+            P = seg_closest(A, B, q);
+        }
+        sd = box_sd(P, c, h);
+    }
+    return sd - kAoMargin - r <= thr;
+}
+
 /* ------------------------------------------------------------- contacts */
 /* Restated in oracle/pgx_oracle.c ("world: object + contacts"): two contact groups
  * (object vs table/plane, robot vs table/plane/object) of at most CG points each, the
@@ -683,10 +828,52 @@ __device__ __forceinline__ void object_candidates(const PgxDevEnv& e, float tau,
     }
 }
 
+/* ReachAO: the obstacles are static colliders (create_obstacle_sphere / _cuboid,
+ * reach_ao.py:819-860: mass 0, not ghosts), so stepSimulation resolves robot contacts with
+ * them like the table's (oracle detect(), "ReachAO" branch): capsule c (wave-uniform) against
+ * each obstacle, one closest pair per pair within the processing threshold tau; the contact
+ * normal points from the obstacle to the robot, the point on the robot is P + r n.  The
+ * capsule-to-centre distance minus the radius / circumradius bounds the pair from below, so
+ * the exact query runs only for pairs that can be within tau. */
+template <class LT>
+__device__ __forceinline__ bool ao_capsule_near(LT& L, int ln, int c, float tau) {
+    const V3 A = lds3(L.capA[c], ln), B = lds3(L.capB[c], ln);
+    bool near = false;
+    for (int o = 0; o < AO_N; o++) {
+        const V3 C = lds3(L.aoC[o], ln);
+        const float dc = norm(C - seg_closest(A, B, C)) - kCapR[c] - (o < 3 ? kAoSize : kAoCubeBound);
+        near = near || dc < tau;
+    }
+    return near;
+}
+template <class LT>
+__device__ __forceinline__ void ao_obstacle_candidates(LT& L, int ln, int c, float tau) {
+    const V3 A = lds3(L.capA[c], ln), B = lds3(L.capB[c], ln);
+    const float r = kCapR[c];
+    const int jc = kCapJ[c];
+    const V3 hcube = v3(kAoSize, kAoSize, kAoSize);
+    for (int o = 0; o < AO_N; o++) {
+        const V3 C = lds3(L.aoC[o], ln);
+        const V3 P0 = seg_closest(A, B, C);
+        const V3 v = C - P0;
+        const float len = norm(v);
+        float d;
+        V3 P = P0, n;
+        if (o < 3) {
+            d = len - r - kAoSize;
+            n = len > 0.0f ? fast_rcp(len) * v : v3(0.0f, 0.0f, 1.0f);
+        } else {
+            if (!(len - r - kAoCubeBound < tau)) continue;
+            d = capsule_box_pair<true>(A, B, r, C, hcube, &P, &n);
+        }
+        if (d < tau) g1_insert(L, ln, d, (float)(32 + 6 * c + o), jc, P + r * n, (-1.0f) * n, v3(0.0f, 0.0f, 0.0f));
+    }
+}
+
 /* Robot capsules against the table/plane (end spheres) and the object (spheres sampled
  * along the axis), from the world end points the FK pass left in LDS.  A runtime loop
  * over the capsule table (wave-uniform index: scalar loads) keeps the code compact. */
-template <int OBJ, class LT>
+template <int OBJ, class LT, int AO = 0>
 __device__ __forceinline__ void robot_contacts(const PgxDevEnv& e, float tau, LT& L, int ln, const ObjState& ob,
                                             const M3& Rc) {
     for (int c = 0; c < PGX_NCAP; c++) {
@@ -704,6 +891,9 @@ __device__ __forceinline__ void robot_contacts(const PgxDevEnv& e, float tau, LT
             }
         }
         if (OBJ && (flags & PGX_CAP_VS_OBJECT)) object_candidates(e, tau, L, ln, ob, Rc, c, true);
+        /* flags 0: the base and panda_link1, whose capsule lies on the joint-1 axis and cannot
+         * move towards an obstacle (the reset keeps them 0.03 clear) */
+        if (AO && flags != 0 && ao_capsule_near(L, ln, c, tau)) ao_obstacle_candidates(L, ln, c, tau);
     }
 }
 
@@ -796,7 +986,7 @@ struct Dyn {
     V3 vcu, wcu;
 };
 
-template <int OBJ, int CONT, class LT, bool PAR = false>
+template <int OBJ, int CONT, class LT, bool PAR = false, int AO = 0>
 __device__ __forceinline__ void substep_dyn(MRef m, const PgxDevEnv& e, const float* q, const float* qd,
                                             const ObjState& ob, LT* Lp, int ln, Dyn& D, int lane = 0) {
     M3 Rc;
@@ -846,10 +1036,10 @@ __device__ __forceinline__ void substep_dyn(MRef m, const PgxDevEnv& e, const fl
         }
     }
     if (CONT) {
-        if constexpr (PAR && !OBJ) {
+        if constexpr (PAR && !OBJ && !AO) {
             robot_table_contacts_g(e, m.contact_dist, *Lp, ln, lane);
         } else {
-            robot_contacts<OBJ>(e, m.contact_dist, *Lp, ln, ob, Rc);
+            robot_contacts<OBJ, LT, AO>(e, m.contact_dist, *Lp, ln, ob, Rc);
             sort_groups(*Lp, ln);
         }
     }
@@ -1072,7 +1262,7 @@ __device__ __forceinline__ V3 mul_sym(const float* s, V3 v) {
  * f = z_c x (H - M o_c) and its angular momentum about o_c is n = I_o z_c with
  *   I_o z = I z - 2 (H.o) z + H (o.z) + o (H.z) + M (|o|^2 z - o (o.z)),
  * and M[c][i] = z_i . (n + (o_c - o_i) x f) for i <= c (CRBA), broadcast to every lane. */
-template <int OBJ, int CONT>
+template <int OBJ, int CONT, int AO = 0>
 __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const float* q, const float* qd,
                                               const ObjState& ob, ContactLdsG* Lp, int es, Dyn& D, int c,
                                               const LaneK& K) {
@@ -1140,6 +1330,28 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
     if (CONT) {
         if constexpr (!OBJ) {
             robot_table_contacts_g(e, m.contact_dist, *Lp, es, c);
+            if constexpr (AO) {
+                /* obstacle contacts (ao_obstacle_candidates): lane c culls capsule c against the
+                 * six obstacles; the capsules near one anywhere in the wave insert their pairs by
+                 * depth (g1_insert) after the table candidates, then id order, as robot_contacts
+                 * discovers them (only an exact depth tie of a table and an obstacle candidate
+                 * could order differently) */
+                const int cc = c < PGX_NCAP ? c : 0;
+                const bool near = c < PGX_NCAP && kCapFlags[cc] != 0 && ao_capsule_near(*Lp, es, cc, m.contact_dist);
+                const uint64_t bn = __ballot(near);
+                unsigned wm = (unsigned)((bn | (bn >> 16) | (bn >> 32) | (bn >> 48)) & 0xFFFFu);
+                if (wm) {
+                    const unsigned rm = row_ballot(near);
+                    sort_g1_by_depth(*Lp, es);
+                    wm = __builtin_amdgcn_readfirstlane(wm);
+                    while (wm) {
+                        const int cn = __builtin_ctz(wm);
+                        wm &= wm - 1u;
+                        if ((rm >> cn) & 1u) ao_obstacle_candidates(*Lp, es, cn, m.contact_dist);
+                    }
+                    sort_groups(*Lp, es);
+                }
+            }
         } else {
             PGX_PROF_MARK(20);
             /* robot_contacts' object cull per capsule lane; without a capsule in reach of the
@@ -1321,12 +1533,12 @@ __device__ __forceinline__ void object_integrate(MRef m, ObjState& ob, V3 v, V3 
     ob.qx = nx * inn; ob.qy = ny * inn; ob.qz = nz * inn; ob.qw = nw * inn;
 }
 
-template <int OBJ, int CONT>
+template <int OBJ, int CONT, int AO = 0>
 __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, float* qd, const float* tq,
                                         ObjState& ob, ContactLds* Lp, int ln) {
     MRef m = *fresh(mp);
     Dyn D;
-    substep_dyn<OBJ, CONT>(m, e, q, qd, ob, Lp, ln, D);
+    substep_dyn<OBJ, CONT, ContactLds, false, AO>(m, e, q, qd, ob, Lp, ln, D);
     const V3 (&z)[NJ] = D.z;
     const V3 (&o)[NJ] = D.o;
     const float (&Mi)[NJ][NJ] = D.Mi;
@@ -1769,12 +1981,12 @@ constexpr bool limit_rows_paired() {
     return (PGX_N_ROWS - NJ) % 2 == 0;
 }
 
-template <int OBJ, int CONT, int PART = 1>
+template <int OBJ, int CONT, int PART = 1, int AO = 0>
 __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q, float* qd, const float* tq,
                                           ObjState& ob, ContactLdsG* Lp, int es, int c, const LaneK& K) {
     MRef m = *fresh(mp);
     Dyn D;
-    substep_dyn_g<OBJ, CONT>(m, e, q, qd, ob, Lp, es, D, c, K);
+    substep_dyn_g<OBJ, CONT, AO>(m, e, q, qd, ob, Lp, es, D, c, K);
     const V3 (&z)[NJ] = D.z;
     const V3 (&o)[NJ] = D.o;
     const float (&vu)[NJ] = D.vu;
@@ -2535,140 +2747,6 @@ __device__ __forceinline__ void store_obj(const PgxDevState& s, int N, int i, co
  * :896-900); the observation's closest distance + unit vector per link (get_obs
  * "vectors+closest_per_link" :902-959).  Exact distances are evaluated only for pairs a
  * cheap bound cannot rule out: the capsule axis against the obstacle's bounding sphere. */
-constexpr int AO_N = PGX_AO_OBSTACLES;
-constexpr float kAoSize = 0.05f, kAoMargin = 0.001f, kAoDummyR = 0.05f;
-constexpr float kAoCubeBound = 0.0866025404f;   /* 0.05 * sqrt(3): cuboid circumradius */
-
-/* AO collision-link slot of each capsule (-1: base, hand) */
-__host__ __device__ constexpr int ao_slot(int c) {
-    return kCapLink[c] < 0 ? -1 : (kCapLink[c] <= 7 ? kCapLink[c] : (kCapLink[c] == 9 ? 8 : -1));
-}
-__device__ constexpr int kAoSlot[PGX_NCAP] = {ao_slot(0), ao_slot(1), ao_slot(2), ao_slot(3), ao_slot(4),
-                                              ao_slot(5), ao_slot(6), ao_slot(7), ao_slot(8), ao_slot(9),
-                                              ao_slot(10), ao_slot(11), ao_slot(12), ao_slot(13)};
-static_assert(PGX_NCAP == 14, "kAoSlot table");
-
-
-/* signed distance to the axis-aligned box (c, h) */
-__device__ __forceinline__ float box_sd(V3 P, V3 c, V3 h) {
-    const float dx = fabsf(P.x - c.x) - h.x, dy = fabsf(P.y - c.y) - h.y, dz = fabsf(P.z - c.z) - h.z;
-    const float ox = fmaxf(dx, 0.0f), oy = fmaxf(dy, 0.0f), oz = fmaxf(dz, 0.0f);
-    return fast_sqrt(ox * ox + oy * oy + oz * oz) + fminf(fmaxf(dx, fmaxf(dy, dz)), 0.0f);
-}
-
-/* closest point of segment AB to C */
-__device__ __forceinline__ V3 seg_closest(V3 A, V3 B, V3 C) {
-    const V3 ab = B - A;
-    const float l2 = dot(ab, ab);
-    float t = l2 > 0.0f ? dot(C - A, ab) / l2 : 0.0f;
-    t = fminf(fmaxf(t, 0.0f), 1.0f);
-    return A + t * ab;
-}
-
-/* capsule (A, B, r) vs rounded box (c, full half extents hf): a golden-section search
- * on the inner box's signed distance along the axis; the unit vector (from the
- * capsule's closest point to the box's, utils.unit_vector) when asked for */
-template <bool VEC>
-__device__ __forceinline__ float capsule_box(V3 A, V3 B, float r, V3 c, V3 hf, V3* u) {
-    const V3 h = v3(hf.x - kAoMargin, hf.y - kAoMargin, hf.z - kAoMargin);
-    const V3 ab = B - A;
-    float lo = 0.0f, hi = 1.0f;
-    const bool seg = dot(ab, ab) > 0.0f;
-    if (seg) {
-        /* golden-section search of the convex box_sd along the axis: one evaluation per step,
-         * 34 steps shrink [0, 1] to 0.618^34 = 8e-8 (the ternary search's 40 steps of two
-         * evaluations reach 9e-8) */
-        const float gr = 0.61803398875f;
-        float t1 = hi - gr * (hi - lo), t2 = lo + gr * (hi - lo);
-        float f1 = box_sd(A + t1 * ab, c, h), f2 = box_sd(A + t2 * ab, c, h);
-        for (int it = 0; it < 34; it++) {
-            if (f1 <= f2) {
-                hi = t2; t2 = t1; f2 = f1;
-                t1 = hi - gr * (hi - lo);
-                f1 = box_sd(A + t1 * ab, c, h);
-            } else {
-                lo = t1; t1 = t2; f1 = f2;
-                t2 = lo + gr * (hi - lo);
-                f2 = box_sd(A + t2 * ab, c, h);
-            }
-        }
-    }
-    V3 P = A + (seg ? 0.5f * (lo + hi) : 0.0f) * ab;
-    float sd = box_sd(P, c, h);
-    if (seg && sd > 0.0f) {
-        /* two alternating projections (box -> segment): the search cannot resolve t where
-         * the distance is flat to second order (a segment passing an edge or a corner);
-         * each can only shorten the pair and pins it */
-        for (int it = 0; it < 2; it++) {
-            const V3 q = v3(fminf(fmaxf(P.x, c.x - h.x), c.x + h.x), fminf(fmaxf(P.y, c.y - h.y), c.y + h.y),
-                            fminf(fmaxf(P.z, c.z - h.z), c.z + h.z));
-            P = seg_closest(A, B, q);
-        }
-        sd = box_sd(P, c, h);
-    }
-    const float d = sd - kAoMargin - r;
-    if (VEC) {
-        V3 n;
-        if (sd > 0.0f) {
-            const V3 q = v3(fminf(fmaxf(P.x, c.x - h.x), c.x + h.x), fminf(fmaxf(P.y, c.y - h.y), c.y + h.y),
-                            fminf(fmaxf(P.z, c.z - h.z), c.z + h.z));
-            const V3 v = q - P;
-            const float len = norm(v);
-            n = len > 0.0f ? fast_rcp(len) * v : v3(0.0f, 0.0f, 0.0f);
-        } else {   /* inside the inner box: out through the nearest face */
-            const float bx = fabsf(P.x - c.x) - h.x, by = fabsf(P.y - c.y) - h.y, bz = fabsf(P.z - c.z) - h.z;
-            const int ax = (bx >= by && bx >= bz) ? 0 : (by >= bz ? 1 : 2);
-            const float sx = P.x < c.x ? 1.0f : -1.0f, sy = P.y < c.y ? 1.0f : -1.0f, sz = P.z < c.z ? 1.0f : -1.0f;
-            n = v3(ax == 0 ? sx : 0.0f, ax == 1 ? sy : 0.0f, ax == 2 ? sz : 0.0f);
-        }
-        /* pb - pa = d * n */
-        *u = d > 0.0f ? n : (d < 0.0f ? (-1.0f) * n : v3(0.0f, 0.0f, 0.0f));
-    }
-    return d;
-}
-
-/* capsule_box(...) <= thr as a decision: the same golden-section search, stopped as soon as a
- * sample is within r + margin of the inner box (the minimum can only be lower) or the best
- * sample minus |AB| times the bracket width (f is |AB|-Lipschitz in t; the minimiser stays in
- * the bracket of a convex f) is farther than that (the minimum cannot reach it); the
- * undecided rest ends as capsule_box does. */
-__device__ __forceinline__ bool capsule_box_hit(V3 A, V3 B, float r, V3 c, V3 hf, float thr = 0.0f) {
-    const V3 h = v3(hf.x - kAoMargin, hf.y - kAoMargin, hf.z - kAoMargin);
-    const V3 ab = B - A;
-    const float lim = kAoMargin + r + thr;
-    if (!(dot(ab, ab) > 0.0f)) return box_sd(A, c, h) - kAoMargin - r <= thr;
-    const float len = norm(ab);
-    const float gr = 0.61803398875f;
-    float lo = 0.0f, hi = 1.0f;
-    float t1 = hi - gr * (hi - lo), t2 = lo + gr * (hi - lo);
-    float f1 = box_sd(A + t1 * ab, c, h), f2 = box_sd(A + t2 * ab, c, h);
-    for (int it = 0; it < 34; it++) {
-        const float fb = fminf(f1, f2);
-        if (fb <= lim) return true;
-        if (fb - len * (hi - lo) > lim) return false;
-        if (f1 <= f2) {
-            hi = t2; t2 = t1; f2 = f1;
-            t1 = hi - gr * (hi - lo);
-            f1 = box_sd(A + t1 * ab, c, h);
-        } else {
-            lo = t1; t1 = t2; f1 = f2;
-            t2 = lo + gr * (hi - lo);
-            f2 = box_sd(A + t2 * ab, c, h);
-        }
-    }
-    V3 P = A + 0.5f * (lo + hi) * ab;
-    float sd = box_sd(P, c, h);
-    if (sd > 0.0f) {
-        for (int it = 0; it < 2; it++) {
-            const V3 q = v3(fminf(fmaxf(P.x, c.x - h.x), c.x + h.x), fminf(fmaxf(P.y, c.y - h.y), c.y + h.y),
-                            fminf(fmaxf(P.z, c.z - h.z), c.z + h.z));
-            P = seg_closest(A, B, q);
-        }
-        sd = box_sd(P, c, h);
-    }
-    return sd - kAoMargin - r <= thr;
-}
-
 /* world end points of every capsule at q (base capsule included) into LDS */
 template <int C = 0, class LT>
 __device__ __forceinline__ void ao_caps_walk(const Chain& k, MRef m, LT& L, int ln) {
@@ -2917,8 +2995,9 @@ __device__ __noinline__ void ao_hollow_sphere(const PgxDevEnv& e, AoDraw& d, dou
  * obstacles by rejection against robot / table / dummy sphere, 4-5 active.  Needs the
  * neutral-pose capsules in LDS; leaves the centres in L.aoC. */
 template <bool PAR, class LT>
-__device__ __noinline__ void ao_reset(const PgxDevEnv& e, LT& L, int ln, int lane, uint64_t env, uint32_t episode, V3 ee,
+__device__ __noinline__ bool ao_reset(const PgxDevEnv& e, LT& L, int ln, int lane, uint64_t env, uint32_t episode, V3 ee,
                                       const double* inject_goal, const double* inject_obst, double* goal) {
+    bool failed = false;   /* set_coll_free_obs gave up: the reference raises StopIteration */
     AoDraw d{env, episode, 0};
     const V3 tc = ao_table_c(e), th = ao_table_h(e);
     double dummy[3] = {0.0, 0.0, 0.0};
@@ -2935,6 +3014,7 @@ __device__ __noinline__ void ao_reset(const PgxDevEnv& e, LT& L, int ln, int lan
     const V3 dm = v3((float)dummy[0], (float)dummy[1], (float)dummy[2]);
     for (int o = 0; o < AO_N; o++) {
         double P[3];
+        bool placed = false;
         for (int it = 0; it < 10000; it++) {
             const double rnd = ao_draw(e, d);
             double sm[3];
@@ -2953,8 +3033,9 @@ __device__ __noinline__ void ao_reset(const PgxDevEnv& e, LT& L, int ln, int lan
                        kAoDummyR;
             }
             const bool coll = dtab <= 0.03f || ddum <= 0.03f || ao_robot_hit<PAR>(L, ln, lane, o < 3 ? 0 : 1, Pf, kAoSize, 0.03f);
-            if (!coll) break;
+            if (!coll) { placed = true; break; }
         }
+        failed = failed || !placed;
         L.aoC[o][0][ln] = (float)P[0]; L.aoC[o][1][ln] = (float)P[1]; L.aoC[o][2][ln] = (float)P[2];
     }
     const int n_active = 4 + (int)(ao_draw(e, d) * 2.0);
@@ -2977,6 +3058,7 @@ __device__ __noinline__ void ao_reset(const PgxDevEnv& e, LT& L, int ln, int lan
     if (inject_obst)
         for (int o = 0; o < AO_N; o++)
             for (int k = 0; k < 3; k++) L.aoC[o][k][ln] = (float)inject_obst[3 * o + k];
+    return failed && !inject_obst;
 }
 
 template <class LT>
@@ -3090,8 +3172,8 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     const int n_substeps = m.n_substeps;
     bool collided = false;
     for (int st = 0; st < n_substeps; st++) {
-        if constexpr (WIDE) substep_g<OBJ, CONT, PART>(mp, e, q, qd, tq, ob, L, ln, c, lk);
-        else substep<OBJ, CONT>(mp, e, q, qd, tq, ob, L, ln);
+        if constexpr (WIDE) substep_g<OBJ, CONT, PART, AO>(mp, e, q, qd, tq, ob, L, ln, c, lk);
+        else substep<OBJ, CONT, AO>(mp, e, q, qd, tq, ob, L, ln);
         if constexpr (AO) {   /* ReachAO step_check_collision: check after every substep, stop on contact */
             ao_caps(*fresh(mp), q, *L, ln);
             const bool hit = WIDE ? ao_collided_g(e, *L, ln, c) : ao_collided(e, *L, ln);
@@ -3150,7 +3232,9 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
             for (int j = 0; j < NJ; j++) { q[j] = mr.neutral_q[j]; qd[j] = 0.0f; }
             ee_state(mr, q, qd, pos, vel);
             ao_caps(mr, q, *L, ln);
-            ao_reset<WIDE != 0>(e, *L, ln, c, e.env_id_offset + (uint64_t)i, episode, pos, nullptr, nullptr, goal);
+            if (ao_reset<WIDE != 0>(e, *L, ln, c, e.env_id_offset + (uint64_t)i, episode, pos, nullptr, nullptr, goal) &&
+                lead)
+                atomicOr(s.errors, PGX_ERR_AO_OBSTACLE);
             episode += 1;
             if constexpr (WIDE) ao_link_obs_g(*L, ln, c);
             else ao_link_obs(*L, ln);
@@ -3246,9 +3330,10 @@ __global__ __launch_bounds__(64) void reset_kernel(const PgxDevModel* __restrict
         for (int j = 0; j < NJ; j++) { q[j] = m.neutral_q[j]; qd[j] = 0.0f; }
         ee_state(m, q, qd, pos, vel);
         ao_caps(m, q, *L, ln);
-        ao_reset<false>(e, *L, ln, 0, e.env_id_offset + (uint64_t)i, episode, pos,
-                 inject_goal ? inject_goal + 3 * (size_t)i : nullptr,
-                 inject_obj ? inject_obj + 3 * AO_N * (size_t)i : nullptr, goal);
+        if (ao_reset<false>(e, *L, ln, 0, e.env_id_offset + (uint64_t)i, episode, pos,
+                            inject_goal ? inject_goal + 3 * (size_t)i : nullptr,
+                            inject_obj ? inject_obj + 3 * AO_N * (size_t)i : nullptr, goal))
+            atomicOr(s.errors, PGX_ERR_AO_OBSTACLE);
         episode += 1;
         ao_link_obs(*L, ln);
     } else {

@@ -245,7 +245,23 @@ class PandaVecEnv:
                if v.obstacles else {}),
             "elapsed": _view(v.elapsed, (n,), torch.int32, self.device),
             "episode": _view(v.episode, (n,), torch.int32, self.device),
+            "errors": _view(v.errors, (1,), torch.int32, self.device),
         }
+
+    def raise_device_errors(self, errors: Optional[int] = None) -> None:
+        """Raise what the kernels flagged (pgx_state_view.errors) and clear it.  The device path
+        (step_tensors / reset_tensors) never synchronises to look; the SB3 path (reset,
+        step_wait) looks at every call.  PGX_ERR_AO_OBSTACLE: ReachAO.set_coll_free_obs raises
+        StopIteration after 10000 rejected obstacle draws (reach_ao.py:1143-1145)."""
+        err = self.state()["errors"]
+        if errors is None:
+            errors = int(err.item())
+        if errors:
+            err.zero_()
+            if errors & abi.ERR_AO_OBSTACLE:
+                raise PgxError("Couldn't find collision free obstacle! (device reset of a ReachAO env gave up "
+                               "after 10000 obstacle draws; reach_ao.py:1143-1145 raises StopIteration)")
+            raise PgxError(f"device error flags 0x{errors:x}")
 
     def _obs_dict(self) -> Dict[str, torch.Tensor]:
         return {"observation": self.obs, "achieved_goal": self.achieved_goal, "desired_goal": self.desired_goal}
@@ -304,6 +320,7 @@ class PandaVecEnv:
             seed = self._pending_seed
         self._pending_seed = None
         self.reset_tensors(seed=seed)
+        self.raise_device_errors()
         return self._numpy_obs()
 
     def seed(self, seed: Optional[int] = None) -> List[Optional[int]]:
@@ -327,6 +344,7 @@ class PandaVecEnv:
                 "flags_dev": torch.empty((4, n), dtype=torch.uint8, device=self.device),
                 "t_observation": torch.empty((n, od), **pin), "t_achieved_goal": torch.empty((n, 3), **pin),
                 "t_desired_goal": torch.empty((n, 3), **pin),
+                "errors": torch.zeros(1, dtype=torch.int32, pin_memory=True),
             }
         return self._hs
 
@@ -359,9 +377,11 @@ class PandaVecEnv:
         for k, src in (("observation", obs["observation"]), ("achieved_goal", obs["achieved_goal"]),
                        ("desired_goal", obs["desired_goal"]), ("reward", rew), ("flags", fd),
                        ("t_observation", self.terminal_obs), ("t_achieved_goal", self.terminal_ag),
-                       ("t_desired_goal", self.terminal_dg)):
+                       ("t_desired_goal", self.terminal_dg), ("errors", self.state()["errors"])):
             hs[k].copy_(src, non_blocking=True)
         stream.synchronize()
+        if hs["errors"].item():
+            self.raise_device_errors(int(hs["errors"].item()))
         # copies: the pinned mirrors are overwritten by the next step
         o = {k: hs[k].numpy().copy() for k in ("observation", "achieved_goal", "desired_goal")}
         r = hs["reward"].numpy().copy()
@@ -478,6 +498,7 @@ class PandaEnv:
             self._vec.reset_tensors()
         else:
             self._vec.reset_tensors(goals=r[0][None, :], objects=None if r[1] is None else r[1][None, :])
+        self._vec.raise_device_errors()
         obs = self._vec._numpy_obs()
         obs = {k: v[0] for k, v in obs.items()}
         return obs, {"is_success": bool(self._vec.success[0].item())}

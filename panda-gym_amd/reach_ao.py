@@ -164,6 +164,8 @@ def reset_draws(rng: np.random.Generator, geom: RobotGeometry) -> Tuple[np.ndarr
             obst[o] = P
             if not any(coll):
                 break
+        else:   # set_coll_free_obs (reach_ao.py:1143-1145): the 10001st attempt raises
+            raise StopIteration("Couldn't find collision free obstacle!")
     n_active = int(rng.integers(4, 6))
     keys = list(range(6))
     rng.shuffle(keys)

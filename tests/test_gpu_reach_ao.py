@@ -36,6 +36,16 @@ def pg():
     return pg
 
 
+def _in_path(ee, kind=3):
+    """Obstacles with one of ``kind`` (3: a cuboid, 0: a sphere) in the path of joint 1 swinging
+    towards +y: the cuboid 6 cm below the EE meets the tool bar (panda_ee, a collision link), the
+    sphere at EE height meets panda_hand first (not a collision link: it blocks without a
+    collision); the rest parked."""
+    obst = np.array([[99.9, 99.9, -99.9]] * 6)
+    obst[kind] = np.asarray(ee) + (np.array([0.0, 0.14, -0.06]) if kind == 3 else np.array([0.0, 0.14, 0.0]))
+    return obst
+
+
 def _obs(venv):
     return venv.obs.cpu().numpy(), venv.achieved_goal.cpu().numpy(), venv.desired_goal.cpu().numpy()
 
@@ -130,34 +140,79 @@ def test_one_step_parity_random_actions(pg, oracle, lanes):
 
 
 def test_collision_truncates_with_penalty(pg, oracle, lanes):
+    """The tool bar driven into a cuboid: the obstacle is a static collider, so the contact rows
+    hold the bar at the surface (oracle: test_collision_link_contact_truncates_at_the_surface)
+    and check_collided's min distance <= 0 registers there.  The substep at which the distance,
+    held at rounding level, first reads <= 0 is decided by rounding, so the device and the fp64
+    oracle need not truncate in the same step; each must truncate with -1 - 100 while touching."""
     n = 4
     venv = pg.PandaVecEnv(ENV, num_envs=n, device="cuda:0", seed=1, lanes_per_env=lanes)
     from oracle.oracle import fk
 
     com, _, _ = fk(venv._cfg.model.contents, np.array(pg.abi.NEUTRAL_Q[:7]))
-    ee = com[11]
-    obst = np.array([[ee[0], ee[1] + 0.14, ee[2]]] + [[99.9, 99.9, -99.9]] * 5)
+    obst = _in_path(com[11])
     goals = np.tile([[0.5, 0.3, 0.3]], (n, 1))
     venv.reset_tensors(goals=goals, objects=np.tile(obst[None], (n, 1, 1)))
     ref = oracle.OracleVecEnv(venv._cfg, n)
     ref.reset(inject_goal=goals, inject_obj=np.tile(obst[None], (n, 1, 1)))
     a = np.zeros((n, 7), np.float32)
     a[:, 0] = 1.0
-    hit = None
-    for k in range(10):
+    hit, hit_ref = None, None
+    for k in range(12):
+        if hit is None:
+            venv.step_tensors(torch.as_tensor(a, device="cuda:0"))
+            tr = venv.truncated.cpu().numpy().astype(bool)
+            assert tr.all() or not tr.any(), k      # identical envs
+            if tr.all():
+                hit = k
+                assert np.all(venv.reward.cpu().numpy() == -101.0)
+                assert not venv.terminated.cpu().numpy().any()
+                tobs = venv.terminal_obs.cpu().numpy()
+                assert np.abs(tobs[:, 20:29].min(1)).max() <= 1e-4     # at the surface, not through it
+                assert np.all(venv.obs.cpu().numpy()[:, 13:20] == 0)   # auto-reset to the neutral pose
+        if hit_ref is None:
+            out = ref.step(a)
+            if out["truncated"].all():
+                hit_ref = k
+    assert hit is not None and hit_ref is not None
+    assert abs(hit - hit_ref) <= 2, (hit, hit_ref)
+    venv.close()
+
+
+def test_obstacle_contact_blocks_the_arm(pg, oracle, lanes):
+    """A sphere in the path of panda_hand (not a check_collided link): the arm is stopped at the
+    surface by the contact rows, on the device as in the oracle, and never truncated."""
+    from oracle.oracle import ao_capsule_sphere, fk
+
+    n = 4
+    venv = pg.PandaVecEnv(ENV, num_envs=n, device="cuda:0", seed=1, lanes_per_env=lanes)
+    m = venv._cfg.model.contents
+    com, _, _ = fk(m, np.array(pg.abi.NEUTRAL_Q[:7]))
+    obst = _in_path(com[11], kind=0)
+    goals = np.tile([[0.5, 0.3, 0.3]], (n, 1))
+    venv.reset_tensors(goals=goals, objects=np.tile(obst[None], (n, 1, 1)))
+    ref = oracle.OracleVecEnv(venv._cfg, n)
+    ref.reset(inject_goal=goals, inject_obj=np.tile(obst[None], (n, 1, 1)))
+    a = np.zeros((n, 7), np.float32)
+    a[:, 0] = 1.0
+    for k in range(25):
         venv.step_tensors(torch.as_tensor(a, device="cuda:0"))
-        out = ref.step(a)
-        tr = venv.truncated.cpu().numpy().astype(bool)
-        assert np.array_equal(tr, out["truncated"].astype(bool)), k
-        if tr.all():
-            hit = k
-            break
-    assert hit is not None
-    assert np.all(venv.reward.cpu().numpy() == -101.0)
-    assert not venv.terminated.cpu().numpy().any()
-    tobs = venv.terminal_obs.cpu().numpy()
-    assert tobs[:, 20:29].min() <= 1e-3
-    assert np.all(venv.obs.cpu().numpy()[:, 13:20] == 0)          # auto-reset to the neutral pose
+        ref.step(a)
+        assert not venv.truncated.cpu().numpy().any(), k
+    q = venv.state()["q"].cpu().numpy().T.astype(np.float64)
+
+    def hand_d(qe):
+        _, rot, org = fk(m, qe)
+        li = m.cap_link[12]   # panda_hand's capsule
+        A = org[li] + rot[li] @ np.array(m.cap_a[12])
+        B = org[li] + rot[li] @ np.array(m.cap_b[12])
+        return ao_capsule_sphere(A, B, m.cap_radius[12], obst[0], 0.05)[0]
+
+    d_dev = [hand_d(qe) for qe in q]
+    d_ref = hand_d(ref.q[0])
+    assert all(-1e-4 <= d <= 1e-3 for d in d_dev), d_dev
+    assert -1e-5 <= d_ref <= 1e-3, d_ref
+    assert np.abs(q[:, 0] - ref.q[0, 0]).max() <= 1e-3
     venv.close()
 
 
@@ -213,7 +268,7 @@ def test_single_env_collision_and_success_keep_terminal_state(pg):
     v = env._vec
     com, _, _ = fk(v._cfg.model.contents, np.array(pg.abi.NEUTRAL_Q[:7]))
     ee = com[11]
-    obst = np.array([[ee[0], ee[1] + 0.14, ee[2]]] + [[99.9, 99.9, -99.9]] * 5)
+    obst = _in_path(ee)
     v.reset_tensors(goals=np.array([[0.5, 0.3, 0.3]]), objects=obst[None])
     a = np.zeros(7, np.float32)
     a[0] = 1.0
@@ -223,7 +278,7 @@ def test_single_env_collision_and_success_keep_terminal_state(pg):
             break
         assert info["is_truncated"] is False and r == -1.0
     assert trunc and info["is_truncated"] is True and r == -101.0 and not term
-    assert obs["observation"][20:29].min() <= 1e-3                 # the colliding state, not a reset
+    assert abs(obs["observation"][20:29].min()) <= 1e-4            # the colliding state, not a reset
     assert np.abs(obs["observation"][13:20]).max() > 0.0
     st = v.state()
     assert int(st["elapsed"][0].item()) == k + 1
@@ -244,7 +299,7 @@ def test_vec_env_infos_is_truncated_on_collision(pg):
 
     com, _, _ = fk(venv._cfg.model.contents, np.array(pg.abi.NEUTRAL_Q[:7]))
     ee = com[11]
-    obst = np.array([[ee[0], ee[1] + 0.14, ee[2]]] + [[99.9, 99.9, -99.9]] * 5)
+    obst = _in_path(ee)
     far = np.array([[99.9, 99.9, -99.9]] * 6)
     objs = np.stack([obst, far, obst, far])
     venv.reset_tensors(goals=np.tile([[0.5, 0.3, 0.3]], (n, 1)), objects=objs)
@@ -275,7 +330,7 @@ def test_is_truncated_is_the_collision_flag_for_any_collision_reward(pg, collisi
     venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=1)
     com, _, _ = fk(venv._cfg.model.contents, np.array(pg.abi.NEUTRAL_Q[:7]))
     ee = com[11]
-    obst = np.array([[ee[0], ee[1] + 0.14, ee[2]]] + [[99.9, 99.9, -99.9]] * 5)
+    obst = _in_path(ee)
     far = np.array([[99.9, 99.9, -99.9]] * 6)
     venv.reset_tensors(goals=np.tile([[0.5, 0.3, 0.3]], (n, 1)), objects=np.stack([obst, far, obst, far]))
     a = np.zeros((n, 7), np.float32)
@@ -290,3 +345,30 @@ def test_is_truncated_is_the_collision_flag_for_any_collision_reward(pg, collisi
     assert rew.tolist() == [-1.0 + collision_reward, -1.0, -1.0 + collision_reward, -1.0]
     venv.close()
     del pg.envs._REGISTRY[env_id]
+
+
+def test_obstacle_sampling_failure_raises(pg, monkeypatch):
+    """The device reset of set_coll_free_obs gives up after 10000 draws like the reference, which
+    raises StopIteration there (reach_ao.py:1143-1145): the kernel sets PGX_ERR_AO_OBSTACLE in the
+    handle's errors word, the SB3 path (reset / step_wait) raises PgxError on it, the device path
+    leaves it for raise_device_errors().  A table swallowing the workspace makes every draw fail."""
+    make_config = pg.abi.make_config
+
+    def huge_table(*a, **k):
+        c = make_config(*a, **k)
+        for i in range(3):
+            c.table_half[i] = 10.0
+        return c
+
+    monkeypatch.setattr(pg.abi, "make_config", huge_table)
+    venv = pg.PandaVecEnv(ENV, num_envs=2, device="cuda:0", seed=1)
+    monkeypatch.undo()
+    venv.state()["errors"].zero_()        # the construction reset already failed
+    venv.reset_tensors()                  # device path: flagged, not raised
+    assert int(venv.state()["errors"].item()) == pg.abi.ERR_AO_OBSTACLE
+    with pytest.raises(pg.PgxError, match="collision free obstacle"):
+        venv.raise_device_errors()
+    assert int(venv.state()["errors"].item()) == 0
+    with pytest.raises(pg.PgxError, match="collision free obstacle"):
+        venv.reset()
+    venv.close()

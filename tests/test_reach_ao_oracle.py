@@ -169,29 +169,67 @@ def test_oracle_injected_reset(oracle):
     assert np.array_equal(env.active[0], [1, 0, 1, 1, 1, 0])
 
 
-def test_collision_truncates_with_penalty(oracle):
-    """An obstacle right in front of the moving link: the substep loop stops at the first
-    contact, the step is truncated with reward -1 - 100 and the env auto-resets."""
+def _push_into_obstacle(cfg, kind, offset, steps=30):
+    """Reset with one obstacle of ``kind`` (0 sphere, 3 cuboid) at EE + offset, then drive joint 1
+    towards +y at full action; returns the per-step outputs and the env."""
     from oracle import oracle as O
 
-    cfg = _cfg(n=1)
     env = O.OracleVecEnv(cfg, 1)
     q0 = np.array(abi.NEUTRAL_Q[:7])
-    from oracle.oracle import fk
-    com, rot, org = fk(cfg.model.contents, q0)
-    ee = com[11]
-    obst = np.array([[ee[0], ee[1] + 0.14, ee[2]]] + [[99.9, 99.9, -99.9]] * 5)
+    com, _, _ = O.fk(cfg.model.contents, q0)
+    obst = np.array([[99.9, 99.9, -99.9]] * 6)
+    obst[kind] = com[11] + np.asarray(offset)
     env.reset(inject_goal=np.array([[0.5, 0.3, 0.3]]), inject_obj=obst[None])
-    first = None
-    for k in range(10):
+    outs = []
+    for _ in range(steps):
         b = env.step(np.array([[1.0, 0, 0, 0, 0, 0, 0]], np.float32))   # swing joint 1 towards +y
+        outs.append((b, env.q[0].copy(), env.qd[0].copy()))
         if b["truncated"][0]:
-            first = k
             break
-    assert first is not None
-    assert b["reward"][0] == -101.0 and not b["terminated"][0]
-    assert b["terminal_obs"][0, 20:29].min() <= 1e-3          # the terminal obs touches the obstacle
-    assert np.all(b["obs"][0, 13:20] == 0)                     # auto-reset: neutral pose at rest
+    return outs, env, obst
+
+
+def _capsule_obstacle_distance(cfg, q, cap, centre, kind):
+    """Distance of capsule ``cap`` of the model (world end points at q) to the obstacle."""
+    from oracle import oracle as O
+
+    m = cfg.model.contents
+    com, rot, org = O.fk(m, q)
+    li = m.cap_link[cap]
+    A = org[li] + rot[li] @ np.array(m.cap_a[cap])
+    B = org[li] + rot[li] @ np.array(m.cap_b[cap])
+    if kind < 3:
+        return O.ao_capsule_sphere(A, B, m.cap_radius[cap], centre, 0.05)[0]
+    return O.ao_capsule_box(A, B, m.cap_radius[cap], centre, np.full(3, 0.05))[0]
+
+
+def test_obstacle_contact_stops_the_hand_at_the_surface(oracle):
+    """The obstacles are static colliders (reach_ao.py:819-860, mass 0), so a link driven into one
+    is stopped at its surface by the contact rows.  A sphere 0.14 m beside the EE meets
+    panda_hand first, which is not one of check_collided's links (reach_ao.py:896-900): the arm
+    stays blocked at the surface and the episode is not truncated."""
+    cfg = _cfg(n=1)
+    outs, env, obst = _push_into_obstacle(cfg, 0, [0.0, 0.14, 0.0])
+    assert not any(b["truncated"][0] for b, _, _ in outs)
+    hand = 12   # model.capsules: panda_hand
+    d = [_capsule_obstacle_distance(cfg, q, hand, obst[0], 0) for _, q, _ in outs]
+    assert min(d) >= -1e-5, min(d)                 # never through (a substep travels ~6e-4)
+    assert max(d[-10:]) <= 1e-3, d[-10:]           # resting on it
+    assert abs(outs[-1][2][0]) < 0.05              # joint 1 stalled against the motor
+
+
+def test_collision_link_contact_truncates_at_the_surface(oracle):
+    """The tool bar (panda_ee, a collision link) driven into a cuboid: the contact holds it at
+    the surface and check_collided's min distance <= 0 registers there -- the terminal
+    observation's distance is at rounding level (not a substep's travel inside the box) --
+    truncating the step with reward -1 - 100 and auto-resetting the env."""
+    cfg = _cfg(n=1)
+    outs, env, obst = _push_into_obstacle(cfg, 3, [0.0, 0.14, -0.06])
+    b = outs[-1][0]
+    assert b["truncated"][0] and b["reward"][0] == -101.0 and not b["terminated"][0]
+    dmin = b["terminal_obs"][0, 20:29].min()
+    assert -1e-5 <= dmin <= 0.0, dmin
+    assert np.all(b["obs"][0, 13:20] == 0)         # auto-reset: neutral pose at rest
 
 
 def test_success_terminates(oracle):
@@ -231,7 +269,8 @@ def test_no_auto_reset_keeps_the_terminal_state(oracle):
     env = O.OracleVecEnv(cfg, 1)
     com, _, _ = fk(cfg.model.contents, np.array(abi.NEUTRAL_Q[:7]))
     ee = com[11]
-    obst = np.array([[ee[0], ee[1] + 0.14, ee[2]]] + [[99.9, 99.9, -99.9]] * 5)
+    # a cuboid in the tool bar's path (_push_into_obstacle): held at the surface, then check_collided
+    obst = np.array([[99.9, 99.9, -99.9]] * 3 + [[ee[0], ee[1] + 0.14, ee[2] - 0.06]] + [[99.9, 99.9, -99.9]] * 2)
     env.reset(inject_goal=np.array([[0.5, 0.3, 0.3]]), inject_obj=obst[None])
     ep0 = int(env.episode[0])
     for k in range(10):
@@ -240,7 +279,7 @@ def test_no_auto_reset_keeps_the_terminal_state(oracle):
             break
     assert b["truncated"][0] and b["reward"][0] == -101.0
     assert np.array_equal(b["obs"], b["terminal_obs"])          # no reset in between
-    assert b["obs"][0, 20:29].min() <= 1e-3 and np.abs(b["obs"][0, 13:20]).max() > 0
+    assert abs(b["obs"][0, 20:29].min()) <= 1e-5 and np.abs(b["obs"][0, 13:20]).max() > 0
     assert env.elapsed[0] == k + 1 and env.episode[0] == ep0
     # TimeLimit without auto-reset: truncated at max_episode_steps, the state is kept
     cfg2 = _cfg(n=1)
@@ -250,3 +289,25 @@ def test_no_auto_reset_keeps_the_terminal_state(oracle):
     env2.reset(inject_goal=np.array([[0.5, 0.3, 0.3]]), inject_obj=far[None])
     tr = [bool(env2.step(np.zeros((1, 7), np.float32))["truncated"][0]) for _ in range(3)]
     assert tr == [False, False, True] and env2.elapsed[0] == 3
+
+
+def test_obstacle_sampling_failure_is_flagged(oracle, monkeypatch):
+    """set_coll_free_obs raises StopIteration on its 10001st attempt (reach_ao.py:1143-1145);
+    set_coll_free_goal falls back to the EE position (:1107-1115).  A table that swallows the
+    whole workspace makes every draw collide: the host's seeded reset raises StopIteration, the
+    oracle's device-stream reset sets PGX_ERR_AO_OBSTACLE (what the kernel writes to the handle's
+    errors word) and keeps the EE as the goal."""
+    from oracle import oracle as O
+
+    cfg = _cfg(n=1)
+    for i in range(3):
+        cfg.table_half[i] = 10.0
+    env = O.OracleVecEnv(cfg, 1)
+    assert env.take_errors() == 0
+    b = env.reset()
+    assert env.take_errors() == abi.ERR_AO_OBSTACLE
+    assert env.take_errors() == 0                               # taking clears it
+    assert np.allclose(b["dg"][0], b["ag"][0])                  # goal = EE position
+    monkeypatch.setattr(reach_ao, "TABLE_HALF", np.array([10.0, 10.0, 10.0]))
+    with pytest.raises(StopIteration, match="collision free obstacle"):
+        reach_ao.seeded_reset(0, reach_ao.RobotGeometry(load_model("panda_custom0")))
