@@ -150,6 +150,8 @@ typedef struct pgx_sim_params {
 #define PGX_FLAG_CONSTRAINT_PASS_BIAS 1   /* re-apply velocity bias in the constraint pass */
 #define PGX_FLAG_IK_COM 2                 /* IK targets the link COM instead of the joint pivot */
 #define PGX_FLAG_NO_RESIDUAL_EXIT 4       /* run all solver iterations */
+#define PGX_FLAG_LINKSTATE_CURRENT 8      /* getLinkState reports the pose after the last substep
+                                             instead of Bullet's cached pose (rejected hypothesis) */
 
 typedef struct pgx_config {
     int32_t task;                 /* PGX_TASK_* */
@@ -226,6 +228,8 @@ typedef struct pgx_step_out {
 typedef struct pgx_state_view {
     float* q;           /* [n_dofs][N] */
     float* qd;          /* [n_dofs][N] */
+    float* qc;          /* [n_dofs][N] pose of Bullet's cached link transforms, which getLinkState
+                           reports (EE obs, IK target): the pose the last substep started from */
     double* goal;       /* [3][N] */
     float* object;      /* [13][N] pos3, quat4 (x,y,z,w), linvel3, angvel3 */
     float* contacts;    /* [2*PGX_CONTACT_SLOTS][N] warm-start cache: (id, normal impulse) per slot */

@@ -79,7 +79,9 @@ class PgxoStats(C.Structure):
                 ("limits_far", C.c_int32), ("n_contacts", C.c_int32)]
 
 
-OBJ_N = 53   # pos3 quat4 linvel3 angvel3 + 8 x (contact feature id, normal impulse) + ReachAO obstacles
+OBJ_N = 60   # pos3 quat4 linvel3 angvel3 + 8 x (contact feature id, normal impulse) + ReachAO obstacles
+#              + the cached link pose qc[7] (getLinkState's pose: before the last substep)
+OBJ_QC = 53
 OBJ_AO = 29  # ReachAO: obstacle centres [6][3] at OBJ_AO, active flags [6] at OBJ_AO + 18
 
 
@@ -225,7 +227,7 @@ class OracleVecEnv:
         self.goal = np.zeros((n, 3))
         self.obj = np.zeros((n, OBJ_N))
         self.obj[:, 6] = 1.0
-        self.obj[:, 13::2] = -1.0
+        self.obj[:, 13:29:2] = -1.0
         self.elapsed = np.zeros(n, dtype=np.int32)
         self.episode = np.zeros(n, dtype=np.uint32)
 
@@ -265,6 +267,11 @@ class OracleVecEnv:
     def obstacles(self) -> np.ndarray:
         """ReachAO obstacle centres [n, 6, 3] (a view)."""
         return self.obj[:, OBJ_AO:OBJ_AO + 18].reshape(self.n, 6, 3)
+
+    @property
+    def qc(self) -> np.ndarray:
+        """The cached link pose [n, 7] getLinkState reports (a view)."""
+        return self.obj[:, OBJ_QC:OBJ_QC + 7]
 
     @property
     def active(self) -> np.ndarray:

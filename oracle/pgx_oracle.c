@@ -350,9 +350,11 @@ static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x >
  * I w (k + k|w|), the base bias term m (w x v) (computeAccelerations...MultiDof:
  * "zeroAccSpatFrc[0].addLinear(m_baseMass * omega.cross(vel))"), gyroscopic w x I w
  * (zero for a cube); orientation by the exponential map (stepPositionsMultiDof). */
-#define OBJ_N 53              /* pos3 quat4 (x,y,z,w) linvel3 angvel3 + 8 x (id, impulse)
-                                 + ReachAO obstacles: centres 6 x 3, active flags 6 */
+#define OBJ_N 60              /* pos3 quat4 (x,y,z,w) linvel3 angvel3 + 8 x (id, impulse)
+                                 + ReachAO obstacles: centres 6 x 3, active flags 6
+                                 + the cached link pose qc[7] (below) */
 #define OBJ_AO 29
+#define OBJ_QC 53
 static void quat_mul(const double* a, const double* b, double* o);
 #define NC_MAX PGX_CONTACT_SLOTS
 
@@ -1020,23 +1022,50 @@ static void quat_to_euler(const double* q, double* rpy) {
 /* RobotTaskEnv._get_obs (core.py:286-296): robot obs (panda.py:264-288) + task obs
  * (push.py:49-63 / pick_and_place.py:52-59: object position, euler, velocity, angular
  * velocity); achieved goal = EE position (Reach) or object position (Push/PnP). */
-static void ao_obs(const pgx_config* c, const double* q, const double* qd, const double* goal, const double* obst,
-                   float* obs, float* ag, float* dg);
+static void ao_obs(const pgx_config* c, const double* q, const double* qd, const double* qc, const double* goal,
+                   const double* obst, float* obs, float* ag, float* dg);
 static void ao_reset_one(const pgx_config* c, int64_t e, const double* inject_goal, const double* inject_obst,
                          double* q, double* qd, double* goal, double* obj, int32_t* elapsed, uint32_t* episode);
 static int ao_collided(const pgx_config* c, const double* q, const double* obst);
 
+/* getLinkState(ee_link, computeLinkVelocity=1) (PyBullet.get_link_position / _velocity,
+ * pybullet.py:249-286; Panda.get_ee_position / _velocity, panda.py:306-312) without
+ * computeForwardKinematics reads the link's cached world transform, which Bullet refreshes
+ * (btMultiBodyDynamicsWorld::forwardKinematics) before the constraint solve of each
+ * stepSimulation -- i.e. at the pose qc *before* the last substep's position update -- and
+ * turns the link's local velocity (compTreeLinkVelocities: the current q and qd) into world
+ * coordinates with that cached rotation.  resetJointState refreshes it (qc = q).  So:
+ *   position = COM of the link at qc,  velocity = R(qc) R(q)^T v(q, qd).
+ * Pinned by the reference's own known answers (test/pybullet_test.py:139-170): after one
+ * env step of joint 6, link 5's orientation [0.707, -0.02, 0.02, 0.707] and COM velocity
+ * [-0.0068, 0, 0.1186] are those of the cached pose (q of substep 19: y = -0.02005,
+ * v_x = -0.00677), while the joint angle (:190-204, getJointState: current) is 0.063 --
+ * the three answers are inconsistent with link states at the current pose (y -0.0222,
+ * v_x -0.0075).  tests/test_oracle_known_answers.py. */
+static void link_state_cached(const pgx_config* c, const double* q, const double* qd, const double* qc, int link,
+                              double pos[3], double vel[3]) {
+    const pgx_model* m = c->model;
+    if (c->params->flags & PGX_FLAG_LINKSTATE_CURRENT) qc = q;
+    kin_t k, kc;
+    fk(m, c->base_pos, q, &k);
+    fk(m, c->base_pos, qc, &kc);
+    double v[3], w[3], vl[3];
+    link_vel(m, &k, qd, link, v, w);
+    for (int i = 0; i < 3; i++)   /* R(q)^T v: the local velocity */
+        vl[i] = k.R[link][i] * v[0] + k.R[link][3 + i] * v[1] + k.R[link][6 + i] * v[2];
+    m3_v(kc.R[link], vl, vel);
+    memcpy(pos, kc.p[link], 3 * sizeof(double));
+}
+
 static void env_obs(const pgx_config* c, const double* q, const double* qd, const double* goal, const double* obj,
                     float* obs, float* ag, float* dg) {
-    if (c->task == PGX_TASK_REACH_AO) { ao_obs(c, q, qd, goal, obj + OBJ_AO, obs, ag, dg); return; }
+    if (c->task == PGX_TASK_REACH_AO) { ao_obs(c, q, qd, obj ? obj + OBJ_QC : q, goal, obj + OBJ_AO, obs, ag, dg); return; }
     const pgx_model* m = c->model;
-    kin_t k;
-    fk(m, c->base_pos, q, &k);
-    double v[3], w[3];
-    link_vel(m, &k, qd, m->ee_link, v, w);
+    double ee[3], v[3];
+    link_state_cached(c, q, qd, obj ? obj + OBJ_QC : q, m->ee_link, ee, v);
     float o[32];
     int n = 0;
-    for (int i = 0; i < 3; i++) o[n++] = (float)k.p[m->ee_link][i];
+    for (int i = 0; i < 3; i++) o[n++] = (float)ee[i];
     for (int i = 0; i < 3; i++) o[n++] = (float)v[i];
     if (!c->block_gripper) o[n++] = 0.0f; /* fixed finger joints in custom_0: width 0 */
     const int has_obj = c->task != PGX_TASK_REACH;
@@ -1049,7 +1078,7 @@ static void env_obs(const pgx_config* c, const double* q, const double* qd, cons
         for (int i = 0; i < 3; i++) o[n++] = (float)obj[10 + i];
     }
     if (obs) memcpy(obs, o, sizeof(float) * n);
-    if (ag) for (int i = 0; i < 3; i++) ag[i] = (float)(has_obj ? obj[i] : k.p[m->ee_link][i]);
+    if (ag) for (int i = 0; i < 3; i++) ag[i] = (float)(has_obj ? obj[i] : ee[i]);
     if (dg) for (int i = 0; i < 3; i++) dg[i] = (float)goal[i];
 }
 
@@ -1082,8 +1111,10 @@ static void reset_one(const pgx_config* c, int64_t e, const double* inject_goal,
         }
         obj[3] = 0.0; obj[4] = 0.0; obj[5] = 0.0; obj[6] = 1.0;
     }
-    if (obj)
+    if (obj) {
         for (int s = 0; s < 8; s++) { obj[13 + 2 * s] = -1.0; obj[13 + 2 * s + 1] = 0.0; }
+        memcpy(obj + OBJ_QC, q, 7 * sizeof(double));   /* resetJointState refreshes the link cache */
+    }
     *elapsed = 0;
     *episode += 1;
 }
@@ -1403,16 +1434,16 @@ static void ao_reset_task(const pgx_config* c, int64_t e, uint32_t episode, cons
 }
 
 /* robot obs (ee pos, ee vel, q, qd) + closest distance per link (9) + unit vectors (27) */
-static void ao_obs(const pgx_config* c, const double* q, const double* qd, const double* goal, const double* obst,
-                   float* obs, float* ag, float* dg) {
+static void ao_obs(const pgx_config* c, const double* q, const double* qd, const double* qc, const double* goal,
+                   const double* obst, float* obs, float* ag, float* dg) {
     const pgx_model* m = c->model;
     kin_t k;
     fk(m, c->base_pos, q, &k);
-    double v[3], w[3];
-    link_vel(m, &k, qd, m->ee_link, v, w);
+    double ee[3], v[3];   /* "ee" obs from getLinkState (cached pose); distances at the current pose */
+    link_state_cached(c, q, qd, qc, m->ee_link, ee, v);
     float o[64];
     int n = 0;
-    for (int i = 0; i < 3; i++) o[n++] = (float)k.p[m->ee_link][i];
+    for (int i = 0; i < 3; i++) o[n++] = (float)ee[i];
     for (int i = 0; i < 3; i++) o[n++] = (float)v[i];
     for (int i = 0; i < 7; i++) o[n++] = (float)q[i];
     for (int i = 0; i < 7; i++) o[n++] = (float)qd[i];
@@ -1424,7 +1455,7 @@ static void ao_obs(const pgx_config* c, const double* q, const double* qd, const
         for (int i = 0; i < 3; i++) o[n++] = (float)(len > 0 ? u[i] / len : 0.0);
     }
     if (obs) memcpy(obs, o, sizeof(float) * n);
-    if (ag) for (int i = 0; i < 3; i++) ag[i] = (float)k.p[m->ee_link][i];
+    if (ag) for (int i = 0; i < 3; i++) ag[i] = (float)ee[i];
     if (dg) for (int i = 0; i < 3; i++) dg[i] = (float)goal[i];
 }
 
@@ -1442,6 +1473,7 @@ static void ao_reset_one(const pgx_config* c, int64_t e, const double* inject_go
             active[o] = inject_obst[3 * o] < 50.0 ? 1.0 : 0.0;
         }
     for (int s = 0; s < 8; s++) { obj[13 + 2 * s] = -1.0; obj[13 + 2 * s + 1] = 0.0; }
+    memcpy(obj + OBJ_QC, q, 7 * sizeof(double));
     *elapsed = 0;
     *episode += 1;
 }
@@ -1489,9 +1521,10 @@ int pgxo_vec_step(const pgx_config* c, int64_t n, double* q, double* qd, double*
         }
         double tq[D];
         if (c->control == PGX_CONTROL_EE) {
-            /* ee_displacement_to_target_arm_angles (panda.py:226-246) */
+            /* ee_displacement_to_target_arm_angles (panda.py:226-246): get_ee_position() is
+             * getLinkState's cached pose (link_state_cached) */
             kin_t k;
-            fk(m, c->base_pos, qe, &k);
+            fk(m, c->base_pos, (p->flags & PGX_FLAG_LINKSTATE_CURRENT) ? qe : oe + OBJ_QC, &k);
             float step32 = (float)c->ee_step;
             double tgt[3];
             for (int i = 0; i < 3; i++) tgt[i] = k.p[m->ee_link][i] + (double)(a[i] * step32);
@@ -1515,6 +1548,7 @@ int pgxo_vec_step(const pgx_config* c, int64_t n, double* q, double* qd, double*
         const int ao = c->task == PGX_TASK_REACH_AO;
         int collided = 0;
         for (int s = 0; s < p->n_substeps; s++) {
+            memcpy(oe + OBJ_QC, qe, 7 * sizeof(double));   /* the link cache: the pose this substep solves at */
             pgxo_world_substep(c, qe, qde, oe, mot, NULL);
             /* ReachAO step_check_collision (reach_ao.py:182-188) */
             PGXO_PHASE(8);

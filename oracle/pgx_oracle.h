@@ -49,7 +49,8 @@ void pgxo_substep(const pgx_model* m, const pgx_sim_params* p, const double base
  * quat4 (x,y,z,w), linvel3, angvel3, contact cache 8 x (feature id, normal impulse). */
 void pgxo_world_substep(const pgx_config* cfg, double* q, double* qd, double* obj,
                         const pgxo_motor* motors, pgxo_stats* st);
-#define PGXO_OBJ_N 53   /* object (29) + ReachAO obstacle centres [6][3] and active flags [6] */
+#define PGXO_OBJ_N 60   /* object (29) + ReachAO obstacle centres [6][3] and active flags [6]
+                           + the cached link pose qc[7] (getLinkState, see pgx_oracle.c) */
 
 /* ReachAO geometry (test helpers): capsule (A, B, r) vs sphere (C, R) / rounded box
  * (c, h); per-link closest obstacle of the 9 collision links at q, returning the

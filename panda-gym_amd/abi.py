@@ -29,6 +29,7 @@ REWARD_CODES = {"sparse": REWARD_SPARSE, "dense": REWARD_DENSE, "sparse_ao": REW
 FLAG_CONSTRAINT_PASS_BIAS = 1
 FLAG_IK_COM = 2
 FLAG_NO_RESIDUAL_EXIT = 4
+FLAG_LINKSTATE_CURRENT = 8   # getLinkState at the pose after the last substep (rejected hypothesis)
 
 HER_FUTURE, HER_FINAL, HER_EPISODE = 0, 1, 2
 
@@ -99,7 +100,7 @@ class PgxStepOut(C.Structure):
 
 class PgxStateView(C.Structure):
     _fields_ = [
-        ("q", C.c_void_p), ("qd", C.c_void_p), ("goal", C.c_void_p), ("object", C.c_void_p),
+        ("q", C.c_void_p), ("qd", C.c_void_p), ("qc", C.c_void_p), ("goal", C.c_void_p), ("object", C.c_void_p),
         ("contacts", C.c_void_p), ("obstacles", C.c_void_p), ("elapsed", C.c_void_p), ("episode", C.c_void_p),
         ("errors", C.c_void_p),
     ]

@@ -377,7 +377,7 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     const size_t N = (size_t)cfg->n_envs;
     auto align = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t off_goal = align(sizeof(PgxDevModel)), off_q = align(off_goal + 3 * N * 8), off_qd = align(off_q + PGX_NJ * N * 4),
-           off_obj = align(off_qd + PGX_NJ * N * 4), off_ct = align(off_obj + 13 * N * 4),
+           off_qc = align(off_qd + PGX_NJ * N * 4), off_obj = align(off_qc + PGX_NJ * N * 4), off_ct = align(off_obj + 13 * N * 4),
            off_ao = align(off_ct + 2 * PGX_CONTACT_SLOTS * N * 4),
            off_el = align(off_ao + (e.ao ? 4 * PGX_AO_OBSTACLES * N * 4 : 0)), off_ep = align(off_el + N * 4),
            off_err = align(off_ep + N * 4), total = align(off_err + 4);
@@ -388,6 +388,7 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     h->ds.goal = (double*)(b + off_goal);
     h->ds.q = (float*)(b + off_q);
     h->ds.qd = (float*)(b + off_qd);
+    h->ds.qc = (float*)(b + off_qc);
     h->ds.object = (float*)(b + off_obj);
     h->ds.contacts = (float*)(b + off_ct);
     h->ds.obstacles = e.ao ? (float*)(b + off_ao) : nullptr;
@@ -422,6 +423,7 @@ int pgx_get_state(pgx_handle h, pgx_state_view* out) {
     if (!h || !out) return fail(PGX_E_INVALID, "null argument");
     out->q = h->ds.q;
     out->qd = h->ds.qd;
+    out->qc = h->ds.qc;
     out->goal = h->ds.goal;
     out->object = h->ds.object;
     out->contacts = h->ds.contacts;

@@ -69,6 +69,7 @@ struct PgxDevEnv {
 struct PgxDevState {
     float* q;          /* [7][N] */
     float* qd;         /* [7][N] */
+    float* qc;         /* [7][N] the link cache's pose (getLinkState: before the last substep) */
     double* goal;      /* [3][N] */
     float* object;     /* [13][N] pos3 quat4 (x,y,z,w) linvel3 angvel3 */
     float* contacts;   /* [2*PGX_CONTACT_SLOTS][N] warm-start cache (feature id, normal impulse) */

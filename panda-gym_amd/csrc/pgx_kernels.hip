@@ -2627,6 +2627,25 @@ __device__ __forceinline__ void ee_state(MRef m, const float* q, const float* qd
     vel = vv;
 }
 
+/* getLinkState(11) as the reference reads it (oracle link_state_cached): Bullet's cached link
+ * transform is the pose qc the last substep was solved at, and the local velocity (current q,
+ * qd) is turned to world with the cached rotation: pos = COM(qc), vel = R7(qc) R7(q)^T v(q, qd)
+ * (the EE link is rigid on link 7, so its rotation cancels in R_ee(qc) R_ee(q)^T). */
+__device__ __forceinline__ void ee_state_cached(MRef m, const float* qc, const float* q, const float* qd, V3& pos,
+                                                V3& vel) {
+    Chain k;
+    fk_chain(m, q, k);
+    const V3 p = k.o[NJ - 1] + mulc(k.R[NJ - 1], kEeCom);
+    V3 vv = v3(0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < NJ; j++) vv = vv + qd[j] * cross(col(k.R[j], 2), p - k.o[j]);
+    const V3 vl = mul_t(k.R[NJ - 1], vv);
+    Chain kc;
+    fk_chain(m, qc, kc);
+    pos = kc.o[NJ - 1] + mulc(kc.R[NJ - 1], kEeCom);
+    vel = mul(kc.R[NJ - 1], vl);
+}
+
 /* -------------------------------------------------------------- RNG */
 /* philox(): pgx_common.h */
 constexpr uint32_t TAG_RESET = 0x52455345u;
@@ -3151,8 +3170,12 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
         float a[3];
 #pragma unroll
         for (int c = 0; c < 3; c++) a[c] = fminf(fmaxf(action[(size_t)ii * A + c], -1.0f), 1.0f);
+        /* get_ee_position() (panda.py:235) is getLinkState's cached pose (ee_state_cached) */
+        float qcl[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; j++) qcl[j] = s.qc[j * N + ii];
         Chain k;
-        fk_chain<WIDE != 0>(m, q, k);
+        fk_chain<WIDE != 0>(m, qcl, k);
         V3 pos = k.o[NJ - 1] + mulc(k.R[NJ - 1], kEeCom);
         V3 tgt = pos + v3(a[0] * m.ee_step, a[1] * m.ee_step, a[2] * m.ee_step);
         tgt.z = fmaxf(0.0f, tgt.z);
@@ -3171,7 +3194,10 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     if constexpr (WIDE) lane_consts(lk);
     const int n_substeps = m.n_substeps;
     bool collided = false;
+    float qprev[NJ];   /* the pose the last substep starts from: getLinkState's cached pose */
     for (int st = 0; st < n_substeps; st++) {
+#pragma unroll
+        for (int j = 0; j < NJ; j++) qprev[j] = q[j];
         if constexpr (WIDE) substep_g<OBJ, CONT, PART, AO>(mp, e, q, qd, tq, ob, L, ln, c, lk);
         else substep<OBJ, CONT, AO>(mp, e, q, qd, tq, ob, L, ln);
         if constexpr (AO) {   /* ReachAO step_check_collision: check after every substep, stop on contact */
@@ -3182,7 +3208,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     }
 
     V3 pos, vel;
-    ee_state(*fresh(mp), q, qd, pos, vel);
+    ee_state_cached(*fresh(mp), qprev, q, qd, pos, vel);
     const int od = e.obs_dim;
     const V3 ag = OBJ ? ob.p : pos;
     double d = distance_f32_f64(ag, goal);
@@ -3229,7 +3255,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
         if constexpr (AO) {
             MRef mr = *fresh(mp);
 #pragma unroll
-            for (int j = 0; j < NJ; j++) { q[j] = mr.neutral_q[j]; qd[j] = 0.0f; }
+            for (int j = 0; j < NJ; j++) { q[j] = mr.neutral_q[j]; qd[j] = 0.0f; qprev[j] = q[j]; }
             ee_state(mr, q, qd, pos, vel);
             ao_caps(mr, q, *L, ln);
             if (ao_reset<WIDE != 0>(e, *L, ln, c, e.env_id_offset + (uint64_t)i, episode, pos, nullptr, nullptr, goal) &&
@@ -3241,6 +3267,8 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
         } else {
             reset_env<OBJ>(m, e, i, episode, nullptr, nullptr, q, qd, goal, ob);
             ee_state(m, q, qd, pos, vel);
+#pragma unroll
+            for (int j = 0; j < NJ; j++) qprev[j] = q[j];   /* resetJointState refreshes the link cache */
         }
         el = 0;
         if (CONT) {
@@ -3263,6 +3291,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     for (int j = 0; j < NJ; j++) {
         s.q[j * N + i] = q[j];
         s.qd[j * N + i] = qd[j];
+        s.qc[j * N + i] = qprev[j];
     }
 #pragma unroll
     for (int c = 0; c < 3; c++) s.goal[c * N + i] = goal[c];
@@ -3356,6 +3385,7 @@ __global__ __launch_bounds__(64) void reset_kernel(const PgxDevModel* __restrict
     for (int j = 0; j < NJ; j++) {
         s.q[j * N + i] = q[j];
         s.qd[j * N + i] = qd[j];
+        s.qc[j * N + i] = q[j];   /* resetJointState refreshes the link cache */
     }
 #pragma unroll
     for (int c = 0; c < 3; c++) s.goal[c * N + i] = goal[c];

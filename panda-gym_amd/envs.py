@@ -229,7 +229,8 @@ class PandaVecEnv:
             pass
 
     def state(self) -> Dict[str, torch.Tensor]:
-        """Device views of the SoA state (q, qd [7,N] f32; goal [3,N] f64; object [13,N] f32 =
+        """Device views of the SoA state (q, qd [7,N] f32; qc [7,N] f32 the pose getLinkState reports;
+        goal [3,N] f64; object [13,N] f32 =
         pos, quat (x,y,z,w), linvel, angvel; contacts [16,N] f32 warm-start cache; elapsed,
         episode [N])."""
         v = abi.PgxStateView()
@@ -238,6 +239,7 @@ class PandaVecEnv:
         return {
             "q": _view(v.q, (7, n), torch.float32, self.device),
             "qd": _view(v.qd, (7, n), torch.float32, self.device),
+            "qc": _view(v.qc, (7, n), torch.float32, self.device),
             "goal": _view(v.goal, (3, n), torch.float64, self.device),
             "object": _view(v.object, (13, n), torch.float32, self.device),
             "contacts": _view(v.contacts, (2 * abi.CONTACT_SLOTS, n), torch.float32, self.device),

@@ -29,6 +29,7 @@ def _state_to_oracle(venv, ref):
     st = venv.state()
     ref.q[:] = st["q"].double().cpu().numpy().T
     ref.qd[:] = st["qd"].double().cpu().numpy().T
+    ref.qc[:] = st["qc"].double().cpu().numpy().T
     ref.goal[:] = st["goal"].cpu().numpy().T
     ref.elapsed[:] = st["elapsed"].cpu().numpy()
     ref.episode[:] = st["episode"].cpu().numpy().view(np.uint32)

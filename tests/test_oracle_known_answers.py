@@ -38,56 +38,89 @@ def test_ik_alternative_hypothesis_rejected(oracle, upstream_model):
     assert not np.allclose(q, expected, atol=ATOL)
 
 
-def _control_joint5_step(oracle, model, flags=0):
+def _control_joint5_step(oracle, model, flags=0, history=False):
     """control_joints("panda", [5], [0.3], [5.0]) then PyBullet.step(): POSITION_CONTROL on joint 5
     (kp 0.1, kd 1, max force 5); every other joint keeps pybullet's default velocity motor
-    (target 0, kd 1, max impulse 1); 20 substeps of 1/500 s."""
+    (target 0, kd 1, max impulse 1); 20 substeps of 1/500 s.  ``history``: also the pose the
+    last substep started from (getLinkState's cached link pose, pgx_oracle.c link_state_cached)."""
     p = abi.default_sim_params(flags=flags)
     entries = {d: (0.0, 0.0, 0.0, 1.0, 1.0) for d in range(9)}
     entries[5] = (0.3, 0.0, 0.1, 1.0, 5.0 * p.dt)
     motors = oracle.make_motors(9, entries)
     q, qd = np.zeros(9), np.zeros(9)
+    qc = q
     for _ in range(20):
+        qc = q
         q, qd, _ = oracle.substep(model, p, q, qd, motors)
-    return q, qd
+    return (q, qd, qc) if history else (q, qd)
+
+
+def _link_state(oracle, model, q, qd, qc, link):
+    """getLinkState(link, computeLinkVelocity=1): the cached pose qc for position / orientation,
+    the local velocity at (q, qd) turned to world with the cached rotation."""
+    from scipy.spatial.transform import Rotation
+
+    _, rot, _ = oracle.fk(model, q)
+    _, rotc, _ = oracle.fk(model, qc)
+    lin, ang = oracle.link_velocity(model, q, qd, link)
+    Rrel = rotc[link] @ rot[link].T
+    quat = Rotation.from_matrix(rotc[link]).as_quat()
+    return quat if quat[3] >= 0 else -quat, Rrel @ lin, Rrel @ ang
 
 
 def test_joint_angle_known_answer(oracle, upstream_model):
-    """test/pybullet_test.py:190-204: joint 5 angle 0.063 after one env step."""
+    """test/pybullet_test.py:190-204: joint 5 angle 0.063 after one env step (getJointState: the
+    current pose)."""
     q, _ = _control_joint5_step(oracle, upstream_model)
     assert abs(q[5] - 0.063) < ATOL, q[5]
 
 
-def test_link_angular_velocity_known_answer(oracle, upstream_model):
-    """test/pybullet_test.py:173-187: link 5 angular velocity [0, -2.969, 0]."""
-    q, qd = _control_joint5_step(oracle, upstream_model)
-    _, ang = oracle.link_velocity(upstream_model, q, qd, 5)
-    assert np.allclose(ang, [0.0, -2.969, 0.0], atol=ATOL), ang
-
-
-def test_link_velocity_known_answer(oracle, upstream_model):
-    """test/pybullet_test.py:156-170: link 5 COM linear velocity [-0.0068, 0, 0.1186]."""
-    q, qd = _control_joint5_step(oracle, upstream_model)
-    lin, _ = oracle.link_velocity(upstream_model, q, qd, 5)
+def test_link_state_known_answers_jointly(oracle, upstream_model):
+    """test/pybullet_test.py:139-187 after the same step: link 5's orientation
+    [0.707, -0.02, 0.02, 0.707], COM velocity [-0.0068, 0, 0.1186] and angular velocity
+    [0, -2.969, 0], all at atol 1e-3, together with the joint angle 0.063 of :190-204 -- which
+    holds only with getLinkState reporting Bullet's cached link pose (the pose the last substep
+    was solved at; velocities from the current local state, turned with the cached rotation)."""
+    q, qd, qc = _control_joint5_step(oracle, upstream_model, history=True)
+    quat, lin, ang = _link_state(oracle, upstream_model, q, qd, qc, 5)
+    assert abs(q[5] - 0.063) < ATOL
+    assert np.allclose(quat, [0.707, -0.02, 0.02, 0.707], atol=ATOL), quat
     assert np.allclose(lin, [-0.0068, 0.0, 0.1186], atol=ATOL), lin
+    assert np.allclose(ang, [0.0, -2.969, 0.0], atol=ATOL), ang
+    assert np.abs(lin - [-0.0068, 0.0, 0.1186]).max() < 1e-4   # 3e-5 off (current-pose rule: 6.7e-4)
 
 
-def test_link_orientation_known_answer_consistency(oracle, upstream_model):
-    """test/pybullet_test.py:139-153 expects [0.707,-0.02,0.02,0.707], but a rotation of joint 5 by
-    the 0.063 of :190-204 from q=0 gives x/z = -/+0.707*sin(0.063/2) = 0.0223: the two answers of
-    the same scenario are inconsistent at atol 1e-3.  We pin the orientation to the value implied by
-    the joint-angle answer (documented in DESIGN.md)."""
-    q, _ = _control_joint5_step(oracle, upstream_model)
-    _, rot, _ = oracle.fk(upstream_model, q)
-    from scipy.spatial.transform import Rotation
+def test_link_state_at_current_pose_rejected(oracle, upstream_model):
+    """The alternative -- link states at the pose after the last substep -- misses the orientation
+    answer: y = -0.7068 sin(0.0627 / 2) = -0.0222, 2.2e-3 from -0.02 (the joint angle answer pins
+    q5 within 1e-3, so no pose consistent with :190-204 gives -0.02 at 1e-3 this way)."""
+    q, qd = _control_joint5_step(oracle, upstream_model)
+    quat, lin, _ = _link_state(oracle, upstream_model, q, qd, q, 5)
+    assert not np.allclose(quat, [0.707, -0.02, 0.02, 0.707], atol=ATOL)
+    assert abs(quat[1] + 0.7068 * math.sin(q[5] / 2)) < 1e-3
 
-    quat = Rotation.from_matrix(rot[5]).as_quat()
-    implied = Rotation.from_matrix(
-        forward_kinematics(load_model("panda_upstream"), [0, 0, 0, 0, 0, 0.063, 0, 0, 0])["R"][5]).as_quat()
-    if quat[3] * implied[3] < 0:
-        quat = -quat
-    assert np.allclose(quat, implied, atol=ATOL)
-    assert np.allclose(quat[[0, 3]], [0.707, 0.707], atol=ATOL)
+
+def test_vec_step_reports_the_cached_link_pose(oracle, custom_model):
+    """The env step (pgxo_vec_step) reports the EE from the cached pose: obs = COM at the pose
+    before the last substep (oracle.qc), velocity turned with its rotation; with
+    PGX_FLAG_LINKSTATE_CURRENT it reports the current pose instead."""
+    from oracle import oracle as O
+
+    outs = {}
+    for flags in (0, abi.FLAG_LINKSTATE_CURRENT):
+        p = abi.default_sim_params(flags=flags)
+        cfg = abi.make_config(abi.EnvSpec(control=abi.CONTROL_JOINTS), 4, custom_model, p, seed=3)
+        env = O.OracleVecEnv(cfg, 4)
+        env.reset()
+        a = env.sample_actions(0)
+        b = env.step(a)
+        com_c, _, _ = O.fk(custom_model, env.qc[0], base=(-0.6, 0, 0))
+        com, _, _ = O.fk(custom_model, env.q[0], base=(-0.6, 0, 0))
+        outs[flags] = (b["obs"][0, :3].astype(np.float64), com_c[11], com[11])
+    got, at_qc, at_q = outs[0]
+    assert np.allclose(got, at_qc, atol=1e-6) and np.abs(at_q - at_qc).max() > 1e-4
+    got2, _, at_q2 = outs[abi.FLAG_LINKSTATE_CURRENT]
+    assert np.allclose(got2, at_q2, atol=1e-6)
 
 
 def test_double_bias_hypothesis_rejected(oracle, upstream_model):

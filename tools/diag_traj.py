@@ -12,6 +12,7 @@ venv.reset_tensors()
 ref = O.OracleVecEnv(venv._cfg, n)
 st = venv.state()
 ref.q[:] = st["q"].double().cpu().numpy().T; ref.qd[:] = st["qd"].double().cpu().numpy().T
+ref.qc[:] = st["qc"].double().cpu().numpy().T
 ref.goal[:] = st["goal"].cpu().numpy().T
 for t in range(50):
     a = venv.sample_actions(t).clone()
