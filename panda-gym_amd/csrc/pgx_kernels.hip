@@ -512,13 +512,72 @@ __device__ __forceinline__ V3 seg_closest(V3 A, V3 B, V3 C) {
  * on the inner box's signed distance along the axis, the signed distance returned; with NV
  * also the closest axis point P and the unit direction n from it towards the box (into the
  * box through the nearest face when P is inside the inner box) */
+/* Does segment A + t ab, t in [0, 1], meet the box [lo, hi]?  (slab clipping) */
+__device__ __forceinline__ bool seg_meets_box(V3 A, V3 ab, V3 lo, V3 hi) {
+    float t0 = 0.0f, t1 = 1.0f;
+    bool miss = false;
+    const float a[3] = {A.x, A.y, A.z}, d[3] = {ab.x, ab.y, ab.z}, l[3] = {lo.x, lo.y, lo.z}, u[3] = {hi.x, hi.y, hi.z};
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        if (fabsf(d[i]) < 1e-20f) {
+            miss = miss || a[i] < l[i] || a[i] > u[i];
+        } else {
+            const float inv = fast_rcp(d[i]);
+            const float ta = (l[i] - a[i]) * inv, tb = (u[i] - a[i]) * inv;
+            t0 = fmaxf(t0, fminf(ta, tb));
+            t1 = fminf(t1, fmaxf(ta, tb));
+        }
+    }
+    return !miss && t0 <= t1;
+}
+/* Closest point P of a segment that misses the box [lo, hi] (its distance is > 0): the squared
+ * distance f(t) = |e(t)|^2, e = P(t) - clamp(P(t)), is convex and piecewise quadratic in t (its
+ * pieces change where a coordinate crosses a slab face), so Newton's step t - f'/f'' is exact
+ * within a piece; safeguarded by the bracket f' changes sign in, it lands on the minimiser in a
+ * few steps (at most one per piece: 7) instead of capsule_box_pair's 34-step search. */
+__device__ __forceinline__ V3 seg_box_closest(V3 A, V3 ab, V3 lo, V3 hi) {
+    const float l2 = dot(ab, ab);
+    const V3 cm = 0.5f * (lo + hi);
+    float t = l2 > 0.0f ? fminf(fmaxf(dot(cm - A, ab) * fast_rcp(l2), 0.0f), 1.0f) : 0.0f;
+    float tl = 0.0f, th = 1.0f;
+    V3 P = A + t * ab;
+    for (int it = 0; it < 10 && l2 > 0.0f; it++) {
+        const float ex = P.x - fminf(fmaxf(P.x, lo.x), hi.x), ey = P.y - fminf(fmaxf(P.y, lo.y), hi.y),
+                    ez = P.z - fminf(fmaxf(P.z, lo.z), hi.z);
+        const float g = ex * ab.x + ey * ab.y + ez * ab.z;   /* f'(t) / 2 */
+        const float H = (ex != 0.0f ? ab.x * ab.x : 0.0f) + (ey != 0.0f ? ab.y * ab.y : 0.0f) +
+                        (ez != 0.0f ? ab.z * ab.z : 0.0f);   /* f''(t) / 2 on this piece */
+        if (g > 0.0f) th = t;
+        else if (g < 0.0f) tl = t;
+        else break;
+        float tn = H > 0.0f ? t - g * fast_rcp(H) : 0.5f * (tl + th);
+        tn = (tn > tl && tn < th) ? tn : 0.5f * (tl + th);
+        if (tn == t) break;
+        t = tn;
+        P = A + t * ab;
+    }
+    return P;
+}
+
 template <bool NV>
 __device__ __forceinline__ float capsule_box_pair(V3 A, V3 B, float r, V3 c, V3 hf, V3* Pout, V3* nout) {
     const V3 h = v3(hf.x - kAoMargin, hf.y - kAoMargin, hf.z - kAoMargin);
     const V3 ab = B - A;
     float lo = 0.0f, hi = 1.0f;
     const bool seg = dot(ab, ab) > 0.0f;
-    if (seg) {
+    if (!seg_meets_box(A, ab, c - h, c + h)) {   /* outside: the exact closest pair (Newton) */
+        const V3 P = seg_box_closest(A, ab, c - h, c + h);
+        const V3 q = v3(fminf(fmaxf(P.x, c.x - h.x), c.x + h.x), fminf(fmaxf(P.y, c.y - h.y), c.y + h.y),
+                        fminf(fmaxf(P.z, c.z - h.z), c.z + h.z));
+        const V3 v = q - P;
+        const float sd = norm(v);
+        if (NV) {
+            *Pout = P;
+            *nout = sd > 0.0f ? fast_rcp(sd) * v : v3(0.0f, 0.0f, 0.0f);
+        }
+        return sd - kAoMargin - r;
+    }
+    if (seg) {   /* the segment enters the inner box: the signed distance by the search */
         /* golden-section search of the convex box_sd along the axis: one evaluation per step,
          * 34 steps shrink [0, 1] to 0.618^34 = 8e-8 (the ternary search's 40 steps of two
          * evaluations reach 9e-8) */
@@ -580,46 +639,17 @@ __device__ __forceinline__ float capsule_box(V3 A, V3 B, float r, V3 c, V3 hf, V
     return d;
 }
 
-/* capsule_box(...) <= thr as a decision: the same golden-section search, stopped as soon as a
- * sample is within r + margin of the inner box (the minimum can only be lower) or the best
- * sample minus |AB| times the bracket width (f is |AB|-Lipschitz in t; the minimiser stays in
- * the bracket of a convex f) is farther than that (the minimum cannot reach it); the
- * undecided rest ends as capsule_box does. */
+/* capsule_box(...) <= thr as a decision (thr >= 0) */
 __device__ __forceinline__ bool capsule_box_hit(V3 A, V3 B, float r, V3 c, V3 hf, float thr = 0.0f) {
     const V3 h = v3(hf.x - kAoMargin, hf.y - kAoMargin, hf.z - kAoMargin);
     const V3 ab = B - A;
-    const float lim = kAoMargin + r + thr;
-    if (!(dot(ab, ab) > 0.0f)) return box_sd(A, c, h) - kAoMargin - r <= thr;
-    const float len = norm(ab);
-    const float gr = 0.61803398875f;
-    float lo = 0.0f, hi = 1.0f;
-    float t1 = hi - gr * (hi - lo), t2 = lo + gr * (hi - lo);
-    float f1 = box_sd(A + t1 * ab, c, h), f2 = box_sd(A + t2 * ab, c, h);
-    for (int it = 0; it < 34; it++) {
-        const float fb = fminf(f1, f2);
-        if (fb <= lim) return true;
-        if (fb - len * (hi - lo) > lim) return false;
-        if (f1 <= f2) {
-            hi = t2; t2 = t1; f2 = f1;
-            t1 = hi - gr * (hi - lo);
-            f1 = box_sd(A + t1 * ab, c, h);
-        } else {
-            lo = t1; t1 = t2; f1 = f2;
-            t2 = lo + gr * (hi - lo);
-            f2 = box_sd(A + t2 * ab, c, h);
-        }
-    }
-    V3 P = A + 0.5f * (lo + hi) * ab;
-    float sd = box_sd(P, c, h);
-    if (sd > 0.0f) {
-        for (int it = 0; it < 2; it++) {
-            const V3 q = v3(fminf(fmaxf(P.x, c.x - h.x), c.x + h.x), fminf(fmaxf(P.y, c.y - h.y), c.y + h.y),
-                            fminf(fmaxf(P.z, c.z - h.z), c.z + h.z));
-            P = seg_closest(A, B, q);
-        }
-        sd = box_sd(P, c, h);
-    }
-    return sd - kAoMargin - r <= thr;
+    /* thr >= 0 in every use: a segment meeting the inner box is within it; one that misses it
+     * has the exact (Newton) distance */
+    if (seg_meets_box(A, ab, c - h, c + h)) return true;
+    const V3 P = seg_box_closest(A, ab, c - h, c + h);
+    const V3 q = v3(fminf(fmaxf(P.x, c.x - h.x), c.x + h.x), fminf(fmaxf(P.y, c.y - h.y), c.y + h.y),
+                    fminf(fmaxf(P.z, c.z - h.z), c.z + h.z));
+    return norm(q - P) - kAoMargin - r <= thr;
 }
 
 /* ------------------------------------------------------------- contacts */
@@ -1331,26 +1361,51 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
         if constexpr (!OBJ) {
             robot_table_contacts_g(e, m.contact_dist, *Lp, es, c);
             if constexpr (AO) {
-                /* obstacle contacts (ao_obstacle_candidates): lane c culls capsule c against the
-                 * six obstacles; the capsules near one anywhere in the wave insert their pairs by
-                 * depth (g1_insert) after the table candidates, then id order, as robot_contacts
-                 * discovers them (only an exact depth tie of a table and an obstacle candidate
-                 * could order differently) */
+                /* obstacle contacts (ao_obstacle_candidates), lane-parallel: per obstacle, lane c
+                 * measures capsule c's pair (the cull first, the exact query only where the pair
+                 * can be within tau); the rare candidates are then inserted by depth (g1_insert)
+                 * after the table candidates, every lane of the env reading the candidate lane's
+                 * values, and finally put in id order.  Obstacle-major insertion instead of
+                 * robot_contacts' capsule-major order: only an exact depth tie could order
+                 * differently. */
+                const float tau = m.contact_dist;
                 const int cc = c < PGX_NCAP ? c : 0;
-                const bool near = c < PGX_NCAP && kCapFlags[cc] != 0 && ao_capsule_near(*Lp, es, cc, m.contact_dist);
-                const uint64_t bn = __ballot(near);
-                unsigned wm = (unsigned)((bn | (bn >> 16) | (bn >> 32) | (bn >> 48)) & 0xFFFFu);
-                if (wm) {
-                    const unsigned rm = row_ballot(near);
-                    sort_g1_by_depth(*Lp, es);
-                    wm = __builtin_amdgcn_readfirstlane(wm);
-                    while (wm) {
-                        const int cn = __builtin_ctz(wm);
-                        wm &= wm - 1u;
-                        if ((rm >> cn) & 1u) ao_obstacle_candidates(*Lp, es, cn, m.contact_dist);
+                const bool cap_on = c < PGX_NCAP && kCapFlags[cc] != 0;
+                const V3 A = lds3(Lp->capA[cc], es), B = lds3(Lp->capB[cc], es);
+                const float r = kCapR[cc];
+                const V3 hcube = v3(kAoSize, kAoSize, kAoSize);
+                const int row0 = (int)(threadIdx.x & ~(unsigned)(GW - 1));
+                bool sorted = false;
+                for (int o = 0; o < AO_N; o++) {
+                    const V3 C = lds3(Lp->aoC[o], es);
+                    V3 P = seg_closest(A, B, C);
+                    const V3 v = C - P;
+                    const float len = norm(v);
+                    float d = 3.0e38f;
+                    V3 n = len > 0.0f ? fast_rcp(len) * v : v3(0.0f, 0.0f, 1.0f);
+                    if (cap_on) {
+                        if (o < 3) d = len - r - kAoSize;
+                        else if (len - r - kAoCubeBound < tau) d = capsule_box_pair<true>(A, B, r, C, hcube, &P, &n);
                     }
-                    sort_groups(*Lp, es);
+                    const bool cand = cap_on && d < tau;
+                    const uint64_t bm = __ballot(cand);
+                    if (bm == 0) continue;
+                    if (!sorted) { sort_g1_by_depth(*Lp, es); sorted = true; }
+                    unsigned wm = __builtin_amdgcn_readfirstlane(
+                        (unsigned)((bm | (bm >> 16) | (bm >> 32) | (bm >> 48)) & 0xFFFFu));
+                    const V3 pa = P + r * n;
+                    while (wm) {
+                        const int k = __builtin_ctz(wm);
+                        wm &= wm - 1u;
+                        const int src = row0 + k;
+                        const bool ck = __shfl((int)cand, src) != 0;
+                        const float dk = __shfl(d, src);
+                        const V3 pk = v3(__shfl(pa.x, src), __shfl(pa.y, src), __shfl(pa.z, src));
+                        const V3 nk = v3(__shfl(n.x, src), __shfl(n.y, src), __shfl(n.z, src));
+                        if (ck) g1_insert(*Lp, es, dk, (float)(32 + 6 * k + o), kCapJ[k], pk, (-1.0f) * nk, v3(0.0f, 0.0f, 0.0f));
+                    }
                 }
+                if (sorted) sort_groups(*Lp, es);
             }
         } else {
             PGX_PROF_MARK(20);
