@@ -531,32 +531,43 @@ __device__ __forceinline__ bool seg_meets_box(V3 A, V3 ab, V3 lo, V3 hi) {
     return !miss && t0 <= t1;
 }
 /* Closest point P of a segment that misses the box [lo, hi] (its distance is > 0): the squared
- * distance f(t) = |e(t)|^2, e = P(t) - clamp(P(t)), is convex and piecewise quadratic in t (its
- * pieces change where a coordinate crosses a slab face), so Newton's step t - f'/f'' is exact
- * within a piece; safeguarded by the bracket f' changes sign in, it lands on the minimiser in a
- * few steps (at most one per piece: 7) instead of capsule_box_pair's 34-step search. */
+ * distance f(t) = |e(t)|^2, e = P(t) - clamp(P(t)), is convex and piecewise quadratic in t, its
+ * pieces changing where a coordinate crosses a slab face (<= 6 breakpoints), so f'(t)/2 =
+ * e(t).ab is continuous, non-decreasing and linear between breakpoints.  Evaluated at 0, 1 and
+ * the breakpoints, the largest point with f' <= 0 and the smallest with f' >= 0 bound the piece
+ * holding the minimiser, where linear interpolation of f' is exact: 8 evaluations, no search
+ * (capsule_box_pair's golden section takes 34; pinned against brute force in
+ * tests/test_gpu_reach_ao.py through the observation's distances and unit vectors). */
 __device__ __forceinline__ V3 seg_box_closest(V3 A, V3 ab, V3 lo, V3 hi) {
-    const float l2 = dot(ab, ab);
-    const V3 cm = 0.5f * (lo + hi);
-    float t = l2 > 0.0f ? fminf(fmaxf(dot(cm - A, ab) * fast_rcp(l2), 0.0f), 1.0f) : 0.0f;
-    float tl = 0.0f, th = 1.0f;
-    V3 P = A + t * ab;
-    for (int it = 0; it < 10 && l2 > 0.0f; it++) {
+    auto fprime = [&](float t) __attribute__((always_inline)) {
+        const V3 P = A + t * ab;
         const float ex = P.x - fminf(fmaxf(P.x, lo.x), hi.x), ey = P.y - fminf(fmaxf(P.y, lo.y), hi.y),
                     ez = P.z - fminf(fmaxf(P.z, lo.z), hi.z);
-        const float g = ex * ab.x + ey * ab.y + ez * ab.z;   /* f'(t) / 2 */
-        const float H = (ex != 0.0f ? ab.x * ab.x : 0.0f) + (ey != 0.0f ? ab.y * ab.y : 0.0f) +
-                        (ez != 0.0f ? ab.z * ab.z : 0.0f);   /* f''(t) / 2 on this piece */
-        if (g > 0.0f) th = t;
-        else if (g < 0.0f) tl = t;
-        else break;
-        float tn = H > 0.0f ? t - g * fast_rcp(H) : 0.5f * (tl + th);
-        tn = (tn > tl && tn < th) ? tn : 0.5f * (tl + th);
-        if (tn == t) break;
-        t = tn;
-        P = A + t * ab;
+        return ex * ab.x + ey * ab.y + ez * ab.z;
+    };
+    float tl = -1.0f, gl = 0.0f, th = 2.0f, gh = 0.0f;
+    auto take = [&](float b) __attribute__((always_inline)) {
+        const float g = fprime(b);
+        if (g <= 0.0f && b > tl) { tl = b; gl = g; }
+        if (g >= 0.0f && b < th) { th = b; gh = g; }
+    };
+    take(0.0f);
+    take(1.0f);
+    const float a[3] = {A.x, A.y, A.z}, d[3] = {ab.x, ab.y, ab.z}, l[3] = {lo.x, lo.y, lo.z}, u[3] = {hi.x, hi.y, hi.z};
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        if (fabsf(d[i]) >= 1e-20f) {
+            const float inv = fast_rcp(d[i]);
+            take(fminf(fmaxf((l[i] - a[i]) * inv, 0.0f), 1.0f));
+            take(fminf(fmaxf((u[i] - a[i]) * inv, 0.0f), 1.0f));
+        }
     }
-    return P;
+    float t;
+    if (tl < 0.0f) t = 0.0f;          /* f'(0) > 0: the minimum is at A */
+    else if (th > 1.0f) t = 1.0f;
+    else t = gh - gl > 0.0f ? tl - gl * (th - tl) * fast_rcp(gh - gl) : tl;
+    t = fminf(fmaxf(t, fmaxf(tl, 0.0f)), fminf(th, 1.0f));
+    return A + t * ab;
 }
 
 template <bool NV>
@@ -565,7 +576,7 @@ __device__ __forceinline__ float capsule_box_pair(V3 A, V3 B, float r, V3 c, V3 
     const V3 ab = B - A;
     float lo = 0.0f, hi = 1.0f;
     const bool seg = dot(ab, ab) > 0.0f;
-    if (!seg_meets_box(A, ab, c - h, c + h)) {   /* outside: the exact closest pair (Newton) */
+    if (!seg_meets_box(A, ab, c - h, c + h)) {   /* outside: the exact closest pair (seg_box_closest) */
         const V3 P = seg_box_closest(A, ab, c - h, c + h);
         const V3 q = v3(fminf(fmaxf(P.x, c.x - h.x), c.x + h.x), fminf(fmaxf(P.y, c.y - h.y), c.y + h.y),
                         fminf(fmaxf(P.z, c.z - h.z), c.z + h.z));
@@ -644,7 +655,7 @@ __device__ __forceinline__ bool capsule_box_hit(V3 A, V3 B, float r, V3 c, V3 hf
     const V3 h = v3(hf.x - kAoMargin, hf.y - kAoMargin, hf.z - kAoMargin);
     const V3 ab = B - A;
     /* thr >= 0 in every use: a segment meeting the inner box is within it; one that misses it
-     * has the exact (Newton) distance */
+     * has the exact (seg_box_closest) distance */
     if (seg_meets_box(A, ab, c - h, c + h)) return true;
     const V3 P = seg_box_closest(A, ab, c - h, c + h);
     const V3 q = v3(fminf(fmaxf(P.x, c.x - h.x), c.x + h.x), fminf(fmaxf(P.y, c.y - h.y), c.y + h.y),
