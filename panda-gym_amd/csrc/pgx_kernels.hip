@@ -663,6 +663,10 @@ __device__ __forceinline__ bool capsule_box_hit(V3 A, V3 B, float r, V3 c, V3 hf
     return norm(q - P) - kAoMargin - r <= thr;
 }
 
+/* ReachAO's table box (table_top is its top face) */
+__device__ __forceinline__ V3 ao_table_c(const PgxDevEnv& e) { return v3(e.table_cx, e.table_cy, e.table_top - e.table_hz); }
+__device__ __forceinline__ V3 ao_table_h(const PgxDevEnv& e) { return v3(e.table_hx, e.table_hy, e.table_hz); }
+
 /* ------------------------------------------------------------- contacts */
 /* Restated in oracle/pgx_oracle.c ("world: object + contacts"): two contact groups
  * (object vs table/plane, robot vs table/plane/object) of at most CG points each, the
@@ -1025,6 +1029,7 @@ struct Dyn {
     float mdiag[NJ];      /* wide layout: diag(M^-1) on every lane */
     float vu[NJ];
     V3 vcu, wcu;
+    bool coll;            /* ReachAO, wide layout: check_collided at the substep's start pose */
 };
 
 template <int OBJ, int CONT, class LT, bool PAR = false, int AO = 0>
@@ -1306,8 +1311,9 @@ __device__ __forceinline__ V3 mul_sym(const float* s, V3 v) {
 template <int OBJ, int CONT, int AO = 0>
 __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const float* q, const float* qd,
                                               const ObjState& ob, ContactLdsG* Lp, int es, Dyn& D, int c,
-                                              const LaneK& K) {
+                                              const LaneK& K, bool check = false) {
     M3 Rc;
+    D.coll = false;
     if (OBJ) Rc = quat_mat(ob);
     if (CONT) { Lp->cnt[0][es] = 0; Lp->cnt[1][es] = 0; }
     if (OBJ) { /* object vertices vs the box top under them, lane v tests vertex v: the 4
@@ -1382,11 +1388,23 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                 const float tau = m.contact_dist;
                 const int cc = c < PGX_NCAP ? c : 0;
                 const bool cap_on = c < PGX_NCAP && kCapFlags[cc] != 0;
+                /* check (every substep but the first): the step loop's check_collided of the
+                 * previous substep's end pose -- this pose -- fused in here, as ao_collided_g
+                 * decides it (same pairs, same arithmetic): lane c's obstacle pairs when c is a
+                 * collision link, its table distance for links 2..ee */
+                const int slot = c < PGX_NCAP ? kAoSlot[cc] : -1;
+                const bool chk = check && slot >= 0;
                 const V3 A = lds3(Lp->capA[cc], es), B = lds3(Lp->capB[cc], es);
                 const float r = kCapR[cc];
                 const V3 hcube = v3(kAoSize, kAoSize, kAoSize);
                 const int row0 = (int)(threadIdx.x & ~(unsigned)(GW - 1));
-                bool sorted = false;
+                bool sorted = false, hit = false;
+                if (chk && slot >= 1) {
+                    const V3 tc = ao_table_c(e), th = ao_table_h(e);
+                    const V3 thi = v3(th.x - kAoMargin, th.y - kAoMargin, th.z - kAoMargin);
+                    const float lb = fminf(box_sd(A, tc, thi), box_sd(B, tc, thi)) - 0.5f * norm(B - A) - kAoMargin - r;
+                    if (lb <= 0.0f) hit = capsule_box_hit(A, B, r, tc, th);
+                }
                 for (int o = 0; o < AO_N; o++) {
                     const V3 C = lds3(Lp->aoC[o], es);
                     V3 P = seg_closest(A, B, C);
@@ -1394,10 +1412,12 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                     const float len = norm(v);
                     float d = 3.0e38f;
                     V3 n = len > 0.0f ? fast_rcp(len) * v : v3(0.0f, 0.0f, 1.0f);
-                    if (cap_on) {
+                    if (cap_on || chk) {
                         if (o < 3) d = len - r - kAoSize;
-                        else if (len - r - kAoCubeBound < tau) d = capsule_box_pair<true>(A, B, r, C, hcube, &P, &n);
+                        else if (len - r - kAoCubeBound < (cap_on ? tau : 0.0f))
+                            d = capsule_box_pair<true>(A, B, r, C, hcube, &P, &n);
                     }
+                    hit = hit || (chk && d <= 0.0f);
                     const bool cand = cap_on && d < tau;
                     const uint64_t bm = __ballot(cand);
                     if (bm == 0) continue;
@@ -1417,6 +1437,8 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                     }
                 }
                 if (sorted) sort_groups(*Lp, es);
+                D.coll = row_any(hit);
+                if (D.coll) return;   /* the step stops here: nothing of this substep runs */
             }
         } else {
             PGX_PROF_MARK(20);
@@ -2048,11 +2070,15 @@ constexpr bool limit_rows_paired() {
 }
 
 template <int OBJ, int CONT, int PART = 1, int AO = 0>
-__device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q, float* qd, const float* tq,
-                                          ObjState& ob, ContactLdsG* Lp, int es, int c, const LaneK& K) {
+__device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q, float* qd, const float* tq,
+                                          ObjState& ob, ContactLdsG* Lp, int es, int c, const LaneK& K,
+                                          bool check = false) {
     MRef m = *fresh(mp);
     Dyn D;
-    substep_dyn_g<OBJ, CONT, AO>(m, e, q, qd, ob, Lp, es, D, c, K);
+    substep_dyn_g<OBJ, CONT, AO>(m, e, q, qd, ob, Lp, es, D, c, K, check);
+    if constexpr (AO) {
+        if (D.coll) return true;   /* collided at the start pose: this substep does not run */
+    }
     const V3 (&z)[NJ] = D.z;
     const V3 (&o)[NJ] = D.o;
     const float (&vu)[NJ] = D.vu;
@@ -2680,6 +2706,7 @@ __device__ __forceinline__ void substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         object_integrate(m, ob, vcu + dvl, wcu + dvw);
     }
     PGX_PROF_MARK(5);
+    return false;
 }
 
 /* EE (link 11) COM position and velocity: getLinkState(11)[0] and [6] */
@@ -2857,8 +2884,6 @@ __device__ __forceinline__ void ao_caps(MRef m, const float* q, LT& L, int ln) {
     ao_caps_walk(k, m, L, ln);
 }
 
-__device__ __forceinline__ V3 ao_table_c(const PgxDevEnv& e) { return v3(e.table_cx, e.table_cy, e.table_top - e.table_hz); }
-__device__ __forceinline__ V3 ao_table_h(const PgxDevEnv& e) { return v3(e.table_hx, e.table_hy, e.table_hz); }
 
 /* check_collided: any collision link within 0 of an obstacle, or links 2..ee of the table */
 template <class LT>
@@ -3262,14 +3287,31 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     bool collided = false;
     float qprev[NJ];   /* the pose the last substep starts from: getLinkState's cached pose */
     for (int st = 0; st < n_substeps; st++) {
+        float qstart[NJ];
 #pragma unroll
-        for (int j = 0; j < NJ; j++) qprev[j] = q[j];
-        if constexpr (WIDE) substep_g<OBJ, CONT, PART, AO>(mp, e, q, qd, tq, ob, L, ln, c, lk);
-        else substep<OBJ, CONT, AO>(mp, e, q, qd, tq, ob, L, ln);
-        if constexpr (AO) {   /* ReachAO step_check_collision: check after every substep, stop on contact */
+        for (int j = 0; j < NJ; j++) qstart[j] = q[j];
+        if constexpr (WIDE) {
+            /* ReachAO step_check_collision (reach_ao.py:182-188): the check after substep st - 1
+             * runs inside substep st's contact detection (the same pose); a hit stops the loop
+             * before anything of substep st happens */
+            if (substep_g<OBJ, CONT, PART, AO>(mp, e, q, qd, tq, ob, L, ln, c, lk, AO && st > 0)) {
+                collided = true;
+                break;
+            }
+        } else {
+            substep<OBJ, CONT, AO>(mp, e, q, qd, tq, ob, L, ln);
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; j++) qprev[j] = qstart[j];
+        if constexpr (AO && !WIDE) {   /* ReachAO step_check_collision: check after every substep */
             ao_caps(*fresh(mp), q, *L, ln);
-            const bool hit = WIDE ? ao_collided_g(e, *L, ln, c) : ao_collided(e, *L, ln);
-            if (hit) { collided = true; break; }
+            if (ao_collided(e, *L, ln)) { collided = true; break; }
+        }
+    }
+    if constexpr (AO && WIDE) {   /* the check after the last substep */
+        if (!collided) {
+            ao_caps(*fresh(mp), q, *L, ln);
+            collided = ao_collided_g(e, *L, ln, c);
         }
     }
 
