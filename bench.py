@@ -40,6 +40,26 @@ def alg_flops() -> dict:
     return {k: v["flops_per_env_step"] for k, v in doc["configs"].items()}
 
 
+def pmc(name: str, envs=None):
+    """profiles/<name>.json (tools/pmc_summary_r3.py), or None when absent or for another batch."""
+    p = os.path.join(ROOT, "profiles", name + ".json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        doc = json.load(f)
+    if envs is not None and doc.get("num_envs") != envs:
+        return None
+    return doc
+
+
+def hbm_roofline(alg_bytes: float, ms: float, prof, kernel: str) -> dict:
+    """Algorithmic bytes of one launch over its time, against the HBM peak; traffic = the PMC bytes."""
+    ach = alg_bytes / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "traffic": prof["hbm_bytes_per_launch"] if prof else None, "alg_bytes_per_launch": alg_bytes,
+            "kernel": kernel, "traffic_source": prof["source"] if prof else None}
+
+
 def valu_roofline(key: str, env_steps_per_s: float, what: str) -> dict:
     """rate x algorithmic FLOPs per env-step / the FP32 vector peak."""
     fl = alg_flops()[key]
@@ -155,6 +175,9 @@ def her_leg(dev, calls: int, with_cpu: bool):
         raise RuntimeError(f"HER ring holds {n_valid} valid transitions, expected {N * HER_EP}")
     alg = her_alg_bytes(B, nbv, buf.row_dim, buf.row_stride)
     achieved = alg / (ms * 1e-3) / 1e9
+    prof = pmc("pmc_sample_kernel")
+    if prof and prof.get("alg_bytes_per_launch") != alg:
+        prof = None
     res = {"metric": "HER relabels/s (virtual transitions, future, her_ratio 0.8)", "value": nbv / (ms * 1e-3),
            "unit": "relabels/s", "samples_per_s": B / (ms * 1e-3), "ms_per_call": ms, "calls": calls,
            "ms_per_add": add_ms,
@@ -162,8 +185,9 @@ def her_leg(dev, calls: int, with_cpu: bool):
                                   f"action {HER_AD}, B={B} "
                                   f"(BASELINE configs[3] relabel leg)", "batch": B, "relabels_per_call": nbv},
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "sample_kernel",
-                        "alg_bytes_per_call": alg}}
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": prof["hbm_bytes_per_launch"] if prof else None,
+                        "kernel": "sample_kernel", "alg_bytes_per_call": alg,
+                        "traffic_source": prof["source"] if prof else None}}
     if with_cpu:
         from oracle import her as H
 
@@ -214,6 +238,10 @@ def task_leg(dev, env_id: str, n: int, steps: int, contacts: bool = True, flops_
            "policy": "device Philox random actions (sample_actions + step per step)"}
     if flops_key:
         res["roofline_valu"] = valu_roofline(flops_key, res["value"], "env-steps/s of this leg (sample + step)")
+    alg = {"push": 351.0, "pick_and_place": 359.0}.get(flops_key)   # SURVEY §8d bytes per env-step
+    if alg:
+        prof = pmc("pmc_object_kernel_" + ("push" if flops_key == "push" else "pnp"), n)
+        res["roofline"] = hbm_roofline(alg * n, ms, prof, "step_kernel<0, 1, 1, 0, 1> (object kernel, 16 lanes per env)")
     return res
 
 
@@ -288,7 +316,10 @@ def sharded_leg(dev, env_id: str, n: int, steps: int, warmup: int, dist, rank: i
             "steps": steps, "warmup": warmup, "scaling": "weak",
             "policy": "device Philox random actions, in-kernel collision / success / TimeLimit auto-reset",
             "obs_digest": digest,
-            "roofline_valu": valu_roofline("reach_ao", value / world, "env-steps/s per GPU of this leg")}
+            "roofline_valu": valu_roofline("reach_ao", value / world, "env-steps/s per GPU of this leg"),
+            # ~650 B per env-step (state, obstacles, contact cache, 56-float obs)
+            "roofline": hbm_roofline(650.0 * n, elapsed / steps * 1e3, pmc("pmc_reach_ao_kernel", n),
+                                     "step_kernel_o2<1, 0, 1, 1, 1> (ReachAO, 16 lanes per env)")}
 
 
 def launch_ranks(n: int) -> int:
@@ -402,6 +433,8 @@ def main():
                     valu["issued"] = {"lane_ops_per_env_step": ins / E,
                                       "tflops_equiv": 2.0 * ins / (kernel_ms * 1e-3) / 1e12,
                                       "redundancy": ins / E / valu["alg_flops_per_env_step"],
+                                      "cycles_per_valu_instr": prof.get("cycles_per_valu_instr"),
+                                      "stall_split": prof.get("stall_split"),
                                       "source": os.path.relpath(PROFILE_JSON, ROOT)}
         line = {
             "metric": "aggregate env-steps/s, PandaReach 4096 envs @1 GPU; 1/2/4/8-GPU scaling",
