@@ -358,6 +358,8 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     /* test hook for the exactness of the speculative limit-row skip (substep_g) */
     e.pgs_mode = 0;
     if (const char* pm = std::getenv("PGX_PGS_MODE")) e.pgs_mode = std::atoi(pm);
+    e.wave_mode = 0;
+    if (const char* wm = std::getenv("PGX_WAVES_PER_SIMD")) e.wave_mode = std::atoi(wm);
     /* Round-2 measurements (tools/time_layouts.py, profiles/r02/time_layouts_r02.json): with
      * contacts the wide layout now wins at every batch -- Reach 16384 0.99 vs 1.29 ms, 65536
      * 3.43 vs 4.78; ReachAO 16384 0.78 vs 1.19; PickAndPlace 16384 3.10 vs 3.29 -- so it is

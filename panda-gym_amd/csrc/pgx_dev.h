@@ -64,6 +64,8 @@ struct PgxDevEnv {
     int32_t lanes_per_env;         /* step layout: 1 (env per lane) or 16 (env per DPP row) */
     int32_t pgs_mode;              /* test hook (PGX_PGS_MODE): 0 auto, 2 never speculate on the limit
                                       rows, 3 always redo the speculative solve with them */
+    int32_t wave_mode;             /* A/B hook (PGX_WAVES_PER_SIMD): 0 auto (two resident waves per SIMD
+                                      beyond 1024 waves), 1 the one-wave build, 2 the two-wave build */
 };
 
 struct PgxDevState {

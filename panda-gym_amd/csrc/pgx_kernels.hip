@@ -3552,7 +3552,7 @@ int pgx_launch_step_arm(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevSt
     const int wide = e.lanes_per_env == GW;
     const int per_block = wide ? EPW : 64;
     dim3 block(64), grid((e.n_envs + per_block - 1) / per_block);
-    const bool two = wide && grid.x > 1024;   /* more waves than SIMDs: two per SIMD */
+    const bool two = e.wave_mode == 2 || (e.wave_mode == 0 && wide && grid.x > 1024);   /* more waves than SIMDs */
     switch ((e.control * 4 + (e.contacts ? 1 : 0)) * 2 + wide) {
         case 0: PGX_STEP(0, 0, 0, 0, 0); break;
         case 1: PGX_STEP(0, 0, 0, 0, 1); break;
@@ -3575,7 +3575,7 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
     const int wide = e.lanes_per_env == GW;
     const int per_block = wide ? EPW : 64;
     dim3 block(64), grid((e.n_envs + per_block - 1) / per_block);
-    const bool two = wide && grid.x > 1024;   /* more waves than SIMDs: two per SIMD */
+    const bool two = e.wave_mode == 2 || (e.wave_mode == 0 && wide && grid.x > 1024);   /* more waves than SIMDs */
     const int variant = e.ao ? 13 : e.control * 4 + (e.has_object ? 2 : 0) + (e.contacts ? 1 : 0);
     switch (variant * 2 + wide) {
         case 6: PGX_STEP(0, 1, 1, 0, 0); break;

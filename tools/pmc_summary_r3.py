@@ -11,6 +11,7 @@ SQ_WAIT_ANY + SQ_WAIT_INST_ANY + SQ_ACTIVE_INST_ANY (quad-cycles).
 """
 import csv
 import glob
+import gzip
 import json
 import os
 import shutil
@@ -47,8 +48,10 @@ def main(src=os.path.join(ROOT, "gpurun_out", "pmc_r3"), round_tag="r03"):
         rows += list(csv.DictReader(open(p)))
     dst = os.path.join(ROOT, "profiles", round_tag, "pmc")
     os.makedirs(dst, exist_ok=True)
-    for p in glob.glob(os.path.join(src, "p*", "run_counter_collection.csv")):
-        shutil.copy(p, os.path.join(dst, os.path.basename(os.path.dirname(p)) + "_counter_collection.csv"))
+    for p in glob.glob(os.path.join(src, "p*", "run_counter_collection.csv")):   # kept gzipped
+        with open(p, "rb") as fi, gzip.open(os.path.join(dst, os.path.basename(os.path.dirname(p)) +
+                                                "_counter_collection.csv.gz"), "wb") as fo:
+            shutil.copyfileobj(fi, fo)
     for name, frag, grid, envs, alg in KERNELS:
         agg = defaultdict(list)
         for r in rows:
