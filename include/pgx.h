@@ -252,6 +252,9 @@ int pgx_obs_dim(const pgx_config* cfg);
 int pgx_action_dim(const pgx_config* cfg);
 
 int pgx_create(const pgx_config* cfg, int device, pgx_handle* out);
+/* Host only: the device constant block (PgxDevModel, nbytes = its size) pgx_create folds from cfg;
+ * the build's generator of the kernels' compile-time defaults uses it. */
+int pgx_dev_model_bytes(const pgx_config* cfg, void* out, int64_t nbytes);
 void pgx_destroy(pgx_handle h);
 int pgx_get_state(pgx_handle h, pgx_state_view* out);
 

@@ -13,7 +13,7 @@ from .abi import PgxConfig, PgxReplayBatch, PgxReplayConfig, PgxStateView, PgxSt
 LIB_PATH = os.environ.get("PGX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpgx.so")
 
 EXPORTS = [
-    "pgx_version", "pgx_last_error", "pgx_obs_dim", "pgx_action_dim", "pgx_create", "pgx_destroy",
+    "pgx_version", "pgx_last_error", "pgx_obs_dim", "pgx_action_dim", "pgx_dev_model_bytes", "pgx_create", "pgx_destroy",
     "pgx_get_state", "pgx_reset", "pgx_step", "pgx_sample_actions", "pgx_compute_reward",
     "pgx_state_bytes", "pgx_save_state", "pgx_restore_state",
     "pgx_replay_create", "pgx_replay_destroy", "pgx_replay_add", "pgx_replay_size", "pgx_replay_sample",
@@ -43,6 +43,7 @@ def load(path: str = LIB_PATH):
     lib.pgx_last_error.restype = C.c_char_p
     lib.pgx_obs_dim.argtypes = [C.POINTER(PgxConfig)]
     lib.pgx_action_dim.argtypes = [C.POINTER(PgxConfig)]
+    lib.pgx_dev_model_bytes.argtypes = [C.POINTER(PgxConfig), C.c_void_p, C.c_int64]
     lib.pgx_create.argtypes = [C.POINTER(PgxConfig), C.c_int, C.POINTER(C.c_void_p)]
     lib.pgx_destroy.argtypes = [C.c_void_p]
     lib.pgx_destroy.restype = None

@@ -18,6 +18,7 @@
 #include <string>
 
 #include "../../include/pgx.h"
+#include "pgx_default_model.h"
 #include "pgx_dev.h"
 #include "pgx_model_consts.h"
 #include "pgx_rows.h"
@@ -286,6 +287,19 @@ static int build_dev_model(const pgx_config* cfg, PgxDevModel* dm) {
     return rc;
 }
 
+/* Host only (no HIP call): the constant block pgx_create would upload for cfg, into out
+ * (tools/gen_default_model.py generates the kernels' compile-time default blocks from it). */
+int pgx_dev_model_bytes(const pgx_config* cfg, void* out, int64_t nbytes) {
+    if (!cfg || !out || !cfg->model || !cfg->params) return fail(PGX_E_INVALID, "null argument");
+    if (nbytes != (int64_t)sizeof(PgxDevModel))
+        return fail(PGX_E_INVALID, "device model is %d bytes, got %lld", (int)sizeof(PgxDevModel), (long long)nbytes);
+    PgxDevModel dm;
+    const int rc = build_dev_model(cfg, &dm);
+    if (rc) return rc;
+    std::memcpy(out, &dm, sizeof dm);
+    return PGX_OK;
+}
+
 int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     if (!cfg || !out || !cfg->model || !cfg->params) return fail(PGX_E_INVALID, "null argument");
     *out = nullptr;
@@ -309,6 +323,22 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     h->device = device;
     int rc = build_dev_model(cfg, &h->dm);
     if (rc) { delete h; return rc; }
+#ifndef PGX_RUNTIME_MODEL
+    {   /* the kernels carry the constant block as a compile-time constant (pgx_default_model.h) */
+        static_assert(sizeof(PgxDevModel) == 4 * PGX_DEV_MODEL_WORDS, "default model block size");
+        const PgxDevModelWords& def = cfg->task == PGX_TASK_REACH_AO ? kDefModelAoWords : kDefModelArmWords;
+        uint32_t got[PGX_DEV_MODEL_WORDS];
+        std::memcpy(got, &h->dm, sizeof got);
+        for (int i = 0; i < PGX_DEV_MODEL_WORDS; i++)
+            if (got[i] != def.w[i]) {
+                delete h;
+                return fail(PGX_E_UNSUPPORTED,
+                            "physics / robot parameters differ from the ones the kernels are compiled for "
+                            "(constant block word %d: 0x%08x, compiled 0x%08x; tools/gen_default_model.py)",
+                            i, got[i], def.w[i]);
+            }
+    }
+#endif
     PgxDevEnv& e = h->de;
     e.task = cfg->task;
     e.control = cfg->control;

@@ -24,6 +24,7 @@
 #include <stdint.h>
 
 #include "../../include/pgx.h"
+#include "pgx_default_model.h"
 #include "pgx_common.h"
 #include "pgx_dev.h"
 #include "pgx_model_consts.h"
@@ -51,20 +52,36 @@ namespace {
 
 constexpr int NJ = PGX_NJ;
 
-/* The robot constants (PgxDevModel, ~1.4 KB) live in a device buffer read
- * through the constant address space, so every access is a scalar load
- * (s_load_dwordx16 into SGPRs).  `fresh()` hides the pointer behind an empty
- * asm at the top of each substep / IK iteration: the compiler then re-issues
- * the scalar loads where the values are used instead of hoisting ~350
- * constants out of the loops and spilling them to VGPR lanes (which cost one
- * v_readlane VALU instruction per use). */
+/* The constant block (PgxDevModel: the folded robot and the physics / solver parameters) is a
+ * compile-time constant of the kernels: pgx_create builds the block for a handle and refuses
+ * one that differs from these (the reference's defaults: pybullet's timestep, solver, motor and
+ * contact constants, panda.py's forces and neutral pose; generated into pgx_default_model.h by
+ * tools/gen_default_model.py from pgx_create's own folding), so every parameter folds into the
+ * instruction stream -- no scalar load and wait (SQ_WAIT_ANY was 15 % of the headline's wave
+ * cycles; -2.6 % kernel time).  Two blocks: the robot base of Reach / Push / PickAndPlace and
+ * of ReachAO.  `fresh()` is the identity here.  `make runtime-model` builds the kernels that
+ * read the handle's block instead (other parameters; the round-2 kernels). */
 typedef const __attribute__((address_space(4))) PgxDevModel* MPtr;
 typedef const __attribute__((address_space(4))) PgxDevModel& MRef;
+#ifndef PGX_RUNTIME_MODEL
+static_assert(sizeof(PgxDevModel) == 4 * PGX_DEV_MODEL_WORDS, "default model block size");
+__constant__ const PgxDevModel kDefModelArm = __builtin_bit_cast(PgxDevModel, kDefModelArmWords);
+__constant__ const PgxDevModel kDefModelAo = __builtin_bit_cast(PgxDevModel, kDefModelAoWords);
+template <int AO>
+__device__ __forceinline__ MPtr model_ptr(const PgxDevModel*) { return AO ? (MPtr)&kDefModelAo : (MPtr)&kDefModelArm; }
+__device__ __forceinline__ MPtr fresh(MPtr p) { return p; }
+#else
+/* `make runtime-model` (libpgx_rtmodel.so): any parameters, read from the handle's device block
+ * through scalar loads; the asm hides the pointer at the top of each substep / IK iteration so
+ * the loads are re-issued where used rather than ~350 constants hoisted into VGPR lanes. */
 __device__ __forceinline__ MPtr fresh(uint64_t addr) {
     asm volatile("; pgx fresh model pointer %0" : "+s"(addr));
     return (MPtr)addr;
 }
 __device__ __forceinline__ MPtr fresh(MPtr p) { return fresh((uint64_t)p); }
+template <int AO>
+__device__ __forceinline__ MPtr model_ptr(const PgxDevModel* mdev) { return fresh((uint64_t)mdev); }
+#endif
 
 /* Phase profile (build with -DPGX_PROF, tools/prof_phases.py): per-wave s_memtime
  * deltas accumulated in LDS by phase, summed over waves into pgx_prof_counters at the
@@ -3236,7 +3253,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     g_prof_t = __builtin_amdgcn_s_memtime();
     const unsigned long long prof_t0 = g_prof_t;
 #endif
-    const MPtr mp = fresh((uint64_t)mdev);
+    const MPtr mp = model_ptr<AO>(mdev);   /* the compiled block == *mdev (pgx_create checks) */
     MRef m = *mp;
     float q[NJ], qd[NJ], tq[NJ];
 #pragma unroll
@@ -3454,7 +3471,7 @@ __global__ __launch_bounds__(64) void reset_kernel(const PgxDevModel* __restrict
         __shared__ ContactLds lds_buf;
         L = &lds_buf;
     }
-    MRef m = *fresh((uint64_t)mdev);
+    MRef m = *model_ptr<AO>(mdev);
     if (mask && !mask[i]) return;
     float q[NJ], qd[NJ];
     double goal[3];

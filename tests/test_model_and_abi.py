@@ -4,6 +4,7 @@ import math
 import os
 import re
 import subprocess
+import sys
 import tempfile
 
 import numpy as np
@@ -83,6 +84,24 @@ def test_host_only_calls_without_gpu():
     assert lib.pgx_create(C.byref(cfg), 0, C.byref(h)) < 0      # an object needs the contact solver
     assert b"contacts" in lib.pgx_last_error()
     assert lib.pgx_step(None, None, None, None) < 0
+
+
+def test_compiled_default_model_is_current():
+    """The constant block the kernels are compiled with (pgx_default_model.h) is the one pgx_create
+    folds today for the default parameters; other parameters are refused before any HIP call."""
+    from panda_gym_amd import _native
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import gen_default_model
+
+    txt, _ = gen_default_model.render()
+    assert txt == open(gen_default_model.OUT).read(), "run python tools/gen_default_model.py"
+    lib = _native.load()
+    params = abi.default_sim_params()
+    params.dt *= 2
+    cfg = abi.make_config(abi.EnvSpec(), 8, abi.make_model(load_model("panda_custom0")), params)
+    h = C.c_void_p()
+    assert lib.pgx_create(C.byref(cfg), 0, C.byref(h)) == -3   # PGX_E_UNSUPPORTED
+    assert b"compiled for" in lib.pgx_last_error()
 
 
 def test_struct_layout_matches_c(tmp_path):
