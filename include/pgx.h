@@ -48,7 +48,17 @@ extern "C" {
 #define PGX_MAX_DOFS 9
 #define PGX_MAX_ROWS 27
 #define PGX_MAX_CAPSULES 16
-#define PGX_CONTACT_SLOTS 8        /* 2 contact groups (object-scene, robot) x 4 points */
+/* Contact row budgets per env (Bullet keeps <= 4 points per colliding pair; the kernels keep
+ * the deepest of those up to a fixed budget per group -- DESIGN.md section 4):
+ * object vs table / plane, and robot vs table / plane / object / obstacles, the latter
+ * PGX_ROBOT_POINTS_ONE_LANE by default and with pgx_config.contacts = PGX_CONTACTS_FULL
+ * PGX_ROBOT_POINTS in Push / PickAndPlace and PGX_ROBOT_POINTS_ARM in Reach / ReachAO. */
+#define PGX_OBJECT_POINTS 4
+#define PGX_ROBOT_POINTS 12
+#define PGX_ROBOT_POINTS_ARM 8
+#define PGX_ROBOT_POINTS_ONE_LANE 4
+#define PGX_CONTACT_SLOTS (PGX_OBJECT_POINTS + PGX_ROBOT_POINTS)
+#define PGX_CONTACTS_FULL 2
 
 #define PGX_OK 0
 #define PGX_E_INVALID -1
@@ -179,7 +189,10 @@ typedef struct pgx_config {
     const pgx_model* model;       /* host pointers, copied at create */
     const pgx_sim_params* params;
     /* scene (Task._create_scene, push.py:31-47; pybullet.py:759-817) */
-    int32_t contacts;             /* 1: robot/table/object contacts (the reference's scene) */
+    int32_t contacts;             /* 1: robot/table/object contacts (the reference's scene), the robot
+                                     group's rows budgeted at PGX_ROBOT_POINTS_ONE_LANE (4) points;
+                                     PGX_CONTACTS_FULL: Bullet's per-pair manifolds kept up to
+                                     PGX_ROBOT_POINTS (object tasks) / _ARM points (16-lane layout) */
     int32_t lanes_per_env;        /* step layout: 0 auto (16 with contacts -- every object task
                                      and ReachAO -- at any batch, and up to 8192 envs without),
                                      1 = one env per lane, 16 = one env per 16-lane DPP row */
@@ -237,6 +250,7 @@ typedef struct pgx_state_view {
     int32_t* elapsed;   /* [N] steps in the current episode */
     uint32_t* episode;  /* [N] episodes finished (RNG counter) */
     uint32_t* errors;   /* [1] sticky PGX_ERR_* bits set by the kernels; the host clears them */
+    int32_t robot_points;  /* the robot contact budget of this handle's kernels (0: no contacts) */
 } pgx_state_view;
 
 /* errors word (pgx_state_view.errors): a device-side reset that cannot complete the way the

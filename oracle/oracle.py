@@ -79,10 +79,52 @@ class PgxoStats(C.Structure):
                 ("limits_far", C.c_int32), ("n_contacts", C.c_int32)]
 
 
-OBJ_N = 60   # pos3 quat4 linvel3 angvel3 + 8 x (contact feature id, normal impulse) + ReachAO obstacles
-#              + the cached link pose qc[7] (getLinkState's pose: before the last substep)
-OBJ_QC = 53
-OBJ_AO = 29  # ReachAO: obstacle centres [6][3] at OBJ_AO, active flags [6] at OBJ_AO + 18
+# obj[] (pgx_oracle.h): pos3 quat4 linvel3 angvel3, the contact cache (feature id, normal impulse)
+# x (OBJECT_POINTS + ROBOT_MAX), ReachAO obstacles, the cached link pose qc[7] (getLinkState's
+# pose: before the last substep)
+OBJECT_POINTS = 4     # PGX_OBJECT_POINTS
+ROBOT_POINTS = 12     # PGX_ROBOT_POINTS: robot slots of the kernels' cache (largest budget)
+ROBOT_MAX = 16        # PGXO_ROBOT_MAX: the oracle's robot slots (its largest budget)
+OBJ_CACHE = 13
+OBJ_CACHE1 = OBJ_CACHE + 2 * OBJECT_POINTS
+OBJ_AO = OBJ_CACHE1 + 2 * ROBOT_MAX   # ReachAO: obstacle centres [6][3], active flags [6] at OBJ_AO + 18
+OBJ_QC = OBJ_AO + 24
+OBJ_N = OBJ_QC + 7
+ROBOT_HIST = 33
+
+
+def set_robot_budget(budget: int = -1) -> None:
+    """The oracle's robot contact budget (default / -1: the configuration's -- pgx_config.contacts 1:
+    4 points, PGX_CONTACTS_FULL: 12 with an object, else 8); PandaVecEnv.robot_contact_budget()
+    gives a handle's."""
+    lib().pgxo_set_robot_budget(int(budget))
+
+
+def pair_hist(clear: bool = True) -> np.ndarray:
+    """Per substep since the last clear: how many robot points Bullet's per-pair manifold rule
+    keeps before the budget (index = count, the last bin = that many or more)."""
+    h = np.zeros(ROBOT_HIST, dtype=np.int64)
+    lib().pgxo_pair_hist_read(h.ctypes.data_as(C.c_void_p), int(clear))
+    return h
+
+
+def last_contacts():
+    """The points of the oracle's last contact detection: (group, feature id, link, separation) arrays."""
+    m = OBJECT_POINTS + ROBOT_MAX
+    g, i, l = (np.zeros(m, dtype=np.int32) for _ in range(3))
+    d = np.zeros(m)
+    n = lib().pgxo_last_contacts(*(a.ctypes.data_as(C.c_void_p) for a in (g, i, l, d)))
+    return g[:n], i[:n], l[:n], d[:n]
+
+
+def set_contact_cache(obj: np.ndarray, cache: np.ndarray) -> None:
+    """obj[:, cache] from the kernel's cache [2 * (OBJECT_POINTS + ROBOT_POINTS)] per env
+    (object-scene slots, then robot slots); the oracle's remaining robot slots are empty."""
+    cache = np.asarray(cache, dtype=np.float64)
+    obj[:, OBJ_CACHE:OBJ_AO:2] = -1.0
+    obj[:, OBJ_CACHE + 1:OBJ_AO:2] = 0.0
+    obj[:, OBJ_CACHE:OBJ_CACHE1] = cache[:, :2 * OBJECT_POINTS]
+    obj[:, OBJ_CACHE1:OBJ_CACHE1 + 2 * ROBOT_POINTS] = cache[:, 2 * OBJECT_POINTS:]
 
 
 def _p(a):
@@ -153,6 +195,8 @@ def world_substep(cfg, q, qd, obj, motors):
     q = _d(q).copy()
     qd = _d(qd).copy()
     obj = _d(obj).copy()
+    if obj.shape != (OBJ_N,):
+        raise ValueError(f"obj must have the oracle layout ({OBJ_N} doubles), got {obj.shape}")
     st = PgxoStats()
     lib().pgxo_world_substep(C.byref(cfg), _p(q), _p(qd), _p(obj), motors, C.byref(st))
     return q, qd, obj, st
@@ -227,7 +271,7 @@ class OracleVecEnv:
         self.goal = np.zeros((n, 3))
         self.obj = np.zeros((n, OBJ_N))
         self.obj[:, 6] = 1.0
-        self.obj[:, 13:29:2] = -1.0
+        self.obj[:, OBJ_CACHE:OBJ_AO:2] = -1.0
         self.elapsed = np.zeros(n, dtype=np.int32)
         self.episode = np.zeros(n, dtype=np.uint32)
 

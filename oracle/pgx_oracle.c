@@ -329,12 +329,17 @@ static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x >
  * Contacts restated from Bullet 3.2.x (btMultiBodyDynamicsWorld +
  * btMultiBodyConstraintSolver) -- unpinned: no known answer exists:
  *  - detection at the start of the step, points with separation < contact_distance
- *    (0.02, speculative); two contact groups -- object vs table/plane, robot vs
- *    table/plane/object -- each keeping its 4 deepest points (ties: lower feature id;
- *    4 = btPersistentManifold size, applied per group rather than per link pair to
- *    bound the kernel's per-env row storage); features with a fixed identity (cube
- *    vertex, capsule end, capsule sample sphere) carry the normal impulse to the next
- *    step (warm start x 0.85) like a manifold point does;
+ *    (0.02, speculative); Bullet's manifold rule: one btPersistentManifold of at most
+ *    MANIFOLD_CACHE_SIZE = 4 points per colliding pair (a capsule -- a child shape of its
+ *    link's compound, btCompoundCollisionAlgorithm keeps a manifold per child -- against
+ *    the table, the plane, the cube or an obstacle; the cube against the table or the
+ *    plane), restated as the pair's 4 deepest candidates; then an explicit per-env row
+ *    budget per group (object vs table/plane: PGX_OBJECT_POINTS, robot vs anything:
+ *    robot_budget, the kernel's PGX_ROBOT_POINTS unless a test sets it), the deepest
+ *    first; depth ties: discovery order (capsule, then ends / samples / obstacles), as
+ *    the kernel ranks; rows ordered by feature id.  Features with a fixed identity (cube
+ *    vertex, capsule end, capsule sample sphere, capsule x obstacle) carry the normal
+ *    impulse to the next step (warm start x 0.85) like a manifold point does;
  *  - cube vs table / plane: cube vertices against the top face of the box under them;
  *    robot capsules (model.capsules) vs table / plane: the end spheres; robot capsules
  *    vs cube: spheres sampled along the capsule axis at <= r/2 spacing vs the box;
@@ -350,13 +355,38 @@ static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x >
  * I w (k + k|w|), the base bias term m (w x v) (computeAccelerations...MultiDof:
  * "zeroAccSpatFrc[0].addLinear(m_baseMass * omega.cross(vel))"), gyroscopic w x I w
  * (zero for a cube); orientation by the exponential map (stepPositionsMultiDof). */
-#define OBJ_N 60              /* pos3 quat4 (x,y,z,w) linvel3 angvel3 + 8 x (id, impulse)
-                                 + ReachAO obstacles: centres 6 x 3, active flags 6
-                                 + the cached link pose qc[7] (below) */
-#define OBJ_AO 29
-#define OBJ_QC 53
+/* obj[]: pos3 quat4 (x,y,z,w) linvel3 angvel3, the contact cache (id, impulse) x
+ * (PGX_OBJECT_POINTS + PGXO_ROBOT_MAX), ReachAO obstacles (centres 6 x 3, active flags 6),
+ * the cached link pose qc[7] (below) */
+#define OBJ_CACHE 13
+#define OBJ_CACHE1 (OBJ_CACHE + 2 * PGX_OBJECT_POINTS)
+#define OBJ_AO (OBJ_CACHE1 + 2 * PGXO_ROBOT_MAX)
+#define OBJ_QC (OBJ_AO + 4 * PGX_AO_OBSTACLES)
+#define OBJ_N (OBJ_QC + 7)
+#define N_CACHE (PGX_OBJECT_POINTS + PGXO_ROBOT_MAX)
+typedef char obj_layout_check[(OBJ_N == PGXO_OBJ_N) ? 1 : -1];
 static void quat_mul(const double* a, const double* b, double* o);
-#define NC_MAX PGX_CONTACT_SLOTS
+#define NC_MAX (PGX_OBJECT_POINTS + PGXO_ROBOT_MAX)
+
+/* the robot group's row budget: -1 = the configuration's (pgx_config.contacts: 4, or with
+ * PGX_CONTACTS_FULL PGX_ROBOT_POINTS with an object, else PGX_ROBOT_POINTS_ARM); tests set
+ * others (PGXO_ROBOT_MAX = no budget in practice).  Per substep, the robot points the per-pair
+ * rule keeps before it. */
+static int robot_budget = -1;
+int64_t pgxo_pair_hist[PGXO_ROBOT_HIST];
+void pgxo_set_robot_budget(int b) { robot_budget = b < 0 ? -1 : (b > PGXO_ROBOT_MAX ? PGXO_ROBOT_MAX : b); }
+void pgxo_pair_hist_read(int64_t* out, int clear) {
+    for (int i = 0; i < PGXO_ROBOT_HIST; i++) { out[i] = pgxo_pair_hist[i]; if (clear) pgxo_pair_hist[i] = 0; }
+}
+/* the last detection's points (tests): group, feature id, link, separation */
+static int last_n;
+static int last_grp[PGX_OBJECT_POINTS + PGXO_ROBOT_MAX], last_id[PGX_OBJECT_POINTS + PGXO_ROBOT_MAX],
+    last_link[PGX_OBJECT_POINTS + PGXO_ROBOT_MAX];
+static double last_dist[PGX_OBJECT_POINTS + PGXO_ROBOT_MAX];
+int pgxo_last_contacts(int32_t* grp, int32_t* id, int32_t* link, double* dist) {
+    for (int i = 0; i < last_n; i++) { grp[i] = last_grp[i]; id[i] = last_id[i]; link[i] = last_link[i]; dist[i] = last_dist[i]; }
+    return last_n;
+}
 
 typedef struct {
     int grp, id, link;
@@ -368,6 +398,7 @@ typedef struct {
     double half, mass, inertia;
     double tc[3], th[3], plane_z;
     const double* obst;   /* ReachAO: obstacle centres [6][3] (static colliders), else NULL */
+    int robot_points;     /* the robot group's budget (pgx_config.contacts: 4, or PGX_CONTACTS_FULL's) */
 } world_t;
 
 /* closest pair of a capsule and an obstacle (ReachAO section below): signed distance d,
@@ -390,14 +421,38 @@ static double ground_z(const world_t* W, const double* P) {
     return W->plane_z;
 }
 
-/* keep the 4 deepest candidates (stable for equal depth: earlier = lower id wins) */
-static void keep4(contact_t* sel, int* n, const contact_t* c) {
-    int pos;
-    if (*n < 4) pos = (*n)++;
-    else if (c->dist < sel[3].dist) pos = 3;
-    else return;
-    while (pos > 0 && c->dist < sel[pos - 1].dist) { sel[pos] = sel[pos - 1]; pos--; }
-    sel[pos] = *c;
+/* candidates of one group in discovery order, each with its colliding pair */
+#define CAND_MAX (32 * PGX_MAX_CAPSULES + 8)
+typedef struct {
+    contact_t c[CAND_MAX];
+    int pair[CAND_MAX];
+    int n;
+} cands_t;
+static void cand_add(cands_t* s, const contact_t* c, int pair) {
+    if (s->n < CAND_MAX) { s->c[s->n] = *c; s->pair[s->n] = pair; s->n++; }
+}
+/* candidate j before candidate i: deeper, or as deep and discovered first */
+static int before(const cands_t* s, int j, int i) {
+    return s->c[j].dist < s->c[i].dist || (s->c[j].dist == s->c[i].dist && j < i);
+}
+/* Bullet's manifold rule (<= 4 points per pair: the pair's 4 deepest), then the group's budget
+ * (its `budget` deepest); returns the kept count, *n_pair = the points before the budget */
+static int select_points(const cands_t* s, int budget, contact_t* out, int* n_pair) {
+    int keep[CAND_MAX], np = 0, n = 0;
+    for (int i = 0; i < s->n; i++) {
+        int rank = 0;
+        for (int j = 0; j < s->n; j++) rank += j != i && s->pair[j] == s->pair[i] && before(s, j, i);
+        keep[i] = rank < 4;
+        np += keep[i];
+    }
+    for (int i = 0; i < s->n; i++) {
+        if (!keep[i]) continue;
+        int rank = 0;
+        for (int j = 0; j < s->n; j++) rank += j != i && keep[j] && before(s, j, i);
+        if (rank < budget) out[n++] = s->c[i];
+    }
+    if (n_pair) *n_pair = np;
+    return n;
 }
 static void sort_by_id(contact_t* s, int n) {
     for (int i = 1; i < n; i++)
@@ -413,11 +468,12 @@ static int capsule_samples(const double* a, const double* b, double r) {
 }
 
 /* contact detection; returns the number of contacts (grouped, each group sorted by id) */
+enum { PAIR_TABLE = 0, PAIR_PLANE = 1, PAIR_CUBE = 2, PAIR_OBSTACLE = 3 };   /* + 16 x capsule */
 static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W, const kin_t* k, const double* obj,
                   contact_t* out) {
     const double tau = p->contact_distance;
-    contact_t g0[4], g1[4];
-    int n0 = 0, n1 = 0;
+    static cands_t s0, s1;   /* single-threaded checker */
+    s0.n = 0; s1.n = 0;
     double Rc[9];
     if (W->has_object) {
         quat_to_mat(obj + 3, Rc);
@@ -430,7 +486,7 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
             double d = P[2] - zt;
             if (d < tau) {
                 contact_t c = {0, v, -1, {0, 0, 1}, {P[0], P[1], P[2]}, {P[0], P[1], zt}, d};
-                keep4(g0, &n0, &c);
+                cand_add(&s0, &c, zt == W->plane_z ? PAIR_PLANE : PAIR_TABLE);
             }
         }
     }
@@ -451,7 +507,7 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
                 double d = P[2] - r - zt;
                 if (d < tau) {
                     contact_t c = {1, 2 * ci + e, li, {0, 0, 1}, {P[0], P[1], P[2] - r}, {P[0], P[1], zt}, d};
-                    keep4(g1, &n1, &c);
+                    cand_add(&s1, &c, 16 * ci + (zt == W->plane_z ? PAIR_PLANE : PAIR_TABLE));
                 }
             }
         }
@@ -486,7 +542,7 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
                     m3_v(Rc, nl, c.n);
                     m3_v(Rc, qb, c.pb);
                     for (int i = 0; i < 3; i++) { c.pb[i] += obj[i]; c.pa[i] = C[i] - r * c.n[i]; }
-                    keep4(g1, &n1, &c);
+                    cand_add(&s1, &c, 16 * ci + PAIR_CUBE);
                 }
             }
         }
@@ -504,16 +560,23 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
                 if (cd.d < tau) {
                     contact_t c = {1, 32 + 6 * ci + o, li, {-cd.n[0], -cd.n[1], -cd.n[2]},
                                    {cd.pa[0], cd.pa[1], cd.pa[2]}, {cd.pb[0], cd.pb[1], cd.pb[2]}, cd.d};
-                    keep4(g1, &n1, &c);
+                    cand_add(&s1, &c, 16 * ci + PAIR_OBSTACLE + o);
                 }
             }
         }
     }
-    sort_by_id(g0, n0); sort_by_id(g1, n1);
-    int n = 0;
-    for (int i = 0; i < n0; i++) out[n++] = g0[i];
-    for (int i = 0; i < n1; i++) out[n++] = g1[i];
-    return n;
+    int np1;
+    const int n0 = select_points(&s0, PGX_OBJECT_POINTS, out, NULL);
+    const int budget = robot_budget >= 0 ? robot_budget : W->robot_points;
+    const int n1 = select_points(&s1, budget, out + n0, &np1);
+    pgxo_pair_hist[np1 < PGXO_ROBOT_HIST - 1 ? np1 : PGXO_ROBOT_HIST - 1]++;
+    sort_by_id(out, n0);
+    sort_by_id(out + n0, n1);
+    last_n = n0 + n1;
+    for (int i = 0; i < last_n; i++) {
+        last_grp[i] = out[i].grp; last_id[i] = out[i].id; last_link[i] = out[i].link; last_dist[i] = out[i].dist;
+    }
+    return n0 + n1;
 }
 
 /* btPlaneSpace1 */
@@ -675,8 +738,8 @@ static void substep_impl(const pgx_model* m, const pgx_sim_params* p, const doub
                 R->lo = 0.0;
                 R->hi = 1e10;
                 /* warm start from the same feature's impulse of the previous step */
-                const double* cache = obj + 13 + 8 * (ct->grp != 0);
-                for (int s = 0; s < 4; s++)
+                const double* cache = obj + (ct->grp != 0 ? OBJ_CACHE1 : OBJ_CACHE);
+                for (int s = 0; s < (ct->grp != 0 ? PGXO_ROBOT_MAX : PGX_OBJECT_POINTS); s++)
                     if ((int)cache[2 * s] == ct->id) R->lam = p->warmstart * cache[2 * s + 1];
                 if (R->lam != 0.0) {
                     for (int d = 0; d < nd; d++) dv[d] += R->Rr[d] * R->lam;
@@ -757,13 +820,13 @@ static void substep_impl(const pgx_model* m, const pgx_sim_params* p, const doub
         q[d] += dt * vn[d];
     }
     if (W) { /* contact cache: this step's features and normal impulses, per group */
-        double* cache = obj + 13;
-        for (int s = 0; s < 8; s++) { cache[2 * s] = -1.0; cache[2 * s + 1] = 0.0; }
+        double* cache = obj + OBJ_CACHE;
+        for (int s = 0; s < N_CACHE; s++) { cache[2 * s] = -1.0; cache[2 * s + 1] = 0.0; }
         int used[2] = {0, 0};
         for (int c = 0; c < ncon; c++) {
             int g = con[c].grp != 0, s = used[g]++;
-            cache[8 * g + 2 * s] = con[c].id;
-            cache[8 * g + 2 * s + 1] = cr[3 * c].lam;
+            cache[2 * PGX_OBJECT_POINTS * g + 2 * s] = con[c].id;
+            cache[2 * PGX_OBJECT_POINTS * g + 2 * s + 1] = cr[3 * c].lam;
         }
     }
     if (has_obj) {
@@ -802,6 +865,8 @@ static void world_of(const pgx_config* c, world_t* W) {
     for (int i = 0; i < 3; i++) { W->tc[i] = c->table_center[i]; W->th[i] = c->table_half[i]; }
     W->plane_z = c->plane_z;
     W->obst = NULL;
+    W->robot_points = c->contacts != PGX_CONTACTS_FULL ? PGX_ROBOT_POINTS_ONE_LANE
+                    : (W->has_object ? PGX_ROBOT_POINTS : PGX_ROBOT_POINTS_ARM);
 }
 
 void pgxo_world_substep(const pgx_config* c, double* q, double* qd, double* obj, const pgxo_motor* motors,
@@ -1112,7 +1177,7 @@ static void reset_one(const pgx_config* c, int64_t e, const double* inject_goal,
         obj[3] = 0.0; obj[4] = 0.0; obj[5] = 0.0; obj[6] = 1.0;
     }
     if (obj) {
-        for (int s = 0; s < 8; s++) { obj[13 + 2 * s] = -1.0; obj[13 + 2 * s + 1] = 0.0; }
+        for (int s = 0; s < N_CACHE; s++) { obj[OBJ_CACHE + 2 * s] = -1.0; obj[OBJ_CACHE + 2 * s + 1] = 0.0; }
         memcpy(obj + OBJ_QC, q, 7 * sizeof(double));   /* resetJointState refreshes the link cache */
     }
     *elapsed = 0;
@@ -1472,7 +1537,7 @@ static void ao_reset_one(const pgx_config* c, int64_t e, const double* inject_go
             memcpy(obst + 3 * o, inject_obst + 3 * o, 3 * sizeof(double));
             active[o] = inject_obst[3 * o] < 50.0 ? 1.0 : 0.0;
         }
-    for (int s = 0; s < 8; s++) { obj[13 + 2 * s] = -1.0; obj[13 + 2 * s + 1] = 0.0; }
+    for (int s = 0; s < N_CACHE; s++) { obj[OBJ_CACHE + 2 * s] = -1.0; obj[OBJ_CACHE + 2 * s + 1] = 0.0; }
     memcpy(obj + OBJ_QC, q, 7 * sizeof(double));
     *elapsed = 0;
     *episode += 1;

@@ -45,12 +45,22 @@ int pgxo_ik(const pgx_model* m, const pgx_sim_params* p, const double base[3], c
             pgxo_stats* st);
 void pgxo_substep(const pgx_model* m, const pgx_sim_params* p, const double base[3], double* q,
                   double* qd, const pgxo_motor* motors, pgxo_stats* st);
-/* One substep of the task's scene (table, plane, object, contacts): obj[29] = pos3,
- * quat4 (x,y,z,w), linvel3, angvel3, contact cache 8 x (feature id, normal impulse). */
+/* One substep of the task's scene (table, plane, object, contacts): obj[PGXO_OBJ_N] = pos3,
+ * quat4 (x,y,z,w), linvel3, angvel3, the contact cache (feature id, normal impulse) x
+ * (PGX_OBJECT_POINTS object-scene slots + PGXO_ROBOT_MAX robot slots), then ReachAO's
+ * obstacles and the cached link pose. */
 void pgxo_world_substep(const pgx_config* cfg, double* q, double* qd, double* obj,
                         const pgxo_motor* motors, pgxo_stats* st);
-#define PGXO_OBJ_N 60   /* object (29) + ReachAO obstacle centres [6][3] and active flags [6]
-                           + the cached link pose qc[7] (getLinkState, see pgx_oracle.c) */
+#define PGXO_ROBOT_MAX 16   /* robot contact slots of the oracle's cache (its largest budget) */
+#define PGXO_OBJ_N (13 + 2 * (PGX_OBJECT_POINTS + PGXO_ROBOT_MAX) + 4 * PGX_AO_OBSTACLES + 7)
+/* the robot group's row budget (default / -1: the configuration's, pgx_config.contacts) and
+ * the histogram of robot points Bullet's per-pair rule keeps before the budget, per substep */
+#define PGXO_ROBOT_HIST 33
+void pgxo_set_robot_budget(int budget);
+void pgxo_pair_hist_read(int64_t* out, int clear);
+/* the last contact detection's points (group 0 object-scene / 1 robot-table / 2 robot-object,
+ * feature id, robot link or -1, separation); returns their number */
+int pgxo_last_contacts(int32_t* grp, int32_t* id, int32_t* link, double* dist);
 
 /* ReachAO geometry (test helpers): capsule (A, B, r) vs sphere (C, R) / rounded box
  * (c, h); per-link closest obstacle of the 9 collision links at q, returning the

@@ -17,7 +17,12 @@ from .model import Model, MAX_LINKS, MAX_DOFS, load_model
 
 MAX_ROWS = 27
 MAX_CAPSULES = 16
-CONTACT_SLOTS = 8
+OBJECT_POINTS = 4             # PGX_OBJECT_POINTS: object vs table / plane contact budget
+ROBOT_POINTS = 12             # PGX_ROBOT_POINTS: robot contact budget, Push / PickAndPlace (16 lanes)
+ROBOT_POINTS_ARM = 8          # PGX_ROBOT_POINTS_ARM: Reach / ReachAO (16 lanes)
+ROBOT_POINTS_ONE_LANE = 4     # PGX_ROBOT_POINTS_ONE_LANE: the one-lane layout
+CONTACT_SLOTS = OBJECT_POINTS + ROBOT_POINTS
+CONTACTS_FULL = 2             # PGX_CONTACTS_FULL: pgx_config.contacts for the full manifold budget
 CAP_VS_TABLE, CAP_VS_OBJECT = 1, 2
 
 TASK_REACH, TASK_PUSH, TASK_PICK_AND_PLACE, TASK_REACH_AO = 0, 1, 2, 3
@@ -102,7 +107,7 @@ class PgxStateView(C.Structure):
     _fields_ = [
         ("q", C.c_void_p), ("qd", C.c_void_p), ("qc", C.c_void_p), ("goal", C.c_void_p), ("object", C.c_void_p),
         ("contacts", C.c_void_p), ("obstacles", C.c_void_p), ("elapsed", C.c_void_p), ("episode", C.c_void_p),
-        ("errors", C.c_void_p),
+        ("errors", C.c_void_p), ("robot_points", C.c_int32),
     ]
 
 
@@ -251,7 +256,8 @@ class EnvSpec:
 
 
 def make_config(spec: EnvSpec, n_envs: int, model: PgxModel, params: PgxSimParams, seed: int = 0,
-                env_id_offset: int = 0, contacts: bool = True, lanes_per_env: int = 0) -> PgxConfig:
+                env_id_offset: int = 0, contacts: bool = True, lanes_per_env: int = 0,
+                full_manifold: bool = False) -> PgxConfig:
     c = PgxConfig()
     c.lanes_per_env = lanes_per_env   # step layout: 0 auto, 1 or 16 (include/pgx.h)
     c.task, c.control, c.reward = spec.task, spec.control, spec.reward
@@ -273,7 +279,7 @@ def make_config(spec: EnvSpec, n_envs: int, model: PgxModel, params: PgxSimParam
     c.joint_step = 0.05     # panda.py:74 max_change_position
     c.model = C.pointer(model)
     c.params = C.pointer(params)
-    c.contacts = 1 if contacts else 0
+    c.contacts = (CONTACTS_FULL if full_manifold else 1) if contacts else 0
     half = OBJECT_SIZE / 2
     if spec.task != TASK_REACH:
         c.goal_offset[2] = half                   # push.py:77 / pick_and_place.py:73 (cube centre)

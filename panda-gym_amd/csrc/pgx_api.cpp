@@ -272,7 +272,6 @@ static int build_dev_model(const pgx_config* cfg, PgxDevModel* dm) {
     dm->ik_residual = (float)p->ik_residual;
     dm->ik_damping = (float)p->ik_damping;
     dm->ik_max_angle = (float)p->ik_max_angle;
-    dm->n_substeps = p->n_substeps;
     dm->num_iterations = p->num_iterations;
     dm->ik_max_iters = p->ik_max_iters;
     dm->ee_step = (float)cfg->ee_step;
@@ -313,12 +312,16 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
         return fail(PGX_E_UNSUPPORTED, "ReachAO is built for joint control, blocked gripper and the table scene");
     if (has_object && !cfg->contacts)
         return fail(PGX_E_INVALID, "object tasks need contacts");
+    if (cfg->contacts < 0 || cfg->contacts > PGX_CONTACTS_FULL)
+        return fail(PGX_E_INVALID, "contacts must be 0, 1 or PGX_CONTACTS_FULL, got %d", cfg->contacts);
     if (has_object && (cfg->object_half <= 0 || cfg->object_mass <= 0 || cfg->object_inertia <= 0))
         return fail(PGX_E_INVALID, "object size, mass and inertia must be > 0");
     if (cfg->control != PGX_CONTROL_EE && cfg->control != PGX_CONTROL_JOINTS)
         return fail(PGX_E_INVALID, "control %d", cfg->control);
     if (cfg->reward != PGX_REWARD_SPARSE && cfg->reward != PGX_REWARD_DENSE)
         return fail(PGX_E_INVALID, "reward %d", cfg->reward);
+    if (cfg->params->n_substeps < 1 || cfg->params->n_substeps > 1000)
+        return fail(PGX_E_INVALID, "n_substeps must be in [1, 1000], got %d", cfg->params->n_substeps);
     pgx_env* h = new pgx_env();
     h->device = device;
     int rc = build_dev_model(cfg, &h->dm);
@@ -360,6 +363,7 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     }
     e.goal_z_zero_prob = cfg->goal_z_zero_prob;
     e.contacts = cfg->contacts ? 1 : 0;
+    e.full_manifold = cfg->contacts == PGX_CONTACTS_FULL ? 1 : 0;
     e.has_object = has_object;
     e.obj_half = (float)cfg->object_half;
     e.obj_inv_mass = e.has_object ? (float)(1.0 / cfg->object_mass) : 0.0f;
@@ -388,6 +392,7 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     /* test hook for the exactness of the speculative limit-row skip (substep_g) */
     e.pgs_mode = 0;
     if (const char* pm = std::getenv("PGX_PGS_MODE")) e.pgs_mode = std::atoi(pm);
+    e.n_substeps = cfg->params->n_substeps;
     e.wave_mode = 0;
     if (const char* wm = std::getenv("PGX_WAVES_PER_SIMD")) e.wave_mode = std::atoi(wm);
     /* Round-2 measurements (tools/time_layouts.py, profiles/r02/time_layouts_r02.json): with
@@ -402,6 +407,10 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
         const int v = std::atoi(lpe);
         if (v != 1 && v != 16) { delete h; return fail(PGX_E_INVALID, "PGX_LANES_PER_ENV must be 1 or 16, got %s", lpe); }
         e.lanes_per_env = v;
+    }
+    if (e.full_manifold && e.lanes_per_env != 16) {
+        delete h;
+        return fail(PGX_E_UNSUPPORTED, "PGX_CONTACTS_FULL needs the 16-lane layout (the one-lane kernels keep 4 robot points)");
     }
 
     rc = hip_check(hipSetDevice(device), "hipSetDevice");
@@ -463,6 +472,9 @@ int pgx_get_state(pgx_handle h, pgx_state_view* out) {
     out->elapsed = h->ds.elapsed;
     out->episode = h->ds.episode;
     out->errors = h->ds.errors;
+    out->robot_points = !h->de.contacts ? 0
+                      : !h->de.full_manifold ? PGX_ROBOT_POINTS_ONE_LANE
+                      : h->de.has_object ? PGX_ROBOT_POINTS : PGX_ROBOT_POINTS_ARM;
     return PGX_OK;
 }
 

@@ -34,7 +34,7 @@ struct PgxDevModel {
     float gravity[3];
     float lin_damp, ang_damp, max_vel, residual_thr, erp, limit_max_imp, kp, kd;
     float ik_residual, ik_damping, ik_max_angle;
-    int32_t n_substeps, num_iterations, ik_max_iters;
+    int32_t num_iterations, ik_max_iters;
     float base[3];
     float ee_step, joint_step;
     float neutral_q[PGX_NJ];
@@ -64,6 +64,8 @@ struct PgxDevEnv {
     int32_t lanes_per_env;         /* step layout: 1 (env per lane) or 16 (env per DPP row) */
     int32_t pgs_mode;              /* test hook (PGX_PGS_MODE): 0 auto, 2 never speculate on the limit
                                       rows, 3 always redo the speculative solve with them */
+    int32_t n_substeps;            /* stepSimulation calls per env step (a runtime loop count) */
+    int32_t full_manifold;         /* contacts == PGX_CONTACTS_FULL: robot budget PGX_ROBOT_POINTS(_ARM) */
     int32_t wave_mode;             /* A/B hook (PGX_WAVES_PER_SIMD): 0 auto (two resident waves per SIMD
                                       beyond 1024 waves), 1 the one-wave build, 2 the two-wave build */
 };

@@ -685,46 +685,70 @@ __device__ __forceinline__ V3 ao_table_c(const PgxDevEnv& e) { return v3(e.table
 __device__ __forceinline__ V3 ao_table_h(const PgxDevEnv& e) { return v3(e.table_hx, e.table_hy, e.table_hz); }
 
 /* ------------------------------------------------------------- contacts */
-/* Restated in oracle/pgx_oracle.c ("world: object + contacts"): two contact groups
- * (object vs table/plane, robot vs table/plane/object) of at most CG points each, the
- * deepest first, rows ordered by feature id; normal rows use ERP / speculative rhs, two
- * friction rows per point along btPlaneSpace1(n) bounded by mu * normal impulse.
+/* Restated in oracle/pgx_oracle.c ("world: object + contacts"): Bullet's manifold rule (at
+ * most 4 points per colliding pair: a capsule against the table, the plane, the object or an
+ * obstacle; the object against the table or the plane), then a row budget per group -- the
+ * CG deepest object-scene points and the RB deepest robot points (RB: robot_budget below) --
+ * rows ordered by feature id; normal rows use ERP / speculative rhs, two friction rows per
+ * point along btPlaneSpace1(n) bounded by mu * normal impulse.
  * Per-env contact data lives in LDS, lane-minor (x[...][lane]): conflict-free and
  * dynamically indexable, unlike VGPRs.  Solver rows are float4 records with a 16-B lane
  * stride, so each quad is one conflict-free ds_read_b128 (MI355X_MICROARCH.md, LDS). */
-constexpr int CG = 4;
+constexpr int CG = PGX_OBJECT_POINTS;   /* object-scene budget; robot points whose rows live in VGPRs */
+constexpr int MANIFOLD = 4;             /* btPersistentManifold MANIFOLD_CACHE_SIZE: points per pair */
+
+/* robot points kept per env: the one-lane layout holds its rows in LDS for 64 envs (4); the
+ * wide layout 4 in VGPRs, and with FULL (PGX_FLAG_FULL_MANIFOLD) the rest, up to
+ * PGX_ROBOT_POINTS / _ARM, in LDS (substep_g's "extra rows") */
+template <int W, int OBJ, int FULL>
+constexpr int robot_budget() {
+    return (W == 64 || !FULL) ? PGX_ROBOT_POINTS_ONE_LANE : (OBJ ? PGX_ROBOT_POINTS : PGX_ROBOT_POINTS_ARM);
+}
+static_assert(PGX_ROBOT_POINTS_ONE_LANE == CG, "the one-lane solver holds CG robot points");
 
 constexpr int CACHE_N = 2 * PGX_CONTACT_SLOTS;
+constexpr int CACHE1 = 2 * CG;           /* robot slots of the cache */
 constexpr float kTableIdLimit = 32.0f;   /* robot feature ids < 32: capsule end vs table/plane */
 
-template <int W>
+template <int W, int OBJ = 1, int FULL = 0>
 struct ContactLdsT {
+    static constexpr int RB = robot_budget<W, OBJ, FULL>();
+    /* wide layout: rows 3 p + dir of point p (object-scene points first when OBJ): the
+     * register rows (NQR, robot points < CG) and every row (NQX, robot points < RB) */
+    static constexpr int P0 = OBJ ? CG : 0;
+    static constexpr int NQR = 3 * (P0 + CG), NQX = 3 * (P0 + RB);
+    static constexpr int XR = (W == 64 || RB <= CG) ? 1 : NQX - NQR;   /* extra rows */
     /* group 0: object vertices vs table / plane (normal +z) */
     float4 g0q[CG][4][W];         /* [0] = contact point - object COM; [1 + dir] = (jinv, den, rhs, lambda) */
     float g0d[CG][W], g0id[CG][W];
-    /* group 1: robot vs table / plane / object */
-    float g1p[CG][3][W];          /* point on the robot */
-    float g1n[CG][3][W];          /* normal, from the other body to the robot */
-    float g1rb[CG][3][W];         /* object contacts: point on the object - object COM */
-    float g1d[CG][W], g1id[CG][W];
-    int g1j[CG][W];               /* arm joint carrying the robot link */
-    /* per direction: (J0..3) (J4..6, jinv) (R0..3) (R4..6, den) (cl, rhs) (ca, lambda) with
-     * J the robot Jacobian row, R = M^-1 J^T, (cl, ca) the object part (0 against the table) */
-    float4 g1q[CG][3][6][W];
+    /* group 1: robot vs table / plane / object / obstacles */
+    float g1p[RB][3][W];          /* point on the robot */
+    float g1n[RB][3][W];          /* normal, from the other body to the robot */
+    float g1rb[RB][3][W];         /* object contacts: point on the object - object COM */
+    float g1d[RB][W], g1id[RB][W];
+    int g1j[RB][W];               /* arm joint carrying the robot link */
+    /* one-lane layout, per direction: (J0..3) (J4..6, jinv) (R0..3) (R4..6, den) (cl, rhs) (ca, lambda)
+     * with J the robot Jacobian row, R = M^-1 J^T, (cl, ca) the object part (0 against the table) */
+    float4 g1q[W == 64 ? CG : 1][3][6][W == 64 ? W : 1];
     int cnt[2][W];
-    float cache[CACHE_N][W];      /* (feature id, normal impulse) x 4 per group */
+    float cache[CACHE_N][W];      /* (feature id, normal impulse): CG object-scene slots, then robot slots */
     float capA[PGX_NCAP][3][W], capB[PGX_NCAP][3][W];   /* capsule end points, world */
     /* ReachAO: obstacle centres, per collision link the closest distance and unit vector */
     float aoC[PGX_AO_OBSTACLES][3][W];
     float aoD[PGX_AO_LINKS][W], aoU[PGX_AO_LINKS][3][W];
     /* wide layout: the contact rows' J (13 coordinates) and M^-1 J^T (arm part) per env,
      * row-major [row q][coordinate], so lane q reads its row back with ds_read_b128 (a transpose) */
-    float4 wJ[W == 64 ? 1 : W][6 * CG][4], wR[W == 64 ? 1 : W][6 * CG][2];
+    /* the extra rows (robot points CG..RB-1, the rare path) keep J and M^-1 J^T jinv here for
+     * the whole solve (lane c reads coordinate c), and per row rhs', lambda', lambda' at the
+     * solve's start, the friction bound factor fk and jinv */
+    float4 wJ[W == 64 ? 1 : W][W == 64 ? 1 : NQX][4], wR[W == 64 ? 1 : W][W == 64 ? 1 : NQX][2];
+    float xrhs[XR][W], xlam[XR][W], xlam0[XR][W], xfk[XR][W], xjinv[XR][W];
     /* one-lane speculative solve: the sweep's start velocities (dv, dvl, dvw) for a redo */
     float spec0[W == 64 ? NJ + 6 : 1][W == 64 ? W : 1];
 };
 using ContactLds = ContactLdsT<64>;   /* one env per lane */
-using ContactLdsG = ContactLdsT<EPW>;
+template <int OBJ, int FULL>
+using ContactLdsGT = ContactLdsT<EPW, OBJ, FULL>;
 
 struct ObjState {
     V3 p, v, w;
@@ -777,9 +801,10 @@ __device__ __forceinline__ void g1_copy(LT& L, int ln, int to, int from) {
 }
 template <class LT>
 __device__ __forceinline__ void g1_insert(LT& L, int ln, float d, float id, int j, V3 p, V3 n, V3 rb) {
+    constexpr int RB = LT::RB;   /* the robot group's budget: its RB deepest */
     int c = L.cnt[1][ln], pos;
-    if (c < CG) { pos = c; L.cnt[1][ln] = c + 1; }
-    else if (d < L.g1d[CG - 1][ln]) pos = CG - 1;
+    if (c < RB) { pos = c; L.cnt[1][ln] = c + 1; }
+    else if (d < L.g1d[RB - 1][ln]) pos = RB - 1;
     else return;
     while (pos > 0 && d < L.g1d[pos - 1][ln]) { g1_copy(L, ln, pos, pos - 1); pos--; }
     L.g1d[pos][ln] = d; L.g1id[pos][ln] = id; L.g1j[pos][ln] = j;
@@ -787,7 +812,7 @@ __device__ __forceinline__ void g1_insert(LT& L, int ln, float d, float id, int 
     L.g1n[pos][0][ln] = n.x; L.g1n[pos][1][ln] = n.y; L.g1n[pos][2][ln] = n.z;
     L.g1rb[pos][0][ln] = rb.x; L.g1rb[pos][1][ln] = rb.y; L.g1rb[pos][2][ln] = rb.z;
 }
-/* group 1 by depth (stable insertion sort of <= 4 entries) */
+/* group 1 by depth (stable insertion sort of <= RB entries) */
 template <class LT>
 __device__ __forceinline__ void sort_g1_by_depth(LT& L, int ln) {
     const int c1 = L.cnt[1][ln];
@@ -802,7 +827,7 @@ __device__ __forceinline__ void sort_g1_by_depth(LT& L, int ln) {
             for (int k = 0; k < 3; k++) { L.g1p[j - 1][k][ln] = p[k]; L.g1n[j - 1][k][ln] = n[k]; L.g1rb[j - 1][k][ln] = rb[k]; }
         }
 }
-/* rows are ordered by feature id (insertion sort of <= 4 entries, via a spare slot-free swap) */
+/* rows are ordered by feature id (insertion sort of <= CG / RB entries) */
 template <class LT>
 __device__ __forceinline__ void sort_groups(LT& L, int ln) {
     const int c0 = L.cnt[0][ln];
@@ -857,6 +882,42 @@ __device__ __forceinline__ void object_candidates(const PgxDevEnv& e, float tau,
         if (!(dot(cp, cp) < reach * reach)) return;
     }
     const float inv_n = ns > 1 ? 1.0f / (float)(ns - 1) : 0.0f;
+    /* Bullet's manifold rule: the capsule x object pair keeps at most MANIFOLD points, its
+     * deepest by (depth, sample); with a robot budget above MANIFOLD that cap binds first, so
+     * a depth-only pass finds the pair's MANIFOLD-th key (ds, ss) and only samples up to it
+     * are inserted.  Depth here is the same expression as below (bit-identical). */
+    float dcut = 3.0e38f;
+    int scut = 1 << 20;
+    if (LT::RB > MANIFOLD && ns > MANIFOLD) {
+        float kd[MANIFOLD];
+        int ks[MANIFOLD];
+#pragma unroll
+        for (int t = 0; t < MANIFOLD; t++) { kd[t] = 3.0e38f; ks[t] = 1 << 20; }
+        for (int s = 0; s < ns; s++) {
+            const V3 C = A + ((float)s * inv_n) * ab;
+            const V3 cl = mul_t(Rc, C - ob.p);
+            const V3 qb = v3(fminf(fmaxf(cl.x, -h), h), fminf(fmaxf(cl.y, -h), h), fminf(fmaxf(cl.z, -h), h));
+            const V3 diff = cl - qb;
+            const float d2 = dot(diff, diff);
+            float depth;
+            if (d2 > 1e-24f) depth = fast_sqrt(d2) - r;
+            else depth = -fminf(fminf(h - fabsf(cl.x), h - fabsf(cl.y)), h - fabsf(cl.z)) - r;
+            if (!(depth < tau)) continue;
+            /* insert (depth, s) into the sorted top-MANIFOLD (a later s never displaces an equal depth) */
+            float dv = depth;
+            int sv = s;
+#pragma unroll
+            for (int t = 0; t < MANIFOLD; t++) {
+                const bool lt = dv < kd[t];
+                const float td = kd[t];
+                const int ts = ks[t];
+                kd[t] = lt ? dv : td; ks[t] = lt ? sv : ts;
+                dv = lt ? td : dv; sv = lt ? ts : sv;
+            }
+        }
+        dcut = kd[MANIFOLD - 1];
+        scut = ks[MANIFOLD - 1];
+    }
     for (int s = 0; s < ns; s++) {
         const V3 C = A + ((float)s * inv_n) * ab;
         const V3 cl = mul_t(Rc, C - ob.p);
@@ -883,7 +944,7 @@ __device__ __forceinline__ void object_candidates(const PgxDevEnv& e, float tau,
             if (ax == 2) qb.z = sz * h;
             depth = -best - r;
         }
-        if (depth < tau) {
+        if (depth < tau && (depth < dcut || (depth == dcut && s <= scut))) {
             const V3 n = mul(Rc, nl);
             g1_insert(L, ln, depth, (float)(32 + 16 * c + s), jc, C - r * n, n, mul(Rc, qb));
         }
@@ -983,9 +1044,9 @@ __device__ __forceinline__ void link_capsules(int j, LT& L, int ln, const M3& R,
  *   object: p += dt v, orientation by the exponential map of w dt
  * M by composite-rigid-body, b by Newton-Euler with Bullet's link damping. */
 /* Robot capsule ends vs the table / plane in the wide layout (no object): lane c tests
- * capsule c's end spheres (the candidates of robot_contacts' table branch); the row keeps
- * the 4 deepest by (depth, discovery order) like g1_insert -- ranked by broadcast only when
- * an env has more than 4 -- and every kept candidate goes straight to its id-ordered slot
+ * capsule c's end spheres (the candidates of robot_contacts' table branch; at most 2 per
+ * pair); the row keeps the RB deepest by (depth, discovery order) like g1_insert -- ranked by
+ * broadcast only when an env has more -- and every kept candidate goes straight to its id-ordered slot
  * (ids 2c + end grow with the lane), so sort_groups has nothing left to do. */
 template <class LT>
 __device__ __forceinline__ void robot_table_contacts_g(const PgxDevEnv& e, float tau, LT& L, int es, int c) {
@@ -1000,7 +1061,7 @@ __device__ __forceinline__ void robot_table_contacts_g(const PgxDevEnv& e, float
     unsigned m0 = row_ballot(c0), m1 = row_ballot(c1);
     const int total = __builtin_popcount(m0) + __builtin_popcount(m1);
     bool k0 = c0, k1 = c1;
-    if (__any(total > CG)) {
+    if (__any(total > LT::RB)) {
         /* rank = candidates strictly before in (depth, discovery = 2 lane + end) order */
         const float e0 = c0 ? d0 : 3.0e38f, e1 = c1 ? d1 : 3.0e38f;
         int r0 = 0, r1 = 0;
@@ -1010,8 +1071,8 @@ __device__ __forceinline__ void robot_table_contacts_g(const PgxDevEnv& e, float
             r0 += (y0 < e0 || (y0 == e0 && K < c)) + (y1 < e0 || (y1 == e0 && K < c));
             r1 += (y0 < e1 || (y0 == e1 && K <= c)) + (y1 < e1 || (y1 == e1 && K < c));
         });
-        k0 = c0 && r0 < CG;
-        k1 = c1 && r1 < CG;
+        k0 = c0 && r0 < LT::RB;
+        k1 = c1 && r1 < LT::RB;
         m0 = row_ballot(k0);
         m1 = row_ballot(k1);
     }
@@ -1325,9 +1386,9 @@ __device__ __forceinline__ V3 mul_sym(const float* s, V3 v) {
  * f = z_c x (H - M o_c) and its angular momentum about o_c is n = I_o z_c with
  *   I_o z = I z - 2 (H.o) z + H (o.z) + o (H.z) + M (|o|^2 z - o (o.z)),
  * and M[c][i] = z_i . (n + (o_c - o_i) x f) for i <= c (CRBA), broadcast to every lane. */
-template <int OBJ, int CONT, int AO = 0>
+template <int OBJ, int CONT, int AO = 0, int FULL = 0>
 __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const float* q, const float* qd,
-                                              const ObjState& ob, ContactLdsG* Lp, int es, Dyn& D, int c,
+                                              const ObjState& ob, ContactLdsGT<OBJ, FULL>* Lp, int es, Dyn& D, int c,
                                               const LaneK& K, bool check = false) {
     M3 Rc;
     D.coll = false;
@@ -2086,13 +2147,13 @@ constexpr bool limit_rows_paired() {
     return (PGX_N_ROWS - NJ) % 2 == 0;
 }
 
-template <int OBJ, int CONT, int PART = 1, int AO = 0>
+template <int OBJ, int CONT, int PART = 1, int AO = 0, int FULL = 0>
 __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q, float* qd, const float* tq,
-                                          ObjState& ob, ContactLdsG* Lp, int es, int c, const LaneK& K,
+                                          ObjState& ob, ContactLdsGT<OBJ, FULL>* Lp, int es, int c, const LaneK& K,
                                           bool check = false) {
     MRef m = *fresh(mp);
     Dyn D;
-    substep_dyn_g<OBJ, CONT, AO>(m, e, q, qd, ob, Lp, es, D, c, K, check);
+    substep_dyn_g<OBJ, CONT, AO, FULL>(m, e, q, qd, ob, Lp, es, D, c, K, check);
     if constexpr (AO) {
         if (D.coll) return true;   /* collided at the start pose: this substep does not run */
     }
@@ -2114,12 +2175,16 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     /* ---- contact rows: per lane J_c and (M^-1 J^T)_c, per row rhs / jinv / den / lambda */
     constexpr int P0 = OBJ ? CG : 0;            /* group-1 rows follow group 0's */
     constexpr int NP = P0 + (CONT ? CG : 0);
+    constexpr int RB = CONT ? ContactLdsGT<OBJ, FULL>::RB : CG;   /* robot budget: points CG.. are the extra rows */
+    constexpr int NQR = ContactLdsGT<OBJ, FULL>::NQR;
+    constexpr int NC_ = OBJ ? 13 : NJ;          /* generalized coordinates in lanes */
+    int n1x = 0;                                /* the wave's largest robot point count, when above CG */
     float cJ[NP > 0 ? NP : 1][3], cR[NP > 0 ? NP : 1][3], crhs[NP > 0 ? NP : 1][3], cjinv[NP > 0 ? NP : 1][3];
     float cden[NP > 0 ? NP : 1][3], clam[NP > 0 ? NP : 1][3];
     bool act[NP > 0 ? NP : 1];
     int n0 = 0, n1 = 0;
     if (CONT) {
-        ContactLdsG& L = *Lp;
+        ContactLdsGT<OBJ, FULL>& L = *Lp;
         n0 = L.cnt[0][es];
         n1 = L.cnt[1][es];
         const float erp_dt = m.contact_erp * m.inv_dt;
@@ -2215,6 +2280,74 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 }
             }
         }
+        /* ---- robot points CG..RB-1 (an env with more than CG robot points: fp64 oracle under
+         * the random policy, Push / PickAndPlace 1.2 % of substeps, Reach 1e-5): the same row
+         * setup, kept in LDS for the solve -- J and M^-1 J^T jinv per coordinate lane in the
+         * wJ / wR rows after the register rows, the row scalars per env -- and solved after
+         * the register rows of each half-sweep (extra_rows below) */
+        if constexpr (RB > CG) {
+            for (int k = CG; k < RB && __any(k < n1); k++) n1x = k + 1;
+            n1x = __builtin_amdgcn_readfirstlane(n1x);
+            float* wj = &L.wJ[es][0][0].x;
+            float* wr = &L.wR[es][0][0].x;
+            for (int k = CG; k < n1x; k++) {   /* wave-uniform */
+                const bool a = k < n1;
+                const V3 P = v3(L.g1p[k][0][es], L.g1p[k][1][es], L.g1p[k][2][es]);
+                const V3 n = v3(L.g1n[k][0][es], L.g1n[k][1][es], L.g1n[k][2][es]);
+                const V3 rb = v3(L.g1rb[k][0][es], L.g1rb[k][1][es], L.g1rb[k][2][es]);
+                const int jl = L.g1j[k][es];
+                const float id = L.g1id[k][es];
+                const bool vs_obj = OBJ && id >= kTableIdLimit;
+                float warm = 0.0f;
+                for (int s = 0; s < RB; s++)
+                    if (L.cache[CACHE1 + 2 * s][es] == id) warm = m.warmstart * L.cache[CACHE1 + 2 * s + 1][es];
+                V3 t1, t2;
+                plane_space(n, t1, t2);
+                const V3 Jv = (arm && c <= jl) ? cross(zc, P - oc) : v3(0, 0, 0);
+                float jinv_n = 0.0f;
+#pragma unroll
+                for (int dir = 0; dir < 3; dir++) {
+                    const V3 u = dir == 0 ? n : (dir == 1 ? t1 : t2);
+                    float J = dot(u, Jv);
+                    if (OBJ) {
+                        const V3 ca = cross(rb, u);
+                        const float oj = pick_obj(-1.0f * u, -1.0f * ca);
+                        J = (!arm && vs_obj) ? oj : J;
+                    }
+                    float R = kobj * J;
+                    sfor<0, NJ>([&](auto bc) __attribute__((always_inline)) {
+                        constexpr int b = decltype(bc)::value;
+                        R += mcol[b] * bcast16<b>(J);
+                    });
+                    const float den = sum16(J * R);
+                    const float rel = sum16(J * vu_c);
+                    const float jinv = den > 2.220446e-16f ? fast_rcp(den) : 0.0f;
+                    float rhs;
+                    if (dir == 0) {
+                        const float pen = L.g1d[k][es];
+                        rhs = (pen > 0.0f ? (-rel - pen * m.inv_dt) : (-pen * erp_dt - rel)) * jinv;
+                    } else {
+                        rhs = -rel * jinv;
+                    }
+                    /* as the register rows: inactive -> zero row; scaled units; an unusable row
+                     * (jinv = 0) is inert (bounds 0, its warm start already in gv) */
+                    const float Ja = a ? J : 0.0f, Ra = a ? R : 0.0f, ja = a ? jinv : 0.0f, da = a ? den : 0.0f;
+                    const float lam = (a && dir == 0) ? warm : 0.0f;
+                    gv += Ra * lam;
+                    if (dir == 0) jinv_n = ja;
+                    const bool rok = a && ja != 0.0f;
+                    const bool rok_n = a && jinv_n != 0.0f;
+                    const int q = 3 * (P0 + k) + dir, xq = q - NQR;
+                    if (c < 16) wj[16 * q + c] = c < NC_ ? Ja : 0.0f;
+                    if (c < 8) wr[8 * q + c] = Ra * ja;
+                    /* every lane of the env writes the same (row-uniform) values */
+                    L.xrhs[xq][es] = (a ? rhs : 0.0f) * da;
+                    L.xlam[xq][es] = L.xlam0[xq][es] = rok_n && dir == 0 ? lam * da : 0.0f;
+                    L.xfk[xq][es] = dir == 0 ? (rok ? 3.0e38f : 0.0f) : (rok ? m.friction * jinv_n * da : 0.0f);
+                    L.xjinv[xq][es] = ja;
+                }
+            }
+        }
     }
 
     PGX_PROF_MARK(22);
@@ -2247,7 +2380,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
              * q reads row q back (and row 16 + q into the second register).  Rows of idle points
              * are zero (their J and R are), so every row is written.  One wave per workgroup: LDS
              * ops of the wave complete in order. */
-            ContactLdsG& L = *Lp;
+            ContactLdsGT<OBJ, FULL>& L = *Lp;
             if (c < NC) {
                 float* wj = &L.wJ[es][0][0].x;
                 float* wr = &L.wR[es][0][0].x;
@@ -2475,6 +2608,62 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
      * [lambda', lambda'] with lambda' = 0 -> delta' = 0, bit for bit), so no per-point branch
      * sits inside the sweep.  The object-scene rows (P0 points, a resting cube has 4) run in
      * every sweep of the object tasks, idle points predicated the same way. */
+    /* gw / gw2 = J_l . dv recomputed from the register rows' J (wJ) -- the extra rows update
+     * dv but have no Delassus lanes -- with the arithmetic of their first computation (build) */
+    auto refresh_gw = [&]() __attribute__((always_inline)) {
+        if constexpr (WROWS && RB > CG) {
+            ContactLdsGT<OBJ, FULL>& L = *Lp;
+            auto one = [&](auto reg_c) __attribute__((always_inline)) {
+                constexpr int R0 = decltype(reg_c)::value * GW;
+                const int qr = R0 + c < NQ ? R0 + c : NQ - 1;
+                const float* jrow = &L.wJ[es][qr][0].x;
+                float w = jrow[0] * bcast16<0>(gv);
+                sfor<1, NC>([&](auto lc) __attribute__((always_inline)) {
+                    constexpr int l = decltype(lc)::value;
+                    w = fmaf(jrow[l], bcast16<l>(gv), w);
+                });
+                return R0 + c < NQ ? w : 0.0f;
+            };
+            gw = one(IC<0>{});
+            if constexpr (TWO) gw2 = one(IC<1>{});
+        }
+    };
+    /* the extra rows (robot points CG..n1x-1) of one half-sweep, after the register rows in the
+     * same order as the oracle's (normal rows, then friction rows; points by id): the row
+     * velocity by a 16-lane reduction, the row data from LDS, the same clamp as crow */
+    int rcol = c;   /* the coordinate of lane c's R entry (MODE 3 slot lanes: their dof's) */
+    auto extra_rows = [&](int fr, float& resid) __attribute__((always_inline)) {
+        if constexpr (WROWS && RB > CG) {
+            ContactLdsGT<OBJ, FULL>& L = *Lp;
+            const float* wj = &L.wJ[es][0][0].x;
+            const float* wr = &L.wR[es][0][0].x;
+            for (int k = CG; k < n1x; k++) {
+                for (int dir = fr; dir < (fr ? 3 : 1); dir++) {
+                    const int q = 3 * (P0 + k) + dir, xq = q - NQR;
+                    const float J = wj[16 * q + c];
+                    const float Rs = rcol < 8 ? wr[8 * q + rcol] : kobj * J * L.xjinv[xq][es];
+                    const float w = sum16(J * gv);
+                    const float lm = L.xlam[xq][es], fkv = L.xfk[xq][es];
+                    float lo, hi;
+                    if (dir) {
+                        const float ln_n = L.xlam[xq - dir][es];
+                        const float mk = ln_n > 0.0f ? 1.0f : 0.0f;
+                        const f2 b = ((f2){-fkv, fkv} * ln_n - lm) * mk;
+                        lo = b.x;
+                        hi = b.y;
+                    } else {
+                        lo = -lm;
+                        hi = fkv;
+                    }
+                    const float delta = __builtin_amdgcn_fmed3f(L.xrhs[xq][es] - w, lo, hi);
+                    L.xlam[xq][es] = lm + delta;
+                    gv += Rs * delta;
+                    resid = fmaxf(resid, fabsf(delta));
+                }
+            }
+            refresh_gw();
+        }
+    };
     auto contact_rows = [&](auto nw_c, float& resid) __attribute__((always_inline)) {
         constexpr int NW = decltype(nw_c)::value;
 #pragma unroll
@@ -2493,6 +2682,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                     else crow(IC<P0 + k>{}, IC<0>{}, false, resid);
                 }
             });
+            if (RB > CG && NW == CG && n1x > CG) extra_rows(fr, resid);
         }
     };
     const bool any_contact = CONT && __any(n0 > 0 || n1 > 0);
@@ -2664,6 +2854,8 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 }
                 /* the checks skip the running dofs and the slot lanes */
                 if ((dmask >> c) & 1u) { rl_c = -3.0e38f; ru_c = -3.0e38f; }
+                if (c == SL0) rcol = ds[0];
+                if (KMAX > 1 && nk > 1 && c == SL0 + 1) rcol = ds[1];
                 PGX_PROF_COUNT(16, nk == 2 ? 1 : 0);
                 PGX_PROF_COUNT(18, any_contact ? 1 : 0);
                 if (KMAX == 1 || nk == 1) solve_w(IC<3>{}, IC<1>{});
@@ -2685,6 +2877,12 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                     clam[p][1] = 0.0f;
                     clam[p][2] = 0.0f;
                 }
+                if constexpr (RB > CG) {
+                    if (n1x > CG) {
+                        ContactLdsGT<OBJ, FULL>& L = *Lp;
+                        for (int xq = 0; xq < 3 * (n1x - CG); xq++) L.xlam[xq][es] = L.xlam0[xq][es];
+                    }
+                }
                 init_bounds();
                 solve_w(IC<2>{}, IC<0>{});
             }
@@ -2703,7 +2901,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         q[j] += m.dt * vn;
     });
     if (CONT) { /* contact cache: this step's features and normal impulses */
-        ContactLdsG& L = *Lp;
+        ContactLdsGT<OBJ, FULL>& L = *Lp;
 #pragma unroll
         for (int s = 0; s < CG; s++) {
             if (OBJ) {
@@ -2713,8 +2911,13 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 L.cache[2 * s][es] = -1.0f;
                 L.cache[2 * s + 1][es] = 0.0f;
             }
-            L.cache[8 + 2 * s][es] = s < n1 ? L.g1id[s][es] : -1.0f;
-            L.cache[8 + 2 * s + 1][es] = s < n1 ? clam[P0 + s][0] * cjinv[P0 + s][0] : 0.0f;
+            L.cache[CACHE1 + 2 * s][es] = s < n1 ? L.g1id[s][es] : -1.0f;
+            L.cache[CACHE1 + 2 * s + 1][es] = s < n1 ? clam[P0 + s][0] * cjinv[P0 + s][0] : 0.0f;
+        }
+        for (int s = CG; s < RB; s++) {
+            const int xq = 3 * (s - CG);
+            L.cache[CACHE1 + 2 * s][es] = s < n1 ? L.g1id[s][es] : -1.0f;
+            L.cache[CACHE1 + 2 * s + 1][es] = s < n1 ? L.xlam[xq][es] * L.xjinv[xq][es] : 0.0f;
         }
     }
     if (OBJ) {
@@ -3220,7 +3423,11 @@ __device__ __forceinline__ int xcd_block() {
 template <int CONTROL, int OBJ, int CONT, int AO, int WIDE, int PART = 1>
 __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, const PgxDevEnv& e,
                                           const PgxDevState& s, const float* __restrict__ action, const PgxDevOut& o) {
-    using LT = ContactLdsT<WIDE ? EPW : 64>;
+    /* WIDE: 0 one lane per env, 1 sixteen, 2 sixteen with the full manifold budget */
+    constexpr int FULL = WIDE == 2 ? 1 : 0;
+    using LT = ContactLdsT<WIDE ? EPW : 64, WIDE ? OBJ : 1, FULL>;
+    /* the cache slots this layout uses (the rest stay empty: the reset kernel clears them) */
+    constexpr int CACHE_K = 2 * (CG + LT::RB);
     const int ln = WIDE ? (int)threadIdx.x / GW : (int)threadIdx.x;   /* env slot in the wave (LDS index) */
     const int c = WIDE ? (int)threadIdx.x % GW : 0;                   /* lane within the env's row */
     const bool lead = c == 0;
@@ -3268,7 +3475,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     if (OBJ) load_obj(s, N, ii, ob);
     if (CONT) {
 #pragma unroll
-        for (int k = 0; k < CACHE_N; k++) L->cache[k][ln] = s.contacts[k * N + ii];
+        for (int k = 0; k < CACHE_K; k++) L->cache[k][ln] = s.contacts[k * N + ii];
     }
     if constexpr (AO) ao_load(s, N, ii, *L, ln);
 
@@ -3300,7 +3507,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     PGX_PROF_MARK(0);
     LaneK lk;
     if constexpr (WIDE) lane_consts(lk);
-    const int n_substeps = m.n_substeps;
+    const int n_substeps = e.n_substeps;
     bool collided = false;
     float qprev[NJ];   /* the pose the last substep starts from: getLinkState's cached pose */
     for (int st = 0; st < n_substeps; st++) {
@@ -3311,7 +3518,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
             /* ReachAO step_check_collision (reach_ao.py:182-188): the check after substep st - 1
              * runs inside substep st's contact detection (the same pose); a hit stops the loop
              * before anything of substep st happens */
-            if (substep_g<OBJ, CONT, PART, AO>(mp, e, q, qd, tq, ob, L, ln, c, lk, AO && st > 0)) {
+            if (substep_g<OBJ, CONT, PART, AO, FULL>(mp, e, q, qd, tq, ob, L, ln, c, lk, AO && st > 0)) {
                 collided = true;
                 break;
             }
@@ -3398,7 +3605,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
         el = 0;
         if (CONT) {
 #pragma unroll
-            for (int k = 0; k < CACHE_N; k++) L->cache[k][ln] = (k & 1) ? 0.0f : -1.0f;
+            for (int k = 0; k < CACHE_K; k++) L->cache[k][ln] = (k & 1) ? 0.0f : -1.0f;
         }
     }
     const V3 ag2 = OBJ ? ob.p : pos;
@@ -3424,7 +3631,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     if constexpr (AO) ao_store(s, N, i, *L, ln);
     if (CONT) {
 #pragma unroll
-        for (int k = 0; k < CACHE_N; k++) s.contacts[k * N + i] = L->cache[k][ln];
+        for (int k = 0; k < CACHE_K; k++) s.contacts[k * N + i] = L->cache[k][ln];
     }
     s.elapsed[i] = el;
     s.episode[i] = episode;
@@ -3570,6 +3777,11 @@ int pgx_launch_step_arm(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevSt
     const int per_block = wide ? EPW : 64;
     dim3 block(64), grid((e.n_envs + per_block - 1) / per_block);
     const bool two = e.wave_mode == 2 || (e.wave_mode == 0 && wide && grid.x > 1024);   /* more waves than SIMDs */
+    if (wide && e.contacts && e.full_manifold) {   /* one wave per SIMD: the extra rows' state would spill */
+        if (e.control) PGX_STEP(1, 0, 1, 0, 2);
+        else PGX_STEP(0, 0, 1, 0, 2);
+        return (int)hipGetLastError();
+    }
     switch ((e.control * 4 + (e.contacts ? 1 : 0)) * 2 + wide) {
         case 0: PGX_STEP(0, 0, 0, 0, 0); break;
         case 1: PGX_STEP(0, 0, 0, 0, 1); break;
@@ -3594,6 +3806,15 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
     dim3 block(64), grid((e.n_envs + per_block - 1) / per_block);
     const bool two = e.wave_mode == 2 || (e.wave_mode == 0 && wide && grid.x > 1024);   /* more waves than SIMDs */
     const int variant = e.ao ? 13 : e.control * 4 + (e.has_object ? 2 : 0) + (e.contacts ? 1 : 0);
+    if (wide && e.full_manifold) {
+        switch (variant) {
+            case 3: PGX_STEP(0, 1, 1, 0, 2); break;
+            case 7: PGX_STEP(1, 1, 1, 0, 2); break;
+            case 13: PGX_STEP(1, 0, 1, 1, 2); break;
+            default: return (int)hipErrorInvalidValue;
+        }
+        return (int)hipGetLastError();
+    }
     switch (variant * 2 + wide) {
         case 6: PGX_STEP(0, 1, 1, 0, 0); break;
         case 7: PGX_STEP(0, 1, 1, 0, 1); break;

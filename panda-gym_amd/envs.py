@@ -146,12 +146,15 @@ class PandaVecEnv:
     ``lanes_per_env`` picks the kernel layout (results agree to fp32 rounding): 16 gives
     each env a 16-lane DPP row (the solver's coordinates split over the lanes; fastest
     while the batch is too small to fill the chip one lane per env), 1 one env per lane,
-    0 (default) chooses: 16 with contacts at every batch size, and up to 8192 envs without)."""
+    0 (default) chooses: 16 with contacts at every batch size, and up to 8192 envs without).
+    ``full_manifold`` keeps Bullet's per-pair manifolds (<= 4 points per colliding pair) up to 8
+    robot points per env in Reach / ReachAO and 12 in Push / PickAndPlace (16-lane layout only);
+    the default keeps the 4 deepest robot points (budget, rates, cost)."""
 
     def __init__(self, env_id: str = "PandaReach-v3", num_envs: int = 4096, device: Any = "cuda:0", seed: int = 0,
                  env_id_offset: int = 0, max_episode_steps: Optional[int] = None, auto_reset: bool = True,
                  n_substeps: int = 20, model_name: str = "panda_custom0", contacts: bool = True,
-                 lanes_per_env: int = 0):
+                 lanes_per_env: int = 0, full_manifold: bool = False):
         if torch is None:
             raise PgxError("PandaVecEnv needs torch for device buffers")
         self.lib = load()
@@ -167,7 +170,8 @@ class PandaVecEnv:
         self._model = abi.make_model(load_model(model_name), ee_link=11)
         self._params = abi.default_sim_params(n_substeps=n_substeps)
         self._cfg = abi.make_config(self.spec, self.num_envs, self._model, self._params, seed=seed,
-                                    env_id_offset=env_id_offset, contacts=contacts, lanes_per_env=lanes_per_env)
+                                    env_id_offset=env_id_offset, contacts=contacts, lanes_per_env=lanes_per_env,
+                                    full_manifold=full_manifold)
         # auto_reset=False: a finished env keeps its terminal state until reset (one gymnasium env)
         self._cfg.no_auto_reset = 0 if auto_reset else 1
         self.auto_reset = bool(auto_reset)
@@ -231,8 +235,8 @@ class PandaVecEnv:
     def state(self) -> Dict[str, torch.Tensor]:
         """Device views of the SoA state (q, qd [7,N] f32; qc [7,N] f32 the pose getLinkState reports;
         goal [3,N] f64; object [13,N] f32 =
-        pos, quat (x,y,z,w), linvel, angvel; contacts [16,N] f32 warm-start cache; elapsed,
-        episode [N])."""
+        pos, quat (x,y,z,w), linvel, angvel; contacts [2 * abi.CONTACT_SLOTS, N] f32 warm-start cache
+        (feature id, normal impulse): object-scene slots, then robot slots; elapsed, episode [N])."""
         v = abi.PgxStateView()
         check(self.lib.pgx_get_state(self._h, C.byref(v)), "pgx_get_state")
         n = self.num_envs
@@ -249,6 +253,13 @@ class PandaVecEnv:
             "episode": _view(v.episode, (n,), torch.int32, self.device),
             "errors": _view(v.errors, (1,), torch.int32, self.device),
         }
+
+    def robot_contact_budget(self) -> int:
+        """Robot contact points this handle's kernels keep per env (the deepest of Bullet's <= 4 per
+        colliding pair; abi.ROBOT_POINTS / ROBOT_POINTS_ARM / ROBOT_POINTS_ONE_LANE; 0 without contacts)."""
+        v = abi.PgxStateView()
+        check(self.lib.pgx_get_state(self._h, C.byref(v)), "pgx_get_state")
+        return int(v.robot_points)
 
     def raise_device_errors(self, errors: Optional[int] = None) -> None:
         """Raise what the kernels flagged (pgx_state_view.errors) and clear it.  The device path

@@ -26,6 +26,9 @@ def pg():
 
 
 def _state_to_oracle(venv, ref):
+    from oracle import oracle as orc
+
+    orc.set_robot_budget(venv.robot_contact_budget() or -1)   # the layout's budget
     st = venv.state()
     ref.q[:] = st["q"].double().cpu().numpy().T
     ref.qd[:] = st["qd"].double().cpu().numpy().T
@@ -34,9 +37,9 @@ def _state_to_oracle(venv, ref):
     ref.elapsed[:] = st["elapsed"].cpu().numpy()
     ref.episode[:] = st["episode"].cpu().numpy().view(np.uint32)
     ref.obj[:, :13] = st["object"].double().cpu().numpy().T
-    ref.obj[:, 13:29] = st["contacts"].double().cpu().numpy().T
+    orc.set_contact_cache(ref.obj, st["contacts"].double().cpu().numpy().T)
     if "obstacles" in st:
-        ref.obj[:, 29:53] = st["obstacles"].double().cpu().numpy().T
+        ref.obj[:, orc.OBJ_AO:orc.OBJ_AO + 24] = st["obstacles"].double().cpu().numpy().T
 
 
 def _check_step(out_gpu, out_ref, goal):

@@ -83,6 +83,11 @@ def test_host_only_calls_without_gpu():
     cfg.task, cfg.contacts = abi.TASK_PUSH, 0
     assert lib.pgx_create(C.byref(cfg), 0, C.byref(h)) < 0      # an object needs the contact solver
     assert b"contacts" in lib.pgx_last_error()
+    cfg.contacts, cfg.lanes_per_env = abi.CONTACTS_FULL, 1   # the full manifold budget: 16 lanes only
+    assert lib.pgx_create(C.byref(cfg), 0, C.byref(h)) == -3
+    assert b"16-lane" in lib.pgx_last_error()
+    cfg.contacts = 3
+    assert lib.pgx_create(C.byref(cfg), 0, C.byref(h)) < 0
     assert lib.pgx_step(None, None, None, None) < 0
 
 
@@ -102,6 +107,27 @@ def test_compiled_default_model_is_current():
     h = C.c_void_p()
     assert lib.pgx_create(C.byref(cfg), 0, C.byref(h)) == -3   # PGX_E_UNSUPPORTED
     assert b"compiled for" in lib.pgx_last_error()
+    # the substep count is a runtime loop bound, not part of the block
+    params = abi.default_sim_params(n_substeps=1)
+    cfg = abi.make_config(abi.EnvSpec(), 8, abi.make_model(load_model("panda_custom0")), params)
+    rc = lib.pgx_create(C.byref(cfg), 0, C.byref(h))
+    assert rc != -3 or b"compiled for" not in lib.pgx_last_error()
+    if rc == 0:
+        lib.pgx_destroy(h)
+
+
+def test_constants_match_header():
+    hdr = open(os.path.join(ROOT, "include", "pgx.h")).read()
+
+    def define(name):
+        return int(re.search(rf"#define {name} (\d+)", hdr).group(1))
+
+    from oracle import oracle as orc
+
+    for name in ("OBJECT_POINTS", "ROBOT_POINTS", "ROBOT_POINTS_ARM", "ROBOT_POINTS_ONE_LANE"):
+        assert getattr(abi, name) == define("PGX_" + name), name
+    assert orc.OBJECT_POINTS == abi.OBJECT_POINTS and orc.ROBOT_MAX >= abi.ROBOT_POINTS
+    assert abi.AO_OBSTACLES == define("PGX_AO_OBSTACLES") and abi.MAX_CAPSULES == define("PGX_MAX_CAPSULES")
 
 
 def test_struct_layout_matches_c(tmp_path):
@@ -114,7 +140,7 @@ def test_struct_layout_matches_c(tmp_path):
               "pgx_step_out": ["terminal_achieved_goal", "terminal_desired_goal"],
               "pgx_replay_config": ["reward_type", "distance_threshold", "her_ratio", "seed"],
               "pgx_transition": ["next_obs", "done", "timeout"],
-              "pgx_replay_batch": ["rows", "env", "goal_slot"], "pgx_state_view": ["episode"]}
+              "pgx_replay_batch": ["rows", "env", "goal_slot"], "pgx_state_view": ["episode", "errors", "robot_points"]}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{ROOT}/include/pgx.h"', "int main(){"]
     for s, fs in fields.items():
         lines.append(f'printf("{s} %zu\\n", sizeof({s}));')

@@ -31,9 +31,11 @@ def _motors(oracle, q):
 
 
 def _obj(pos, vel=(0, 0, 0), w=(0, 0, 0), quat=(0, 0, 0, 1)):
-    o = np.zeros(29)
+    from oracle import oracle as orc
+
+    o = np.zeros(orc.OBJ_N)
     o[0:3], o[3:7], o[7:10], o[10:13] = pos, quat, vel, w
-    o[13::2] = -1.0
+    o[orc.OBJ_CACHE:orc.OBJ_AO:2] = -1.0
     return o
 
 
@@ -149,3 +151,67 @@ def test_euler_matches_pybullet_convention(oracle, rpy):
     env.obj[0, 0:3] = (0.0, 0.0, 0.5)
     b = env.step(np.zeros((1, 3), np.float32))   # one step in free fall: orientation unchanged (w = 0)
     assert np.allclose(b["obs"][0, 9:12], rpy, atol=1e-5)
+
+
+# ---------------------------------------------------------------- manifold rule + row budget
+# Bullet keeps one btPersistentManifold of <= 4 points per colliding pair (a capsule -- a child
+# shape of its link's compound -- against the table, the plane, the cube or an obstacle); the
+# build then keeps the deepest points up to a per-env budget (include/pgx.h: with
+# PGX_CONTACTS_FULL 8 robot points in Reach / ReachAO, 12 in Push / PickAndPlace; else 4).  Poses: a resting arm
+# with the hand and a finger on the table (found by sampling joint space), and the cube at the
+# closed fingertips.
+TWO_LINKS_ON_TABLE_Q = [-1.1690350756013894, 0.6106566125901616, 0.23087389083588095, -2.3777880820996167,
+                        0.6961929207547803, 1.5588531369310048, -0.6269433985552224]
+
+
+def _detect(oracle, cfg, q, obj, budget=-1):
+    """one substep from rest at q (motors holding q); the detection's points and the number the
+    per-pair rule keeps before the budget"""
+    oracle.set_robot_budget(budget)
+    try:
+        oracle.pair_hist(clear=True)
+        _run(oracle, cfg, obj, 1, q=q)
+        h = oracle.pair_hist(clear=True)
+        return oracle.last_contacts(), int(np.nonzero(h)[0][0])
+    finally:
+        oracle.set_robot_budget(-1)
+
+
+def _robot(pts):
+    g, i, l, d = pts
+    r = g != 0
+    return i[r], l[r], d[r]
+
+
+def test_two_links_on_table_keep_all_points(oracle):
+    cfg = _cfg(task=abi.TASK_REACH)
+    cfg.contacts = abi.CONTACTS_FULL
+    obj = _obj((0.0, 0.0, 0.0))
+    pts, n_pair = _detect(oracle, cfg, TWO_LINKS_ON_TABLE_Q, obj)
+    ids, links, d = _robot(pts)
+    assert n_pair == 5 and len(ids) == 5                        # all of them (budget 8)
+    assert len(set(links.tolist())) == 2 and np.all(ids < 32)   # two links, capsule ends vs the table
+    assert np.all(d < 0.02) and np.all(np.diff(ids) > 0)        # within tau, rows in id order
+    cfg.contacts = 1                                            # the default budget: the 4 deepest
+    pts4, _ = _detect(oracle, cfg, TWO_LINKS_ON_TABLE_Q, obj)
+    ids4, _, d4 = _robot(pts4)
+    assert len(ids4) == 4 and d4.max() <= np.sort(d)[3]
+
+
+def test_link_on_cube_keeps_all_points_per_pair_cap(oracle):
+    cfg = _cfg(task=abi.TASK_PUSH)
+    cfg.contacts = abi.CONTACTS_FULL
+    env = oracle.OracleVecEnv(cfg, 1)
+    env.reset()   # cfg seed 0
+    ee = env.step(np.zeros((1, 3)))["obs"][0, :3]   # the cube at the closed fingertips, in the air
+    q = env.q[0].copy()
+    pts, n_pair = _detect(oracle, cfg, q, _obj(tuple(ee)))
+    ids, links, d = _robot(pts)
+    assert np.all(ids >= 32)                                    # capsule spheres vs the cube
+    caps = (ids - 32) // 16
+    per_pair = np.bincount(caps)
+    assert per_pair.max() == 4 and (per_pair > 0).sum() >= 2    # >= 2 capsules, each capped at 4
+    assert n_pair == len(ids) > 4                               # the budget (12) cuts nothing
+    cfg.contacts = 1
+    pts4, _ = _detect(oracle, cfg, q, _obj(tuple(ee)))
+    assert len(_robot(pts4)[0]) == 4

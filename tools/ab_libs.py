@@ -13,7 +13,8 @@ import os, sys, json, torch
 sys.path.insert(0, os.getcwd())
 import panda_gym_amd as pg
 env_id, n, contacts = sys.argv[1], int(sys.argv[2]), bool(int(sys.argv[3]))
-venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=0, contacts=contacts)
+kw = json.loads(os.environ.get("AB_KW", "{}"))   # e.g. AB_KW='{"full_manifold": true}'
+venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=0, contacts=contacts, **kw)
 venv.reset_tensors()
 for t in range(30):
     venv.step_tensors(venv.sample_actions(t))

@@ -47,6 +47,6 @@ for t in range(steps):
         print("   ref obs", out["obs"][i, :12])
         print("   pre contacts", pre_c[i])
         print("   gpu contacts", gc[i])
-        print("   ref contacts", ref.obj[i, 13:29])
+        print("   ref contacts", ref.obj[i, 13:53])
     worst.append(max(ee.max(), ob.max()))
 print("max one-step error", max(worst))
