@@ -743,6 +743,9 @@ struct ContactLdsT {
      * solve's start, the friction bound factor fk and jinv */
     float4 wJ[W == 64 ? 1 : W][W == 64 ? 1 : NQX][4], wR[W == 64 ? 1 : W][W == 64 ? 1 : NQX][2];
     float xrhs[XR][W], xlam[XR][W], xlam0[XR][W], xfk[XR][W], xjinv[XR][W];
+    /* the register rows' Delassus entries against the extra rows: lane l of Delassus register b
+     * reads W[16 b + l][extra row] jinv (its gw update for that row's impulse) */
+    float wx[W == 64 ? 1 : W][XR > 1 ? 2 : 1][XR][16];
     /* one-lane speculative solve: the sweep's start velocities (dv, dvl, dvw) for a redo */
     float spec0[W == 64 ? NJ + 6 : 1][W == 64 ? W : 1];
 };
@@ -2429,6 +2432,21 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                     w = fmaf(Jq[l], bcast16<l>(gv), w);
                 });
                 gwr = w;
+                if constexpr (RB > CG) {   /* W[q][x] jinv_x against the extra rows x (rare) */
+                    for (int xq = 0; xq < 3 * (n1x - CG); xq++) {
+                        const int sx = NQR + xq;
+                        const float* js = &L.wJ[es][sx][0].x;
+                        const float* rs = &L.wR[es][sx][0].x;   /* M^-1 J^T jinv, coordinates 0..7 */
+                        const float jv = L.xjinv[xq][es];
+                        float wq = 0.0f;
+                        sfor<0, NC>([&](auto lc) __attribute__((always_inline)) {
+                            constexpr int l = decltype(lc)::value;
+                            const float rl_ = l < 8 ? rs[l] : (l < 10 ? inv_m : inv_i) * js[l] * jv;
+                            wq = fmaf(Jq[l], rl_, wq);
+                        });
+                        L.wx[es][decltype(reg_c)::value][xq][c] = rl ? wq : 0.0f;
+                    }
+                }
             };
             build(IC<0>{}, Wm, Wc, gw);
             /* rows 16..23 belong to robot points 1..3 (slots fill from 0): idle in every env of
@@ -2436,6 +2454,30 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             if constexpr (TWO) { if (g1k_any[1]) build(IC<1>{}, Wm2, Wc2, gw2); }
         }
     }
+    /* the extra rows' scalars into lanes (row x: lane x % 16 of register x / 16) */
+    constexpr int XB = (RB > CG) ? (3 * (RB - CG) + GW - 1) / GW : 1;
+    float xs_rhs[XB], xs_lam[XB], xs_fk[XB], xs_jinv[XB];
+    auto load_xs = [&](bool start) __attribute__((always_inline)) {
+        if constexpr (RB > CG) {
+            ContactLdsGT<OBJ, FULL>& L = *Lp;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+            for (int b = 0; b < XB; b++) {
+                const int xq = GW * b + c;
+                const bool ok = xq < 3 * (n1x - CG);
+                const int xr = ok ? xq : 0;
+                xs_lam[b] = ok ? L.xlam0[xr][es] : 0.0f;
+                if (start) {
+                    xs_rhs[b] = ok ? L.xrhs[xr][es] : 0.0f;
+                    xs_fk[b] = ok ? L.xfk[xr][es] : 0.0f;
+                    xs_jinv[b] = ok ? L.xjinv[xr][es] : 0.0f;
+                }
+            }
+        }
+    };
+#pragma unroll
+    for (int b = 0; b < XB; b++) { xs_rhs[b] = 0.0f; xs_lam[b] = 0.0f; xs_fk[b] = 0.0f; xs_jinv[b] = 0.0f; }
+    if (RB > CG && n1x > CG) load_xs(true);
     PGX_PROF_MARK(23);
 
     /* ---- motor / limit rows (as substep()): per row rhs and lambda, per dof jinv / den */
@@ -2608,60 +2650,49 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
      * [lambda', lambda'] with lambda' = 0 -> delta' = 0, bit for bit), so no per-point branch
      * sits inside the sweep.  The object-scene rows (P0 points, a resting cube has 4) run in
      * every sweep of the object tasks, idle points predicated the same way. */
-    /* gw / gw2 = J_l . dv recomputed from the register rows' J (wJ) -- the extra rows update
-     * dv but have no Delassus lanes -- with the arithmetic of their first computation (build) */
-    auto refresh_gw = [&]() __attribute__((always_inline)) {
-        if constexpr (WROWS && RB > CG) {
-            ContactLdsGT<OBJ, FULL>& L = *Lp;
-            auto one = [&](auto reg_c) __attribute__((always_inline)) {
-                constexpr int R0 = decltype(reg_c)::value * GW;
-                const int qr = R0 + c < NQ ? R0 + c : NQ - 1;
-                const float* jrow = &L.wJ[es][qr][0].x;
-                float w = jrow[0] * bcast16<0>(gv);
-                sfor<1, NC>([&](auto lc) __attribute__((always_inline)) {
-                    constexpr int l = decltype(lc)::value;
-                    w = fmaf(jrow[l], bcast16<l>(gv), w);
-                });
-                return R0 + c < NQ ? w : 0.0f;
-            };
-            gw = one(IC<0>{});
-            if constexpr (TWO) gw2 = one(IC<1>{});
-        }
-    };
     /* the extra rows (robot points CG..n1x-1) of one half-sweep, after the register rows in the
      * same order as the oracle's (normal rows, then friction rows; points by id): the row
-     * velocity by a 16-lane reduction, the row data from LDS, the same clamp as crow */
+     * velocity by a 16-lane reduction (no Delassus lane), J and M^-1 J^T jinv per coordinate
+     * lane and the register rows' couplings from LDS (loads independent of the chain), the row
+     * scalars in lanes of registers (row x: lane x % 16 of xs_*[x / 16]), read by broadcast */
     int rcol = c;   /* the coordinate of lane c's R entry (MODE 3 slot lanes: their dof's) */
-    auto extra_rows = [&](int fr, float& resid) __attribute__((always_inline)) {
+    auto extra_rows = [&](auto fr_c, float& resid) __attribute__((always_inline)) {
         if constexpr (WROWS && RB > CG) {
+            constexpr int FR = decltype(fr_c)::value;
             ContactLdsGT<OBJ, FULL>& L = *Lp;
             const float* wj = &L.wJ[es][0][0].x;
             const float* wr = &L.wR[es][0][0].x;
-            for (int k = CG; k < n1x; k++) {
-                for (int dir = fr; dir < (fr ? 3 : 1); dir++) {
-                    const int q = 3 * (P0 + k) + dir, xq = q - NQR;
-                    const float J = wj[16 * q + c];
-                    const float Rs = rcol < 8 ? wr[8 * q + rcol] : kobj * J * L.xjinv[xq][es];
-                    const float w = sum16(J * gv);
-                    const float lm = L.xlam[xq][es], fkv = L.xfk[xq][es];
-                    float lo, hi;
-                    if (dir) {
-                        const float ln_n = L.xlam[xq - dir][es];
-                        const float mk = ln_n > 0.0f ? 1.0f : 0.0f;
-                        const f2 b = ((f2){-fkv, fkv} * ln_n - lm) * mk;
-                        lo = b.x;
-                        hi = b.y;
-                    } else {
-                        lo = -lm;
-                        hi = fkv;
-                    }
-                    const float delta = __builtin_amdgcn_fmed3f(L.xrhs[xq][es] - w, lo, hi);
-                    L.xlam[xq][es] = lm + delta;
-                    gv += Rs * delta;
-                    resid = fmaxf(resid, fabsf(delta));
+            sfor<0, RB - CG>([&](auto kc) __attribute__((always_inline)) {
+                constexpr int kx = decltype(kc)::value;
+                if (CG + kx < n1x) {
+                    sfor<FR ? 1 : 0, FR ? 3 : 1>([&](auto dc) __attribute__((always_inline)) {
+                        constexpr int dir = decltype(dc)::value, xq = 3 * kx + dir, q = NQR + xq;
+                        constexpr int b = xq / GW, l = xq % GW, bn = (3 * kx) / GW, ln_ = (3 * kx) % GW;
+                        const float J = wj[16 * q + c];
+                        const float jv = bcast16<l>(xs_jinv[b]);
+                        const float Rs = rcol < 8 ? wr[8 * q + rcol] : kobj * J * jv;
+                        const float w = sum16(J * gv);
+                        const float lm = bcast16<l>(xs_lam[b]), fkv = bcast16<l>(xs_fk[b]);
+                        float lo, hi;
+                        if constexpr (dir != 0) {
+                            const float ln_n = bcast16<ln_>(xs_lam[bn]);
+                            const float mk = ln_n > 0.0f ? 1.0f : 0.0f;
+                            const f2 bb = ((f2){-fkv, fkv} * ln_n - lm) * mk;
+                            lo = bb.x;
+                            hi = bb.y;
+                        } else {
+                            lo = -lm;
+                            hi = fkv;
+                        }
+                        const float delta = __builtin_amdgcn_fmed3f(bcast16<l>(xs_rhs[b]) - w, lo, hi);
+                        xs_lam[b] = lane_sel<l>(lm + delta, xs_lam[b]);
+                        gv += Rs * delta;
+                        gw += L.wx[es][0][xq][c] * delta;
+                        if constexpr (TWO) gw2 += L.wx[es][1][xq][c] * delta;
+                        resid = fmaxf(resid, fabsf(delta));
+                    });
                 }
-            }
-            refresh_gw();
+            });
         }
     };
     auto contact_rows = [&](auto nw_c, float& resid) __attribute__((always_inline)) {
@@ -2682,7 +2713,10 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                     else crow(IC<P0 + k>{}, IC<0>{}, false, resid);
                 }
             });
-            if (RB > CG && NW == CG && n1x > CG) extra_rows(fr, resid);
+            if (RB > CG && NW == CG && n1x > CG) {
+                if (fr) extra_rows(IC<1>{}, resid);
+                else extra_rows(IC<0>{}, resid);
+            }
         }
     };
     const bool any_contact = CONT && __any(n0 > 0 || n1 > 0);
@@ -2877,12 +2911,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                     clam[p][1] = 0.0f;
                     clam[p][2] = 0.0f;
                 }
-                if constexpr (RB > CG) {
-                    if (n1x > CG) {
-                        ContactLdsGT<OBJ, FULL>& L = *Lp;
-                        for (int xq = 0; xq < 3 * (n1x - CG); xq++) L.xlam[xq][es] = L.xlam0[xq][es];
-                    }
-                }
+                if (RB > CG && n1x > CG) load_xs(false);
                 init_bounds();
                 solve_w(IC<2>{}, IC<0>{});
             }
@@ -2914,10 +2943,18 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             L.cache[CACHE1 + 2 * s][es] = s < n1 ? L.g1id[s][es] : -1.0f;
             L.cache[CACHE1 + 2 * s + 1][es] = s < n1 ? clam[P0 + s][0] * cjinv[P0 + s][0] : 0.0f;
         }
-        for (int s = CG; s < RB; s++) {
-            const int xq = 3 * (s - CG);
-            L.cache[CACHE1 + 2 * s][es] = s < n1 ? L.g1id[s][es] : -1.0f;
-            L.cache[CACHE1 + 2 * s + 1][es] = s < n1 ? L.xlam[xq][es] * L.xjinv[xq][es] : 0.0f;
+        if constexpr (RB > CG) {
+            if (n1x > CG) {   /* the extra normal rows' impulses: lane x % 16 of xs_lam[x / 16] to LDS */
+#pragma unroll
+                for (int b = 0; b < XB; b++)
+                    if (GW * b + c < 3 * (n1x - CG)) L.xlam[GW * b + c][es] = xs_lam[b];
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            }
+            for (int s = CG; s < RB; s++) {
+                const int xq = 3 * (s - CG);
+                L.cache[CACHE1 + 2 * s][es] = s < n1 ? L.g1id[s][es] : -1.0f;
+                L.cache[CACHE1 + 2 * s + 1][es] = s < n1 ? L.xlam[xq][es] * L.xjinv[xq][es] : 0.0f;
+            }
         }
     }
     if (OBJ) {

@@ -20,7 +20,8 @@ NAMES = ["prologue+IK", "FK+detect", "dynamics", "row setup", "PGS sweeps", "int
 def run(env_id, n, contacts, launches=100, warm=26):
     lib = _native.load()
     buf = (C.c_ulonglong * 24)()
-    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=0, contacts=contacts)
+    kw = json.loads(os.environ.get("PH_KW", "{}"))   # e.g. PH_KW='{"full_manifold": true}'
+    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=0, contacts=contacts, **kw)
     venv.reset_tensors()
     for t in range(warm):
         venv.step_tensors(venv.sample_actions(t))
