@@ -2605,6 +2605,21 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             Wc[q] *= cjinv[q / 3][q % 3];
             if (TWO) Wc2[q] *= cjinv[q / 3][q % 3];
         }
+        /* from here lane q of gw (gw2) holds x_q = rhs'_q - w_q, what its row clamps: a contact row
+         * reads it with one broadcast and every impulse updates it with the negated coupling, so
+         * the rows' rhs' leave the registers (24 per lane in the object tasks) */
+        float r0 = 0.0f, r1 = 0.0f;
+        sfor<0, NQ>([&](auto qc) __attribute__((always_inline)) {
+            constexpr int q = decltype(qc)::value;
+            if constexpr (q < GW) r0 = lane_sel<q>(crhs[q / 3][q % 3], r0);
+            else r1 = lane_sel<q - GW>(crhs[q / 3][q % 3], r1);
+        });
+        gw = r0 - gw;
+        if (TWO) gw2 = r1 - gw2;
+#pragma unroll
+        for (int q = 0; q < NQ; q++) { Wc[q] = -Wc[q]; Wc2[q] = -Wc2[q]; }
+#pragma unroll
+        for (int d = 0; d < NJ; d++) { wms[d] = -wms[d]; wms2[d] = -wms2[d]; }
     }
     /* shifted bounds as for the joint rows: delta' = clamp(rhs' - w, lo' - lambda', hi' - lambda').
      * A normal row's upper bound is +inf (0 with lambda' = 0 for an unusable row, below); a
@@ -2629,8 +2644,8 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             lo = -lm;
             hi = chi[p];
         }
-        const float w = q < GW ? bcast16<q % GW>(gw) : bcast16<q % GW>(gw2);
-        const float delta = __builtin_amdgcn_fmed3f(crhs[p][dir] - w, lo, hi);
+        const float x = q < GW ? bcast16<q % GW>(gw) : bcast16<q % GW>(gw2);   /* rhs' - w */
+        const float delta = __builtin_amdgcn_fmed3f(x, lo, hi);
         clam[p][dir] = lm + delta;
         gv += cR[p][dir] * delta;
         gw += Wc[q] * delta;
@@ -2687,8 +2702,8 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                         const float delta = __builtin_amdgcn_fmed3f(bcast16<l>(xs_rhs[b]) - w, lo, hi);
                         xs_lam[b] = lane_sel<l>(lm + delta, xs_lam[b]);
                         gv += Rs * delta;
-                        gw += L.wx[es][0][xq][c] * delta;
-                        if constexpr (TWO) gw2 += L.wx[es][1][xq][c] * delta;
+                        gw = fmaf(-L.wx[es][0][xq][c], delta, gw);   /* x = rhs' - w: negated coupling */
+                        if constexpr (TWO) gw2 = fmaf(-L.wx[es][1][xq][c], delta, gw2);
                         resid = fmaxf(resid, fabsf(delta));
                     });
                 }
