@@ -743,6 +743,9 @@ struct ContactLdsT {
      * solve's start, the friction bound factor fk and jinv */
     float4 wJ[W == 64 ? 1 : W][W == 64 ? 1 : NQX][4], wR[W == 64 ? 1 : W][W == 64 ? 1 : NQX][2];
     float xrhs[XR][W], xlam[XR][W], xlam0[XR][W], xfk[XR][W], xjinv[XR][W];
+    /* wide layout, the register points' normal rows: jinv (the cache's impulse lambda' jinv)
+     * and lambda' at the solve's start (a redo), kept here through the sweeps */
+    float pjn[W == 64 ? 1 : 2 * CG][W], pl0[W == 64 ? 1 : 2 * CG][W];
     /* the register rows' Delassus entries against the extra rows: lane l of Delassus register b
      * reads W[16 b + l][extra row] jinv (its gw update for that row's impulse) */
     float wx[W == 64 ? 1 : W][XR > 1 ? 2 : 1][XR][16];
@@ -2625,6 +2628,10 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
      * A normal row's upper bound is +inf (0 with lambda' = 0 for an unusable row, below); a
      * friction row is idle (bounds 0) while its normal impulse is 0. */
     float chi[NPP];
+    if constexpr (CONT) {   /* the normal rows' jinv for the cache: in LDS through the sweeps */
+#pragma unroll
+        for (int p = 0; p < NP; p++) Lp->pjn[p][es] = cjinv[p][0];
+    }
 #pragma unroll
     for (int p = 0; p < NP; p++) {
         chi[p] = rok[p][0] ? 3.0e38f : 0.0f;
@@ -2637,7 +2644,8 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         if (fr) {   /* idle while the normal impulse is 0: the bound pair times 0 (an unusable
                      * row has fk = 0 and lambda' = 0, so its bounds are 0 as well) */
             const float mk = ln_n > 0.0f ? 1.0f : 0.0f;
-            const f2 b = ((f2){-fk[p][dir], fk[p][dir]} * ln_n - lm) * mk;
+            const float fkv = fk[p][dir];
+            const f2 b = ((f2){-fkv, fkv} * ln_n - lm) * mk;
             lo = b.x;
             hi = b.y;
         } else {
@@ -2857,9 +2865,10 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 nk = __builtin_popcount(dmask);
             }
             const float gv0 = gv, gw0 = gw, gw20 = gw2;
-            float cl0[NPP];
+            if constexpr (CONT) {   /* the start lambda'_n for a redo: in LDS through the sweeps */
 #pragma unroll
-            for (int p = 0; p < NP; p++) cl0[p] = clam[p][0];
+                for (int p = 0; p < NP; p++) Lp->pl0[p][es] = clam[p][0];
+            }
             if (PART && !spec_all && nk <= KMAX) {
                 PGX_PROF_COUNT(7, 1);
                 /* slots in the pairs' table order; slot lane SL0 + S mirrors dof d_S */
@@ -2922,7 +2931,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 gw2 = gw20;
 #pragma unroll
                 for (int p = 0; p < NP; p++) {
-                    clam[p][0] = cl0[p];
+                    clam[p][0] = CONT ? Lp->pl0[p][es] : 0.0f;
                     clam[p][1] = 0.0f;
                     clam[p][2] = 0.0f;
                 }
@@ -2950,13 +2959,13 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         for (int s = 0; s < CG; s++) {
             if (OBJ) {
                 L.cache[2 * s][es] = s < n0 ? L.g0id[s][es] : -1.0f;
-                L.cache[2 * s + 1][es] = s < n0 ? clam[s][0] * cjinv[s][0] : 0.0f;
+                L.cache[2 * s + 1][es] = s < n0 ? clam[s][0] * L.pjn[s][es] : 0.0f;
             } else {
                 L.cache[2 * s][es] = -1.0f;
                 L.cache[2 * s + 1][es] = 0.0f;
             }
             L.cache[CACHE1 + 2 * s][es] = s < n1 ? L.g1id[s][es] : -1.0f;
-            L.cache[CACHE1 + 2 * s + 1][es] = s < n1 ? clam[P0 + s][0] * cjinv[P0 + s][0] : 0.0f;
+            L.cache[CACHE1 + 2 * s + 1][es] = s < n1 ? clam[P0 + s][0] * L.pjn[P0 + s][es] : 0.0f;
         }
         if constexpr (RB > CG) {
             if (n1x > CG) {   /* the extra normal rows' impulses: lane x % 16 of xs_lam[x / 16] to LDS */

@@ -31,7 +31,7 @@ def main():
         with open(tmp, "w") as f:
             f.write(txt)
         src = tmp
-    flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-fhip-fp32-correctly-rounded-divide-sqrt",
+    flags = [*os.environ.get("REGS_FLAGS", "").split(), "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-fhip-fp32-correctly-rounded-divide-sqrt",
              "-Wno-unused-function", f"-DPGX_TU={args.tu}"]
     if args.tu != "1":
         flags.append("-fno-slp-vectorize")
