@@ -62,14 +62,16 @@ def test_object_reset_and_one_step_parity(pg, oracle, env_id, lanes):
 OUTLIER = 1e-3   # per-step errors above this must be explained by the oracle's own sensitivity
 
 
-def _one_step_errors(pg, oracle, env_id, n, steps, seed, actions=None, lanes=0, outliers=None):
+def _one_step_errors(pg, oracle, env_id, n, steps, seed, actions=None, lanes=0, outliers=None, full=False,
+                     over=None):
     """Per step, from the device state copied into the oracle: |device - oracle| of the EE
     position (obs 0:3) and the achieved goal (EE or object position).  With ``outliers`` (a
     list), every sample above OUTLIER is recorded with its oracle input for _self_sensitivity."""
-    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=seed, lanes_per_env=lanes)
+    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=seed, lanes_per_env=lanes, full_manifold=full)
     venv.reset_tensors(seed=seed)
     ref = oracle.OracleVecEnv(venv._cfg, n)
     ee_err, ag_err = [], []
+    n_obj = 4   # the object-scene slots ahead of the robot slots in the contact cache
     for t in range(steps):
         _state_to_oracle(venv, ref)
         saved = (ref.q.copy(), ref.qd.copy(), ref.goal.copy(), ref.obj.copy(), ref.elapsed.copy(),
@@ -79,6 +81,8 @@ def _one_step_errors(pg, oracle, env_id, n, steps, seed, actions=None, lanes=0, 
         venv.step_tensors(a)
         out = ref.step(a.cpu().numpy())
         obs, ag, dg = _obs(venv)
+        if over is not None:   # envs whose last substep held more than 4 robot points
+            over[0] += int(((venv.state()["contacts"][2 * n_obj::2] >= 0).sum(dim=0) > 4).sum().item())
         assert np.array_equal(venv.truncated.cpu().numpy(), out["truncated"]), t
         if out["truncated"].any():
             continue
@@ -156,6 +160,27 @@ def test_random_policy_one_step_parity(pg, oracle, env_id, lanes):
         assert rec["err_ag"] <= OUTLIER or s_ag >= rec["err_ag"], (rec["t"], rec["env"], rec["err_ag"], s_ag)
     cube = final["object"].cpu().numpy()
     assert cube[2].min() > -0.4
+
+
+@pytest.mark.parametrize("env_id", ["PandaPush-v3", "PandaPickAndPlace-v3"])
+def test_full_manifold_random_policy_one_step_parity(pg, oracle, env_id):
+    """PGX_CONTACTS_FULL (16 lanes, robot budget 12): the same per-step bars as the default
+    budget over a random-policy run in which envs hold more than 4 robot points (the extra
+    rows in LDS), against the oracle at the same budget."""
+    outl, over = [], [0]
+    ee, ag, final = _one_step_errors(pg, oracle, env_id, 256, 50, 21, lanes=16, outliers=outl, full=True, over=over)
+    cfg, _keep = outl.pop()
+    assert over[0] > 0, "no env held more than 4 robot points"
+    for name, e in (("ee", ee), ("object", ag)):
+        assert np.percentile(e, 99) <= 1e-5, (name, np.percentile(e, 99))
+        assert np.percentile(e, 99.9) <= 1e-4, (name, np.percentile(e, 99.9))
+        assert e.max() <= 1e-2, (name, e.max())
+    assert len(outl) <= ee.size // 2000, len(outl)
+    for rec in outl:
+        s_ee, s_ag = _self_sensitivity(oracle, cfg, rec, trials=32)
+        assert rec["err_ee"] <= OUTLIER or s_ee >= rec["err_ee"], (rec["t"], rec["env"], rec["err_ee"], s_ee)
+        assert rec["err_ag"] <= OUTLIER or s_ag >= rec["err_ag"], (rec["t"], rec["env"], rec["err_ag"], s_ag)
+    assert final["object"].cpu().numpy()[2].min() > -0.4
 
 
 def test_scripted_push_moves_cube_like_oracle(pg, oracle):
