@@ -184,18 +184,23 @@ class PandaVecEnv:
         self.seed_value = seed
         n, od = self.num_envs, self.obs_dim
         kw = dict(device=self.device)
-        self.obs = torch.zeros((n, od), dtype=torch.float32, **kw)
-        self.achieved_goal = torch.zeros((n, 3), dtype=torch.float32, **kw)
-        self.desired_goal = torch.zeros((n, 3), dtype=torch.float32, **kw)
-        self.reward = torch.zeros(n, dtype=torch.float32, **kw)
-        self.success = torch.zeros(n, dtype=torch.uint8, **kw)
-        self.terminated = torch.zeros(n, dtype=torch.uint8, **kw)
-        self.truncated = torch.zeros(n, dtype=torch.uint8, **kw)
-        self.terminal_obs = torch.zeros((n, od), dtype=torch.float32, **kw)
-        self.terminal_ag = torch.zeros((n, 3), dtype=torch.float32, **kw)
-        self.terminal_dg = torch.zeros((n, 3), dtype=torch.float32, **kw)
-        # Task.is_truncated (ReachAO is_collided): written by the kernel; zero for the other tasks
-        self.task_trunc = torch.zeros(n, dtype=torch.uint8, **kw)
+        # every step output is a view into one device buffer (f32 arrays, then the u8 flags), so
+        # the SB3 path brings a step back with a single D2H copy
+        f32 = [("obs", (n, od)), ("achieved_goal", (n, 3)), ("desired_goal", (n, 3)), ("reward", (n,)),
+               ("terminal_obs", (n, od)), ("terminal_ag", (n, 3)), ("terminal_dg", (n, 3))]
+        # Task.is_truncated (task_trunc, ReachAO is_collided): written by the kernel; zero for the others
+        u8 = ["success", "terminated", "truncated", "task_trunc"]
+        nf = sum(int(np.prod(shape)) for _, shape in f32)
+        self._outbuf = torch.zeros(4 * nf + len(u8) * n, dtype=torch.uint8, **kw)
+        self._out_f32 = self._outbuf[:4 * nf].view(torch.float32)
+        self._out_u8 = self._outbuf[4 * nf:].view(len(u8), n)
+        o = 0
+        for name, shape in f32:
+            k = int(np.prod(shape))
+            setattr(self, name, self._out_f32[o:o + k].view(shape))
+            o += k
+        for i, name in enumerate(u8):
+            setattr(self, name, self._out_u8[i])
         self._actions = torch.zeros((n, self.action_dim), dtype=torch.float32, **kw)
         self._out = abi.PgxStepOut(self.obs.data_ptr(), self.achieved_goal.data_ptr(), self.desired_goal.data_ptr(),
                                    self.reward.data_ptr(), self.success.data_ptr(), self.terminated.data_ptr(),
@@ -351,14 +356,20 @@ class PandaVecEnv:
             self._hs = {
                 "act": torch.empty((n, ad), **pin), "act_dev": torch.empty((n, ad), dtype=torch.float32,
                                                                            device=self.device),
-                "observation": torch.empty((n, od), **pin), "achieved_goal": torch.empty((n, 3), **pin),
-                "desired_goal": torch.empty((n, 3), **pin), "reward": torch.empty(n, **pin),
-                "flags": torch.empty((4, n), dtype=torch.uint8, pin_memory=True),
-                "flags_dev": torch.empty((4, n), dtype=torch.uint8, device=self.device),
-                "t_observation": torch.empty((n, od), **pin), "t_achieved_goal": torch.empty((n, 3), **pin),
-                "t_desired_goal": torch.empty((n, 3), **pin),
+                "packed": torch.empty(self._outbuf.numel(), dtype=torch.uint8, pin_memory=True),
                 "errors": torch.zeros(1, dtype=torch.int32, pin_memory=True),
+                "errors_dev": self.state()["errors"],   # a view of the library's word (stable)
             }
+            nf = self._out_f32.numel()
+            hf = self._hs["packed"][:4 * nf].view(torch.float32)
+            o = 0
+            for name, shape in (("observation", (n, od)), ("achieved_goal", (n, 3)), ("desired_goal", (n, 3)),
+                                ("reward", (n,)), ("t_observation", (n, od)), ("t_achieved_goal", (n, 3)),
+                                ("t_desired_goal", (n, 3))):
+                k = int(np.prod(shape))
+                self._hs[name] = hf[o:o + k].view(shape)
+                o += k
+            self._hs["flags"] = self._hs["packed"][4 * nf:].view(4, n)   # success, terminated, truncated, task
         return self._hs
 
     def step_async(self, actions) -> None:
@@ -382,16 +393,8 @@ class PandaVecEnv:
         self._pending = None
         hs = self._host_stage()
         stream = torch.cuda.current_stream(self.device)
-        fd = hs["flags_dev"]
-        fd[0].copy_(term)
-        fd[1].copy_(trunc)
-        fd[2].copy_(succ)
-        fd[3].copy_(self.task_trunc)
-        for k, src in (("observation", obs["observation"]), ("achieved_goal", obs["achieved_goal"]),
-                       ("desired_goal", obs["desired_goal"]), ("reward", rew), ("flags", fd),
-                       ("t_observation", self.terminal_obs), ("t_achieved_goal", self.terminal_ag),
-                       ("t_desired_goal", self.terminal_dg), ("errors", self.state()["errors"])):
-            hs[k].copy_(src, non_blocking=True)
+        hs["packed"].copy_(self._outbuf, non_blocking=True)   # every output, one DMA
+        hs["errors"].copy_(hs["errors_dev"], non_blocking=True)
         stream.synchronize()
         if hs["errors"].item():
             self.raise_device_errors(int(hs["errors"].item()))
@@ -399,7 +402,7 @@ class PandaVecEnv:
         o = {k: hs[k].numpy().copy() for k in ("observation", "achieved_goal", "desired_goal")}
         r = hs["reward"].numpy().copy()
         fl = hs["flags"].numpy() != 0
-        te, tr, sc, col = fl[0].copy(), fl[1].copy(), fl[2], fl[3]
+        sc, te, tr, col = fl[0], fl[1].copy(), fl[2].copy(), fl[3]
         d = te | tr
         infos: List[Dict[str, Any]] = [{"is_success": s, "is_truncated": c}
                                        for s, c in zip(sc.tolist(), col.tolist())]
