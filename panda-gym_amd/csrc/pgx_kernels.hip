@@ -756,6 +756,21 @@ using ContactLds = ContactLdsT<64>;   /* one env per lane */
 template <int OBJ, int FULL>
 using ContactLdsGT = ContactLdsT<EPW, OBJ, FULL>;
 
+/* The warm start of feature id: factor x the impulse of the cache slot holding id among slots
+ * first .. first + N - 1 (the last match, as the oracle's loop; 0 without).  Every slot is read
+ * unconditionally and selected, so the reads issue together behind one wait instead of a
+ * compare-branch-read chain per slot. */
+template <int N, class LT>
+__device__ __forceinline__ float warm_lookup(const LT& L, int ln, int first, float id, float factor) {
+    float warm = 0.0f;
+#pragma unroll
+    for (int s = 0; s < N; s++) {
+        const float sid = L.cache[first + 2 * s][ln], imp = L.cache[first + 2 * s + 1][ln];
+        warm = sid == id ? factor * imp : warm;
+    }
+    return warm;
+}
+
 struct ObjState {
     V3 p, v, w;
     float qx, qy, qz, qw;
@@ -1049,6 +1064,27 @@ __device__ __forceinline__ void link_capsules(int j, LT& L, int ln, const M3& R,
  *   qd = clamp(qd_u + M^-1 J^T lambda); q += dt*qd   (constraint pass, stepPositions)
  *   object: p += dt v, orientation by the exponential map of w dt
  * M by composite-rigid-body, b by Newton-Euler with Bullet's link damping. */
+/* Capsule c's table constants for lane c of a 16-lane row (lanes >= PGX_NCAP: capsule 0's, as
+ * the callers' cc = 0), selected from compile-time values: a lane-indexed read of the constant
+ * tables compiles to a global load and a vmcnt wait inside the substep loop. */
+struct CapLane {
+    float r;
+    int flags, ns, j, slot;
+};
+__device__ __forceinline__ CapLane cap_lane() {
+    float r = kCapR[0], fl = (float)kCapFlags[0], ns = (float)kCapNs[0], j = (float)kCapJ[0];
+    float sl = (float)ao_slot(0);
+    sfor<1, PGX_NCAP>([&](auto kc) __attribute__((always_inline)) {
+        constexpr int K = decltype(kc)::value;
+        r = lane_sel<K>(kCapR[K], r);
+        fl = lane_sel<K>((float)kCapFlags[K], fl);
+        ns = lane_sel<K>((float)kCapNs[K], ns);
+        j = lane_sel<K>((float)kCapJ[K], j);
+        sl = lane_sel<K>((float)ao_slot(K), sl);
+    });
+    return CapLane{r, (int)fl, (int)ns, (int)j, (int)sl};
+}
+
 /* Robot capsule ends vs the table / plane in the wide layout (no object): lane c tests
  * capsule c's end spheres (the candidates of robot_contacts' table branch; at most 2 per
  * pair); the row keeps the RB deepest by (depth, discovery order) like g1_insert -- ranked by
@@ -1057,10 +1093,11 @@ __device__ __forceinline__ void link_capsules(int j, LT& L, int ln, const M3& R,
 template <class LT>
 __device__ __forceinline__ void robot_table_contacts_g(const PgxDevEnv& e, float tau, LT& L, int es, int c) {
     const int cc = c < PGX_NCAP ? c : 0;
-    const bool on = c < PGX_NCAP && (kCapFlags[cc] & PGX_CAP_VS_TABLE);
+    const CapLane cl = cap_lane();
+    const bool on = c < PGX_NCAP && (cl.flags & PGX_CAP_VS_TABLE);
     const V3 A = lds3(L.capA[cc], es), B = lds3(L.capB[cc], es);
-    const float r = kCapR[cc];
-    const bool two = kCapNs[cc] != 1;
+    const float r = cl.r;
+    const bool two = cl.ns != 1;
     const float d0 = A.z - r - ground_z(e, A.x, A.y);
     const float d1 = B.z - r - ground_z(e, B.x, B.y);
     const bool c0 = on && d0 < tau, c1 = on && two && d1 < tau;
@@ -1084,7 +1121,7 @@ __device__ __forceinline__ void robot_table_contacts_g(const PgxDevEnv& e, float
     }
     const unsigned below = (1u << (c & 15)) - 1u;
     const int base = __builtin_popcount(m0 & below) + __builtin_popcount(m1 & below);
-    const int jc = kCapJ[cc];
+    const int jc = cl.j;
     if (k0) {
         const int sl = base;
         L.g1d[sl][es] = d0; L.g1id[sl][es] = (float)(2 * c); L.g1j[sl][es] = jc;
@@ -1471,15 +1508,16 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                  * differently. */
                 const float tau = m.contact_dist;
                 const int cc = c < PGX_NCAP ? c : 0;
-                const bool cap_on = c < PGX_NCAP && kCapFlags[cc] != 0;
+                const CapLane cl = cap_lane();
+                const bool cap_on = c < PGX_NCAP && cl.flags != 0;
                 /* check (every substep but the first): the step loop's check_collided of the
                  * previous substep's end pose -- this pose -- fused in here, as ao_collided_g
                  * decides it (same pairs, same arithmetic): lane c's obstacle pairs when c is a
                  * collision link, its table distance for links 2..ee */
-                const int slot = c < PGX_NCAP ? kAoSlot[cc] : -1;
+                const int slot = c < PGX_NCAP ? cl.slot : -1;
                 const bool chk = check && slot >= 0;
                 const V3 A = lds3(Lp->capA[cc], es), B = lds3(Lp->capB[cc], es);
-                const float r = kCapR[cc];
+                const float r = cl.r;
                 const V3 hcube = v3(kAoSize, kAoSize, kAoSize);
                 const int row0 = (int)(threadIdx.x & ~(unsigned)(GW - 1));
                 bool sorted = false, hit = false;
@@ -1530,15 +1568,16 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
              * object anywhere in the wave the robot group holds table candidates only, which
              * robot_table_contacts_g finds lane-parallel (the same candidates, order and ids) */
             const int cc = c < PGX_NCAP ? c : 0;
+            const CapLane cl = cap_lane();
             bool near = false;
-            if (c < PGX_NCAP && (kCapFlags[cc] & PGX_CAP_VS_OBJECT)) {
+            if (c < PGX_NCAP && (cl.flags & PGX_CAP_VS_OBJECT)) {
                 const V3 A = lds3(Lp->capA[cc], es), B = lds3(Lp->capB[cc], es);
                 const V3 ab = B - A;
                 const float l2 = dot(ab, ab);
                 float t = l2 > 0.0f ? dot(ob.p - A, ab) * fast_rcp(l2) : 0.0f;
                 t = fminf(fmaxf(t, 0.0f), 1.0f);
                 const V3 cp = A + t * ab - ob.p;
-                const float reach = kCapR[cc] + 1.7320508f * e.obj_half + m.contact_dist;
+                const float reach = cl.r + 1.7320508f * e.obj_half + m.contact_dist;
                 near = dot(cp, cp) < reach * reach;
             }
             /* table candidates lane-parallel (id-ordered, so re-sorted by depth: ids grow with
@@ -1736,9 +1775,7 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
                 const float4 r4 = L.g0q[k][0][ln];
                 const V3 r = v3(r4.x, r4.y, r4.z);
                 const float id = L.g0id[k][ln];
-                float warm = 0.0f;
-#pragma unroll
-                for (int s = 0; s < CG; s++) if (L.cache[2 * s][ln] == id) warm = m.warmstart * L.cache[2 * s + 1][ln];
+                const float warm = warm_lookup<CG>(L, ln, 0, id, m.warmstart);
 #pragma unroll
                 for (int dir = 0; dir < 3; dir++) {
                     /* u = +z, -y, +x (btPlaneSpace1(+z)); ang = r x u */
@@ -1766,10 +1803,7 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
                 const int jl = L.g1j[k][ln];
                 const float id = L.g1id[k][ln];
                 const bool vs_obj = OBJ && id >= kTableIdLimit;
-                float warm = 0.0f;
-#pragma unroll
-                for (int s = 0; s < CG; s++)
-                    if (L.cache[8 + 2 * s][ln] == id) warm = m.warmstart * L.cache[8 + 2 * s + 1][ln];
+                const float warm = warm_lookup<CG>(L, ln, CACHE1, id, m.warmstart);
                 V3 t1, t2;
                 plane_space(n, t1, t2);
                 V3 Jv[NJ];
@@ -2194,15 +2228,28 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         n0 = L.cnt[0][es];
         n1 = L.cnt[1][es];
         const float erp_dt = m.contact_erp * m.inv_dt;
+        /* the warm-start cache slots, read once for every point (ids, impulses) */
+        float cid0[CG], cim0[CG], cid1[CG], cim1[CG];
+#pragma unroll
+        for (int s2 = 0; s2 < CG; s2++) {
+            cid0[s2] = OBJ ? L.cache[2 * s2][es] : -1.0f;
+            cim0[s2] = OBJ ? L.cache[2 * s2 + 1][es] : 0.0f;
+            cid1[s2] = L.cache[CACHE1 + 2 * s2][es];
+            cim1[s2] = L.cache[CACHE1 + 2 * s2 + 1][es];
+        }
+        auto warm_of = [&](const float* ids, const float* ims, float id) __attribute__((always_inline)) {
+            float w = 0.0f;
+#pragma unroll
+            for (int s2 = 0; s2 < CG; s2++) w = ids[s2] == id ? m.warmstart * ims[s2] : w;
+            return w;
+        };
 #pragma unroll
         for (int k = 0; k < P0; k++) { /* object vertices vs the box top: object coordinates only */
             act[k] = k < n0;
             const float4 r4 = L.g0q[k][0][es];
             const V3 r = v3(r4.x, r4.y, r4.z);
             const float id = L.g0id[k][es];
-            float warm = 0.0f;
-#pragma unroll
-            for (int s = 0; s < CG; s++) if (L.cache[2 * s][es] == id) warm = m.warmstart * L.cache[2 * s + 1][es];
+            const float warm = warm_of(cid0, cim0, id);
 #pragma unroll
             for (int dir = 0; dir < 3; dir++) {
                 const V3 lin = dir == 0 ? v3(0, 0, 1) : (dir == 1 ? v3(0, -1, 0) : v3(1, 0, 0));
@@ -2245,10 +2292,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 const int jl = L.g1j[k][es];
                 const float id = L.g1id[k][es];
                 const bool vs_obj = OBJ && id >= kTableIdLimit;
-                float warm = 0.0f;
-#pragma unroll
-                for (int s = 0; s < CG; s++)
-                    if (L.cache[8 + 2 * s][es] == id) warm = m.warmstart * L.cache[8 + 2 * s + 1][es];
+                const float warm = warm_of(cid1, cim1, id);
                 V3 t1, t2;
                 plane_space(n, t1, t2);
                 const V3 Jv = (arm && c <= jl) ? cross(zc, P - oc) : v3(0, 0, 0);
@@ -2304,9 +2348,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 const int jl = L.g1j[k][es];
                 const float id = L.g1id[k][es];
                 const bool vs_obj = OBJ && id >= kTableIdLimit;
-                float warm = 0.0f;
-                for (int s = 0; s < RB; s++)
-                    if (L.cache[CACHE1 + 2 * s][es] == id) warm = m.warmstart * L.cache[CACHE1 + 2 * s + 1][es];
+                const float warm = warm_lookup<RB>(L, es, CACHE1, id, m.warmstart);
                 V3 t1, t2;
                 plane_space(n, t1, t2);
                 const V3 Jv = (arm && c <= jl) ? cross(zc, P - oc) : v3(0, 0, 0);
@@ -3244,11 +3286,12 @@ __device__ __forceinline__ bool ao_collided_g(const PgxDevEnv& e, LT& L, int es,
     const V3 thi = v3(th.x - kAoMargin, th.y - kAoMargin, th.z - kAoMargin);
     const V3 hcube = v3(kAoSize, kAoSize, kAoSize);
     const int cc = c < PGX_NCAP ? c : 0;
-    const int slot = c < PGX_NCAP ? kAoSlot[cc] : -1;
+    const CapLane cl = cap_lane();
+    const int slot = c < PGX_NCAP ? cl.slot : -1;
     bool hit = false;
     if (slot >= 0) {
         const V3 A = lds3(L.capA[cc], es), B = lds3(L.capB[cc], es);
-        const float r = kCapR[cc];
+        const float r = cl.r;
         for (int o = 0; o < AO_N; o++) {
             const V3 C = lds3(L.aoC[o], es);
             const V3 P = seg_closest(A, B, C);
@@ -3272,12 +3315,13 @@ template <class LT>
 __device__ __forceinline__ void ao_link_obs_g(LT& L, int es, int c) {
     const V3 hcube = v3(kAoSize, kAoSize, kAoSize);
     const int cc = c < PGX_NCAP ? c : 0;
-    const int slot = c < PGX_NCAP ? kAoSlot[cc] : -1;
+    const CapLane cl = cap_lane();
+    const int slot = c < PGX_NCAP ? cl.slot : -1;
     float best = 3.0e38f;
     V3 bu = v3(0.0f, 0.0f, 0.0f);
     if (slot >= 0) {
         const V3 A = lds3(L.capA[cc], es), B = lds3(L.capB[cc], es);
-        const float r = kCapR[cc];
+        const float r = cl.r;
         for (int o = 0; o < AO_N; o++) {
             const V3 C = lds3(L.aoC[o], es);
             const V3 P = seg_closest(A, B, C);
