@@ -2276,6 +2276,24 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         }
         /* robot vs table / plane / object: this lane's joint axis and pivot */
         const V3 zc = pick_v3(z), oc = pick_v3(o);
+        /* the points' records read up front, one batch behind one wait (read inside each point's
+         * branch they cost a wait per point) */
+        V3 gP[CG], gN[CG], gRb[CG];
+        int gJ[CG];
+        float gId[CG], gD[CG];
+        auto read_point = [&](int k) __attribute__((always_inline)) {
+            gP[k] = v3(L.g1p[k][0][es], L.g1p[k][1][es], L.g1p[k][2][es]);
+            gN[k] = v3(L.g1n[k][0][es], L.g1n[k][1][es], L.g1n[k][2][es]);
+            gRb[k] = OBJ ? v3(L.g1rb[k][0][es], L.g1rb[k][1][es], L.g1rb[k][2][es]) : v3(0.0f, 0.0f, 0.0f);
+            gJ[k] = L.g1j[k][es];
+            gId[k] = L.g1id[k][es];
+            gD[k] = L.g1d[k][es];
+        };
+        /* (ReachAO: points are rare and the o2 kernel's registers scarce: read per point) */
+        if (!AO && __any(n1 > 0)) {
+#pragma unroll
+            for (int k = 0; k < CG; k++) read_point(k);
+        }
 #pragma unroll
         for (int k = 0; k < (CONT ? CG : 0); k++) {
             const int p = P0 + k;
@@ -2286,11 +2304,12 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 cjinv[p][dir] = 0.0f; cden[p][dir] = 0.0f; clam[p][dir] = 0.0f;
             }
             if (__any(act[p])) {   /* wave-uniform; robot points are sparse */
-                const V3 P = v3(L.g1p[k][0][es], L.g1p[k][1][es], L.g1p[k][2][es]);
-                const V3 n = v3(L.g1n[k][0][es], L.g1n[k][1][es], L.g1n[k][2][es]);
-                const V3 rb = v3(L.g1rb[k][0][es], L.g1rb[k][1][es], L.g1rb[k][2][es]);
-                const int jl = L.g1j[k][es];
-                const float id = L.g1id[k][es];
+                if (AO) read_point(k);
+                const V3 P = gP[k];
+                const V3 n = gN[k];
+                const V3 rb = gRb[k];
+                const int jl = gJ[k];
+                const float id = gId[k];
                 const bool vs_obj = OBJ && id >= kTableIdLimit;
                 const float warm = warm_of(cid1, cim1, id);
                 V3 t1, t2;
@@ -2315,7 +2334,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                     const float jinv = den > 2.220446e-16f ? fast_rcp(den) : 0.0f;
                     float rhs;
                     if (dir == 0) {
-                        const float pen = L.g1d[k][es];
+                        const float pen = gD[k];
                         rhs = (pen > 0.0f ? (-rel - pen * m.inv_dt) : (-pen * erp_dt - rel)) * jinv;
                     } else {
                         rhs = -rel * jinv;
@@ -2997,17 +3016,21 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     });
     if (CONT) { /* contact cache: this step's features and normal impulses */
         ContactLdsGT<OBJ, FULL>& L = *Lp;
+        /* every slot's id and jinv read unconditionally (one batch, one wait), then selected */
+        float gid0[CG], pj0[CG], gid1[CG], pj1[CG];
 #pragma unroll
         for (int s = 0; s < CG; s++) {
-            if (OBJ) {
-                L.cache[2 * s][es] = s < n0 ? L.g0id[s][es] : -1.0f;
-                L.cache[2 * s + 1][es] = s < n0 ? clam[s][0] * L.pjn[s][es] : 0.0f;
-            } else {
-                L.cache[2 * s][es] = -1.0f;
-                L.cache[2 * s + 1][es] = 0.0f;
-            }
-            L.cache[CACHE1 + 2 * s][es] = s < n1 ? L.g1id[s][es] : -1.0f;
-            L.cache[CACHE1 + 2 * s + 1][es] = s < n1 ? clam[P0 + s][0] * L.pjn[P0 + s][es] : 0.0f;
+            gid0[s] = OBJ ? L.g0id[s][es] : -1.0f;
+            pj0[s] = OBJ ? L.pjn[s][es] : 0.0f;
+            gid1[s] = L.g1id[s][es];
+            pj1[s] = L.pjn[P0 + s][es];
+        }
+#pragma unroll
+        for (int s = 0; s < CG; s++) {
+            L.cache[2 * s][es] = (OBJ && s < n0) ? gid0[s] : -1.0f;
+            L.cache[2 * s + 1][es] = (OBJ && s < n0) ? clam[s][0] * pj0[s] : 0.0f;
+            L.cache[CACHE1 + 2 * s][es] = s < n1 ? gid1[s] : -1.0f;
+            L.cache[CACHE1 + 2 * s + 1][es] = s < n1 ? clam[P0 + s][0] * pj1[s] : 0.0f;
         }
         if constexpr (RB > CG) {
             if (n1x > CG) {   /* the extra normal rows' impulses: lane x % 16 of xs_lam[x / 16] to LDS */
