@@ -746,6 +746,9 @@ struct ContactLdsT {
     /* wide layout, the register points' normal rows: jinv (the cache's impulse lambda' jinv)
      * and lambda' at the solve's start (a redo), kept here through the sweeps */
     float pjn[W == 64 ? 1 : 2 * CG][W], pl0[W == 64 ? 1 : 2 * CG][W];
+    /* wide layout, object tasks: the limit rows' rhs' and lambda' of the all-rows solve (in
+     * registers beside the 24 contact rows they set the kernel's register peak) */
+    float lrhs[W == 64 ? 1 : PGX_N_ROWS - PGX_NJ][W], llam[W == 64 ? 1 : PGX_N_ROWS - PGX_NJ][W];
     /* the register rows' Delassus entries against the extra rows: lane l of Delassus register b
      * reads W[16 b + l][extra row] jinv (its gw update for that row's impulse) */
     float wx[W == 64 ? 1 : W][XR > 1 ? 2 : 1][XR][16];
@@ -2196,6 +2199,14 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                                           ObjState& ob, ContactLdsGT<OBJ, FULL>* Lp, int es, int c, const LaneK& K,
                                           bool check = false) {
     MRef m = *fresh(mp);
+    /* The object tasks keep the limit rows of the all-rows solve (a failed speculation, limit
+     * pairs near two or more dofs) in LDS, and the two-waves-per-SIMD kernel (PART 2, 256
+     * registers, taken above 4096 envs) takes that solve instead of the partial one: in
+     * registers, those rows beside the 24 contact rows set the kernel's register peak (256 VGPR
+     * + 172 AGPR; squeezed into 256 they spilled inside every sweep, PickAndPlace 16384 6.5 ms).
+     * PickAndPlace 16384: 2.93 -> 2.59 ms (profiles/r03/ab_lds_limit_rows.log). */
+    constexpr bool LDS_LIM = OBJ;
+    constexpr bool NO_PART = OBJ && PART == 2;
     Dyn D;
     substep_dyn_g<OBJ, CONT, AO, FULL>(m, e, q, qd, ob, Lp, es, D, c, K, check);
     if constexpr (AO) {
@@ -2623,6 +2634,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             const int kind = kPgxRowCode[r] >> 4, d = kPgxRowCode[r] & 15;
             lam[r] = 0.0f;
             if (kind == 0) bnd[d] = (f2){-m.max_impulse[d] * den[d], m.max_impulse[d] * den[d]};
+            else if (LDS_LIM) __hip_atomic_store(&Lp->llam[r - NJ][es], 0.0f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         }
     };
     init_bounds();
@@ -2636,6 +2648,16 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         if constexpr (kind == 0) {
             delta = __builtin_amdgcn_fmed3f(x, bnd[d].x, bnd[d].y);
             bnd[d] -= (f2){delta, delta};
+        } else if constexpr (LDS_LIM) {
+            /* the object tasks' limit rows (the all-rows solve only) in LDS: relaxed atomics so
+             * they are neither hoisted out of the sweep loop nor promoted back to registers */
+            float* lr = &Lp->lrhs[r - NJ][es];
+            float* ll = &Lp->llam[r - NJ][es];
+            const float rr = __hip_atomic_load(lr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            const float lm = __hip_atomic_load(ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            const float xl = kind == 2 ? rr + bcast16<d>(gv) : rr - bcast16<d>(gv);
+            delta = __builtin_amdgcn_fmed3f(xl, -lm, lhi[d] - lm);
+            __hip_atomic_store(ll, lm + delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         } else {
             delta = __builtin_amdgcn_fmed3f(x, -lam[r], lhi[d] - lam[r]);
             lam[r] += delta;
@@ -2912,6 +2934,11 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     } else {
         PGX_PROF_COUNT(10, 1);
         init_limit_rows();
+        if constexpr (LDS_LIM) {   /* the limit rows' rhs' for an all-rows solve: in LDS */
+#pragma unroll
+            for (int r = NJ; r < PGX_N_ROWS; r++)
+                __hip_atomic_store(&Lp->lrhs[r - NJ][es], rhs[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
         if (e.pgs_mode != 2) {
             float rl[NJ], ru[NJ];
 #pragma unroll
@@ -2934,7 +2961,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
 #pragma unroll
                 for (int p = 0; p < NP; p++) Lp->pl0[p][es] = clam[p][0];
             }
-            if (PART && !spec_all && nk <= KMAX) {
+            if (PART && !NO_PART && !spec_all && nk <= KMAX) {   /* (NO_PART: all rows instead, fewer registers) */
                 PGX_PROF_COUNT(7, 1);
                 /* slots in the pairs' table order; slot lane SL0 + S mirrors dof d_S */
                 int ds[2] = {0, 0};
@@ -3794,7 +3821,7 @@ __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict_
 template <int CONTROL, int OBJ, int CONT, int AO, int WIDE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void step_kernel_o2(
     const PgxDevModel* __restrict__ mdev, PgxDevEnv e, PgxDevState s, const float* __restrict__ action, PgxDevOut o) {
-    step_body<CONTROL, OBJ, CONT, AO, WIDE, AO ? 0 : 1>(mdev, e, s, action, o);
+    step_body<CONTROL, OBJ, CONT, AO, WIDE, AO ? 0 : 2>(mdev, e, s, action, o);
 }
 
 template <int OBJ, int AO>
@@ -3949,9 +3976,9 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
     }
     switch (variant * 2 + wide) {
         case 6: PGX_STEP(0, 1, 1, 0, 0); break;
-        case 7: PGX_STEP(0, 1, 1, 0, 1); break;
+        case 7: PGX_STEP2(0, 1, 1, 0, 1); break;
         case 14: PGX_STEP(1, 1, 1, 0, 0); break;
-        case 15: PGX_STEP(1, 1, 1, 0, 1); break;
+        case 15: PGX_STEP2(1, 1, 1, 0, 1); break;
         case 26: PGX_STEP(1, 0, 1, 1, 0); break;
         case 27: PGX_STEP2(1, 0, 1, 1, 1); break;
         default: return (int)hipErrorInvalidValue;   /* object without contacts: rejected at create */

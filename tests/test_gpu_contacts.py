@@ -328,6 +328,30 @@ def test_partial_limit_rows_are_exact(pg, monkeypatch, env_id, contacts, n):
     assert np.array_equal(runs["0"], runs["2"])
 
 
+@pytest.mark.parametrize("env_id", ["PandaPush-v3", "PandaPickAndPlace-v3"])
+def test_object_kernel_two_waves_per_simd_exact(pg, monkeypatch, env_id):
+    """The object kernel's two-waves-per-SIMD build (256 registers, taken above 4096 envs; its
+    all-rows solve an out-of-line call, pgs_all_rows) equals the one-wave build bit for bit, in
+    the default solve and with every substep forced through the all-rows call (PGX_PGS_MODE=2)
+    or through a redo after the speculative solve (PGX_PGS_MODE=3)."""
+    runs = {}
+    for wm in ("1", "2"):
+        for mode in ("0", "2", "3"):
+            monkeypatch.setenv("PGX_WAVES_PER_SIMD", wm)
+            monkeypatch.setenv("PGX_PGS_MODE", mode)
+            v = pg.PandaVecEnv(env_id, num_envs=4096, device="cuda:0", seed=9, lanes_per_env=16)
+            v.reset_tensors()
+            outs = []
+            for t in range(16):
+                v.step_tensors(v.sample_actions(t))
+                outs.append(torch.cat([v.obs, v.state()["qd"].T], 1).cpu().numpy().copy())
+            runs[(wm, mode)] = np.stack(outs)
+            v.close()
+    ref = runs[("1", "0")]
+    for k, r in runs.items():
+        assert np.array_equal(ref, r), k
+
+
 @pytest.mark.parametrize("case", ["two_links_on_table", "link_on_cube"])
 def test_contact_budget_cases_keep_all_points(pg, oracle, case, lanes):
     """The oracle's manifold-rule cases (test_oracle_contacts.py) on the device: an arm with the
