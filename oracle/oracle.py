@@ -15,9 +15,11 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "libpgx_oracle.so")
 FLOPS_LIB_PATH = os.path.join(HERE, "_build", "libpgx_oracle_flops.so")   # operation-counting build
+FP32_LIB_PATH = os.path.join(HERE, "_build", "libpgx_oracle_fp32.so")     # the algorithm in fp32 arithmetic
 
 _lib = None
 _flops_lib = None
+_fp32_lib = None
 
 
 def build() -> str:
@@ -49,6 +51,20 @@ def flops_lib():
         for f in ("pgxo_vec_step", "pgxo_vec_reset", "pgxo_flops_nphase"):
             getattr(_flops_lib, f).restype = C.c_int
     return _flops_lib
+
+
+def fp32_lib():
+    """The same oracle evaluated in fp32 arithmetic (oracle/fp32_emul.cpp): every operation's
+    result rounded to float -- the restated algorithm's own rounding envelope at the device's
+    precision."""
+    global _fp32_lib
+    if _fp32_lib is None:
+        if not os.path.exists(FP32_LIB_PATH):
+            build()
+        _fp32_lib = C.CDLL(FP32_LIB_PATH)
+        for f in ("pgxo_vec_step", "pgxo_vec_reset"):
+            getattr(_fp32_lib, f).restype = C.c_int
+    return _fp32_lib
 
 
 class PgxoFlops(C.Structure):
@@ -253,9 +269,10 @@ def philox(ctr, key):
 class OracleVecEnv:
     """Host-side fp64 mirror of one libpgx handle (AoS state), same vec-env semantics."""
 
-    def __init__(self, cfg, n: int, counting: bool = False):
-        """``counting``: run on the operation-counting build (read_flops) instead."""
-        self._lib = flops_lib() if counting else lib()
+    def __init__(self, cfg, n: int, counting: bool = False, fp32: bool = False):
+        """``counting``: run on the operation-counting build (read_flops) instead; ``fp32``: on
+        the build that rounds every operation to float (fp32_lib)."""
+        self._lib = flops_lib() if counting else (fp32_lib() if fp32 else lib())
         self.cfg = cfg
         self.n = n
         self.nd = cfg.model.contents.n_dofs

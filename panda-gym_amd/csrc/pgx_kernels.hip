@@ -2706,14 +2706,28 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         });
         gw = r0 - gw;
         if (TWO) gw2 = r1 - gw2;
+        /* object tasks: an unusable normal row (inactive point, den <= SIMD_EPSILON: lambda' = 0)
+         * holds x = -3e38 in its lane, so med3(x, -0, +3e38) = 0 with the one upper bound of every
+         * normal row -- 8 bound registers fewer at the register peak (PickAndPlace 16384 -4 %,
+         * Reach +0.8 %: there the per-point bound stays); other rows' impulses move that x by
+         * finite amounts only */
+        if constexpr (OBJ) {
+            sfor<0, NQ / 3>([&](auto pc) __attribute__((always_inline)) {
+                constexpr int p = decltype(pc)::value, q = 3 * p;
+                const bool usable = act[p] && cjinv[p][0] != 0.0f;
+                if constexpr (q < GW) gw = usable ? gw : lane_sel<q>(-3.0e38f, gw);
+                else gw2 = usable ? gw2 : lane_sel<q - GW>(-3.0e38f, gw2);
+            });
+        }
 #pragma unroll
         for (int q = 0; q < NQ; q++) { Wc[q] = -Wc[q]; Wc2[q] = -Wc2[q]; }
 #pragma unroll
         for (int d = 0; d < NJ; d++) { wms[d] = -wms[d]; wms2[d] = -wms2[d]; }
     }
     /* shifted bounds as for the joint rows: delta' = clamp(rhs' - w, lo' - lambda', hi' - lambda').
-     * A normal row's upper bound is +inf (0 with lambda' = 0 for an unusable row, below); a
-     * friction row is idle (bounds 0) while its normal impulse is 0. */
+     * A normal row's upper bound is +inf (0 with lambda' = 0 for an unusable row; in the object
+     * tasks such a row is inert through its x, above); a friction row is idle (bounds 0) while
+     * its normal impulse is 0. */
     float chi[NPP];
     if constexpr (CONT) {   /* the normal rows' jinv for the cache: in LDS through the sweeps */
 #pragma unroll
@@ -2737,7 +2751,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             hi = b.y;
         } else {
             lo = -lm;
-            hi = chi[p];
+            hi = OBJ ? 3.0e38f : chi[p];
         }
         const float x = q < GW ? bcast16<q % GW>(gw) : bcast16<q % GW>(gw2);   /* rhs' - w */
         const float delta = __builtin_amdgcn_fmed3f(x, lo, hi);

@@ -1,0 +1,72 @@
+"""The device's deviation from the fp64 oracle against the restated algorithm's own fp32 envelope.
+
+The device computes in fp32, the oracle restates the reference (Bullet, fp64) in fp64.  How close
+should they be?  oracle/fp32_emul.cpp builds the same oracle with every operation rounded to
+float: the restated algorithm evaluated at the device's precision, in the oracle's own order.  Per
+step, from the device state copied into all three, this test records |device - fp64| and
+|fp32 oracle - fp64| on the same inputs and the same actions, and asserts the device is at
+least as close to fp64 as the fp32 evaluation of the algorithm is -- 99th and 99.9th percentiles
+of the positions (EE, object) and the 99th of the EE velocity.  The kernels' other bars
+(test_gpu_parity.py, test_gpu_contacts.py, test_gpu_reach_ao.py) sit inside this envelope; the
+figures are printed for DESIGN.md §6.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from test_gpu_parity import _state_to_oracle  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def pg():
+    import panda_gym_amd as pg
+
+    pg.load_native()
+    return pg
+
+
+def _copy_state(src, dst):
+    for k in ("q", "qd", "qc", "goal", "obj", "elapsed", "episode"):
+        getattr(dst, k)[:] = getattr(src, k)
+
+
+CASES = [("PandaReach-v3", True), ("PandaReach-v3", False), ("PandaPush-v3", True), ("PandaPickAndPlace-v3", True),
+         ("PandaReachAO-v3", True)]
+
+
+@pytest.mark.parametrize("env_id,contacts", CASES)
+def test_device_inside_fp32_envelope(pg, oracle, env_id, contacts):
+    n, steps = 128, 40
+    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=13, contacts=contacts)
+    venv.reset_tensors(seed=13)
+    r64 = oracle.OracleVecEnv(venv._cfg, n)
+    r32 = oracle.OracleVecEnv(venv._cfg, n, fp32=True)
+    obj = env_id in ("PandaPush-v3", "PandaPickAndPlace-v3")
+    dev_p, f32_p, dev_v, f32_v = [], [], [], []
+    for t in range(steps):
+        _state_to_oracle(venv, r64)   # (sets the fp64 build's contact budget; the fp32 build's default is the same)
+        _copy_state(r64, r32)
+        a = venv.sample_actions(t).clone()
+        venv.step_tensors(a)
+        an = a.cpu().numpy()
+        o64, o32 = r64.step(an), r32.step(an)
+        obs = venv.obs.cpu().numpy()
+        keep = (o64["truncated"] == 0) & (venv.truncated.cpu().numpy() == 0)   # a TimeLimit step resets the env
+        if not keep.any():
+            continue
+        cols = [0, 1, 2] + ([6, 7, 8] if obj else [])
+        dev_p.append(np.abs(obs[keep][:, cols] - o64["obs"][keep][:, cols]).ravel())
+        f32_p.append(np.abs(o32["obs"][keep][:, cols] - o64["obs"][keep][:, cols]).ravel())
+        dev_v.append(np.abs(obs[keep][:, 3:6] - o64["obs"][keep][:, 3:6]).ravel())
+        f32_v.append(np.abs(o32["obs"][keep][:, 3:6] - o64["obs"][keep][:, 3:6]).ravel())
+    venv.close()
+    dp, fp, dv, fv = (np.concatenate(x) for x in (dev_p, f32_p, dev_v, f32_v))
+    q = lambda x, p: float(np.percentile(x, p))  # noqa: E731
+    print(f"\n{env_id} contacts={contacts}: position device p99 {q(dp, 99):.2e} p99.9 {q(dp, 99.9):.2e} "
+          f"max {dp.max():.2e} | fp32 oracle p99 {q(fp, 99):.2e} p99.9 {q(fp, 99.9):.2e} max {fp.max():.2e}; "
+          f"EE velocity device p99 {q(dv, 99):.2e} max {dv.max():.2e} | fp32 oracle p99 {q(fv, 99):.2e} max {fv.max():.2e}")
+    assert q(dp, 99) <= q(fp, 99) and q(dp, 99.9) <= q(fp, 99.9)
+    assert q(dv, 99) <= q(fv, 99)
