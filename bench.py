@@ -241,7 +241,9 @@ def task_leg(dev, env_id: str, n: int, steps: int, contacts: bool = True, flops_
     alg = {"push": 351.0, "pick_and_place": 359.0}.get(flops_key)   # SURVEY §8d bytes per env-step
     if alg:
         prof = pmc("pmc_object_kernel_" + ("push" if flops_key == "push" else "pnp"), n)
-        res["roofline"] = hbm_roofline(alg * n, ms, prof, "step_kernel<0, 1, 1, 0, 1> (object kernel, 16 lanes per env)")
+        kname = ("step_kernel_o2<0, 1, 1, 0, 1> (object kernel, 16 lanes per env, two waves per SIMD)" if n > 4096
+                 else "step_kernel<0, 1, 1, 0, 1> (object kernel, 16 lanes per env)")
+        res["roofline"] = hbm_roofline(alg * n, ms, prof, kname)
     return res
 
 

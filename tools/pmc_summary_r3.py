@@ -36,7 +36,7 @@ def her_alg():
 KERNELS = [
     ("pmc_step_kernel", "step_kernel<0, 0, 1, 0, 1>", 4096 * 16, 4096, 199.0 * 4096),
     ("pmc_object_kernel_push", "step_kernel<0, 1, 1, 0, 1>", 4096 * 16, 4096, 351.0 * 4096),
-    ("pmc_object_kernel_pnp", "step_kernel<0, 1, 1, 0, 1>", 16384 * 16, 16384, 359.0 * 16384),
+    ("pmc_object_kernel_pnp", "step_kernel_o2<0, 1, 1, 0, 1>", 16384 * 16, 16384, 359.0 * 16384),
     ("pmc_reach_ao_kernel", "step_kernel_o2<1, 0, 1, 1, 1>", 8192 * 16, 8192, 650.0 * 8192),
     ("pmc_sample_kernel", "sample_kernel", None, None, None),
 ]
