@@ -749,6 +749,10 @@ struct ContactLdsT {
     /* wide layout, object tasks: the limit rows' rhs' and lambda' of the all-rows solve (in
      * registers beside the 24 contact rows they set the kernel's register peak) */
     float lrhs[W == 64 ? 1 : PGX_N_ROWS - PGX_NJ][W], llam[W == 64 ? 1 : PGX_N_ROWS - PGX_NJ][W];
+    /* wide layout: state that lives across the substep loop but is read once per substep or after
+     * it, parked here instead of in registers (the motor targets; the substeps' start poses,
+     * double-buffered: getLinkState's cached pose is the last completed substep's start) */
+    float ltq[W == 64 ? 1 : PGX_NJ][W], lqs[W == 64 ? 1 : 2][W == 64 ? 1 : PGX_NJ][W];
     /* the register rows' Delassus entries against the extra rows: lane l of Delassus register b
      * reads W[16 b + l][extra row] jinv (its gw update for that row's impulse) */
     float wx[W == 64 ? 1 : W][XR > 1 ? 2 : 1][XR][16];
@@ -3641,9 +3645,6 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
         q[j] = s.q[j * N + ii];
         qd[j] = s.qd[j * N + ii];
     }
-    double goal[3];
-#pragma unroll
-    for (int c = 0; c < 3; c++) goal[c] = s.goal[c * N + ii];
     ObjState ob;
     if (OBJ) load_obj(s, N, ii, ob);
     if (CONT) {
@@ -3683,10 +3684,30 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     const int n_substeps = e.n_substeps;
     bool collided = false;
     float qprev[NJ];   /* the pose the last substep starts from: getLinkState's cached pose */
+    /* PARK (wide layout with contacts, an LDS buffer): the motor targets and the substeps' start
+     * poses wait in LDS (relaxed atomics: not promoted back into registers) -- ~14 registers
+     * fewer across the substep loop, which the two-waves-per-SIMD kernels otherwise spill to
+     * scratch and reload from memory in every substep */
+    constexpr bool PARK = WIDE && CONT;
+    auto lds_st = [&](float* a, float v) __attribute__((always_inline)) { __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT); };
+    auto lds_ld = [&](float* a) __attribute__((always_inline)) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT); };
+    if constexpr (PARK) {
+#pragma unroll
+        for (int j = 0; j < NJ; j++) lds_st(&L->ltq[j][ln], tq[j]);
+    }
+    int qslot = 0;   /* PARK: the buffer holding the last completed substep's start pose */
     for (int st = 0; st < n_substeps; st++) {
         float qstart[NJ];
+        if constexpr (PARK) {
 #pragma unroll
-        for (int j = 0; j < NJ; j++) qstart[j] = q[j];
+            for (int j = 0; j < NJ; j++) {
+                lds_st(&L->lqs[st & 1][j][ln], q[j]);
+                tq[j] = lds_ld(&L->ltq[j][ln]);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < NJ; j++) qstart[j] = q[j];
+        }
         if constexpr (WIDE) {
             /* ReachAO step_check_collision (reach_ao.py:182-188): the check after substep st - 1
              * runs inside substep st's contact detection (the same pose); a hit stops the loop
@@ -3698,8 +3719,11 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
         } else {
             substep<OBJ, CONT, AO>(mp, e, q, qd, tq, ob, L, ln);
         }
+        if constexpr (PARK) qslot = st & 1;
+        else {
 #pragma unroll
-        for (int j = 0; j < NJ; j++) qprev[j] = qstart[j];
+            for (int j = 0; j < NJ; j++) qprev[j] = qstart[j];
+        }
         if constexpr (AO && !WIDE) {   /* ReachAO step_check_collision: check after every substep */
             ao_caps(*fresh(mp), q, *L, ln);
             if (ao_collided(e, *L, ln)) { collided = true; break; }
@@ -3712,6 +3736,13 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
         }
     }
 
+    if constexpr (PARK) {
+#pragma unroll
+        for (int j = 0; j < NJ; j++) qprev[j] = lds_ld(&L->lqs[qslot][j][ln]);
+    }
+    double goal[3];   /* read after the substep loop: not live across it */
+#pragma unroll
+    for (int c = 0; c < 3; c++) goal[c] = s.goal[c * N + ii];
     V3 pos, vel;
     ee_state_cached(*fresh(mp), qprev, q, qd, pos, vel);
     const int od = e.obs_dim;
