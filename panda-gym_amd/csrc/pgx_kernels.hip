@@ -753,6 +753,7 @@ struct ContactLdsT {
      * it, parked here instead of in registers (the motor targets; the substeps' start poses,
      * double-buffered: getLinkState's cached pose is the last completed substep's start) */
     float ltq[W == 64 ? 1 : PGX_NJ][W], lqs[W == 64 ? 1 : 2][W == 64 ? 1 : PGX_NJ][W];
+    float lkc[W == 64 ? 1 : 16][W == 64 ? 1 : 16];   /* the lane constants (LaneK fields x lane c) */
     /* the register rows' Delassus entries against the extra rows: lane l of Delassus register b
      * reads W[16 b + l][extra row] jinv (its gw update for that row's impulse) */
     float wx[W == 64 ? 1 : W][XR > 1 ? 2 : 1][XR][16];
@@ -3691,9 +3692,13 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     constexpr bool PARK = WIDE && CONT;
     auto lds_st = [&](float* a, float v) __attribute__((always_inline)) { __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT); };
     auto lds_ld = [&](float* a) __attribute__((always_inline)) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT); };
+    float* lkf = &lk.mass;   /* LaneK: 16 floats */
+    static_assert(sizeof(LaneK) == 16 * sizeof(float), "LaneK layout");
     if constexpr (PARK) {
 #pragma unroll
         for (int j = 0; j < NJ; j++) lds_st(&L->ltq[j][ln], tq[j]);
+#pragma unroll
+        for (int f = 0; f < 16; f++) lds_st(&L->lkc[f][c], lkf[f]);   /* (every env's lane c writes the same) */
     }
     int qslot = 0;   /* PARK: the buffer holding the last completed substep's start pose */
     for (int st = 0; st < n_substeps; st++) {
@@ -3704,6 +3709,8 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
                 lds_st(&L->lqs[st & 1][j][ln], q[j]);
                 tq[j] = lds_ld(&L->ltq[j][ln]);
             }
+#pragma unroll
+            for (int f = 0; f < 16; f++) lkf[f] = lds_ld(&L->lkc[f][c]);
         } else {
 #pragma unroll
             for (int j = 0; j < NJ; j++) qstart[j] = q[j];
