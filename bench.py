@@ -27,7 +27,25 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
 VALU_PEAK_TFLOPS = 157.3         # FP32 vector peak (spec)
-ALG_BYTES_PER_ENV_STEP = 199.0   # read 84 + write 115 B per Reach env-step
+EPISODE_STEPS = 50               # the TimeLimit: terminal outputs and reset writes amortised over an episode
+
+
+def alg_bytes_per_env_step(task: str, obs_dim: int, action_dim: int, robot_points: int) -> dict:
+    """HBM bytes one env-step must move: the state it carries -- q, qd and the
+    cached link pose qc (f32 x 7 each), the fp64 goal, the contact warm-start cache (feature id,
+    impulse) of the robot budget's slots and, with an object, the cube's 13 floats and its 4
+    object-scene slots; ReachAO's 6 obstacle centres; the TimeLimit and episode counters --
+    read and written back (the goal and obstacles only on a reset), the action read, and the
+    outputs written: obs, achieved / desired goal, reward, success / terminated / truncated
+    (+ ReachAO's task flag), the terminal obs / goals on an episode's last step."""
+    obj = task in ("push", "pick_and_place")
+    ao = task == "reach_ao"
+    state = 3 * 7 * 4 + 8 + 2 * 4 * (robot_points + (4 if obj else 0)) + (13 * 4 if obj else 0)
+    read = state + 24 + (72 if ao else 0) + 4 * action_dim
+    out = 4 * obs_dim + 12 + 12 + 4 + 3 + (1 if ao else 0)
+    reset = (4 * obs_dim + 24 + 24 + (72 if ao else 0)) / EPISODE_STEPS
+    write = state + out + reset
+    return {"read": read, "write": write, "total": read + write}
 PROFILE_JSON = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
 # algorithmic FLOPs per env-step, op-counted in the oracle and frozen (oracle/count_flops.py)
 FLOPS_JSON = os.path.join(ROOT, "tests", "golden", "flops_per_env_step.json")
@@ -61,11 +79,16 @@ def hbm_roofline(alg_bytes: float, ms: float, prof, kernel: str) -> dict:
 
 
 def valu_roofline(key: str, env_steps_per_s: float, what: str) -> dict:
-    """rate x algorithmic FLOPs per env-step / the FP32 vector peak."""
+    """rate x algorithmic FLOPs per env-step / the FP32 vector peak.  The count is
+    the minimal (recursive: CRBA + Newton-Euler + Cholesky) formulation's; the oracle's Jacobian
+    form of the same dynamics is reported beside it, labelled, and not used for the fraction."""
     fl = alg_flops()[key]
+    with open(FLOPS_JSON) as f:
+        jac = json.load(f)["configs"][key].get("jacobian", {}).get("flops_per_env_step")
     ach = env_steps_per_s * fl / 1e12
     return {"bound": "valu", "achieved": ach, "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / VALU_PEAK_TFLOPS,
-            "alg_flops_per_env_step": fl, "rate": what,
+            "alg_flops_per_env_step": fl, "formulation": "recursive (CRBA + Newton-Euler + Cholesky)",
+            "jacobian_form_flops_per_env_step": jac, "rate": what,
             "source": os.path.relpath(FLOPS_JSON, ROOT) + f" [{key}] (fp64 oracle op-count, oracle/count_flops.py)"}
 
 
@@ -220,6 +243,7 @@ def task_leg(dev, env_id: str, n: int, steps: int, contacts: bool = True, flops_
     import panda_gym_amd as pg
 
     venv = pg.PandaVecEnv(env_id, num_envs=n, device=dev, seed=1, contacts=contacts)
+    obs_dim, act_dim, budget = venv.obs_dim, venv.action_dim, venv.robot_contact_budget()
     venv.reset_tensors()
     for t in range(20):
         venv.step_tensors(venv.sample_actions(t))
@@ -233,12 +257,15 @@ def task_leg(dev, env_id: str, n: int, steps: int, contacts: bool = True, flops_
     torch.cuda.synchronize(dev)
     ms = e0.elapsed_time(e1) / steps
     venv.close()
-    res = {"env_id": env_id, "envs": n, "contacts": contacts, "value": n / (ms * 1e-3), "unit": "env-steps/s",
+    res = {"env_id": env_id, "envs": n, "contacts": contacts, "robot_points": budget, "value": n / (ms * 1e-3),
+           "unit": "env-steps/s",
            "ms_per_step": ms, "steps": steps,
            "policy": "device Philox random actions (sample_actions + step per step)"}
     if flops_key:
         res["roofline_valu"] = valu_roofline(flops_key, res["value"], "env-steps/s of this leg (sample + step)")
-    alg = {"push": 351.0, "pick_and_place": 359.0}.get(flops_key)   # SURVEY §8d bytes per env-step
+    alg = None
+    if flops_key in ("push", "pick_and_place"):
+        alg = alg_bytes_per_env_step(flops_key, obs_dim, act_dim, budget)["total"]
     if alg:
         prof = pmc("pmc_object_kernel_" + ("push" if flops_key == "push" else "pnp"), n)
         kname = ("step_kernel_o2<0, 1, 1, 0, 1> (object kernel, 16 lanes per env, two waves per SIMD)" if n > 4096
@@ -294,6 +321,7 @@ def sharded_leg(dev, env_id: str, n: int, steps: int, warmup: int, dist, rank: i
     from panda_gym_amd.shard import max_over_ranks, shard_offset
 
     venv = pg.PandaVecEnv(env_id, num_envs=n, device=dev, seed=1, env_id_offset=shard_offset(rank, n))
+    ab = alg_bytes_per_env_step("reach_ao", venv.obs_dim, venv.action_dim, venv.robot_contact_budget())["total"]
     venv.reset_tensors()
 
     def barrier():
@@ -319,8 +347,8 @@ def sharded_leg(dev, env_id: str, n: int, steps: int, warmup: int, dist, rank: i
             "policy": "device Philox random actions, in-kernel collision / success / TimeLimit auto-reset",
             "obs_digest": digest,
             "roofline_valu": valu_roofline("reach_ao", value / world, "env-steps/s per GPU of this leg"),
-            # ~650 B per env-step (state, obstacles, contact cache, 56-float obs)
-            "roofline": hbm_roofline(650.0 * n, elapsed / steps * 1e3, pmc("pmc_reach_ao_kernel", n),
+            # state, obstacles, contact cache, 56-float obs
+            "roofline": hbm_roofline(ab * n, elapsed / steps * 1e3, pmc("pmc_reach_ao_kernel", n),
                                      "step_kernel_o2<1, 0, 1, 1, 1> (ReachAO, 16 lanes per env)")}
 
 
@@ -376,7 +404,10 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    for _ in range(args.warmup):
+    # steady state: one whole episode (the TimeLimit, 50 steps) before the warmup steps, so the timed
+    # window sits past the first auto-resets wherever --steps / --warmup put it (the first episode's
+    # early steps are cheaper: the arm starts at rest, no env resets)
+    for _ in range(venv.spec.max_episode_steps + args.warmup):
         venv.step_tensors(venv.sample_actions())
     barrier()
     t0 = time.perf_counter()
@@ -412,13 +443,15 @@ def main():
                                             world, coll_dev)
 
     if rank == 0:
-        alg_bytes = ALG_BYTES_PER_ENV_STEP * E
+
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
         traffic = None
         # the binding roofline: algorithmic FLOPs (op-counted in the oracle, frozen) over the
         # kernel's own launch time (HIP events on the launch stream)
         fkey = {"PandaReach-v3": "reach_table", "PandaPush-v3": "push", "PandaPickAndPlace-v3": "pick_and_place",
                 "PandaReachAO-v3": "reach_ao"}.get(args.env_id)
+        alg_bytes = alg_bytes_per_env_step(fkey or "reach_table", venv.obs_dim, venv.action_dim,
+                                           venv.robot_contact_budget())["total"] * E
         valu = None
         if fkey:
             valu = valu_roofline(fkey, E / (kernel_ms * 1e-3), "env-steps/s of the step kernel alone (kernel_ms)")
@@ -442,6 +475,9 @@ def main():
             "metric": "aggregate env-steps/s, PandaReach 4096 envs @1 GPU; 1/2/4/8-GPU scaling",
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            # the step kernel alone (HIP events over --kernel-launches launches on the launch stream)
+            "kernel_ms": kernel_ms, "steady_state": f"timed after {venv.spec.max_episode_steps} + {args.warmup} "
+                                                    f"untimed steps (one whole episode: auto-resets in the window)",
             "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: device Philox random policy U[-1,1)^3, 50-step episodes with in-kernel auto-reset",
             "config": {"workload": f"{args.env_id} (ee control, sparse reward), {E} envs per GPU, the "

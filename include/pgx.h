@@ -27,10 +27,13 @@
  *   pgx_compute_reward  Task.compute_reward bound as env.compute_reward
  *                       (core.py:282; reach.py:84-89, push.py:93-98,
  *                       pick_and_place.py:91-96) over a batch (HER relabel)
- *   pgx_get_state /     PyBullet.get_joint_angles / get_joint_velocities /
- *   pgx_set_state       set_joint_angles pybullet.py:313-348,416-435 and
- *                       RobotTaskEnv.save_state/restore_state core.py:310-336
- *                       (device snapshots are plain buffer copies)
+ *   pgx_get_state       PyBullet.get_joint_angles / get_joint_velocities
+ *                       pybullet.py:313-348 (device views of the SoA state)
+ *   pgx_snapshot /      RobotTaskEnv.save_state / restore_state / remove_state
+ *   pgx_restore /       core.py:310-336 -> PyBullet.save_state / restore_state /
+ *   pgx_release         remove_state pybullet.py:79-102 (state ids)
+ *   pgx_save_state /    the same snapshot into / out of a caller-owned device
+ *   pgx_restore_state   buffer (no id)
  *
  * Error convention: every call returns PGX_OK (0) or a negative PGX_E_* code;
  * pgx_last_error() returns a thread-local message for the last failure.
@@ -152,8 +155,16 @@ typedef struct pgx_sim_params {
     int32_t flags;                /* PGX_FLAG_* hypotheses (oracle only) */
     double contact_distance;      /* contact processing threshold 0.02 (gContactBreakingThreshold) */
     double contact_erp;           /* ERP of multibody contact rows (m_erp 0.2) */
-    double friction;              /* combined lateral friction 0.5 * 0.5 (btManifoldResult) */
+    double friction;              /* combined lateral friction of the cube against the table / plane:
+                                     0.5 * 0.5 (each body's pybullet default; btManifoldResult
+                                     multiplies the two) */
     double warmstart;             /* m_warmstartingFactor 0.85 (normal impulses) */
+    /* combined lateral friction of robot link i (Bullet link index) against the scene's bodies --
+     * table, plane, cube, obstacles, each at the default 0.5: 0.5 x the link's own, 0.5 x 0.5
+     * except panda_ee and panda_leftfinger (links 9, 10), which Panda.__init__ raises to 1.0
+     * (panda.py:69-70: set_lateral_friction(fingers_indices), pybullet.py:880-892 changeDynamics).
+     * Their spinning friction 0.001 (panda.py:71-72) combines with the others' 0 to 0: no row. */
+    double link_friction[PGX_MAX_LINKS];
 } pgx_sim_params;
 
 /* oracle-only modelling switches (documented in DESIGN.md) */
@@ -162,6 +173,9 @@ typedef struct pgx_sim_params {
 #define PGX_FLAG_NO_RESIDUAL_EXIT 4       /* run all solver iterations */
 #define PGX_FLAG_LINKSTATE_CURRENT 8      /* getLinkState reports the pose after the last substep
                                              instead of Bullet's cached pose (rejected hypothesis) */
+#define PGX_FLAG_DYN_RECURSIVE 16         /* M and b by composite rigid bodies + Newton-Euler (the
+                                             kernel's formulation; same dynamics) instead of the
+                                             Jacobian form: for the operation count */
 
 typedef struct pgx_config {
     int32_t task;                 /* PGX_TASK_* */
@@ -293,10 +307,22 @@ int pgx_sample_actions(pgx_handle h, float* action, uint64_t step, void* stream)
 int pgx_compute_reward(const float* achieved_goal, const float* desired_goal, int64_t batch,
                        int32_t reward_type, double distance_threshold, float* out, void* stream);
 
-/* Single-kernel copies of the whole SoA state (snapshot = save_state). */
+/* Single-kernel copies of the whole SoA state into / out of a caller-owned device buffer. */
 int pgx_state_bytes(pgx_handle h, int64_t* nbytes);
 int pgx_save_state(pgx_handle h, void* dst_device, void* stream);
 int pgx_restore_state(pgx_handle h, const void* src_device, void* stream);
+
+/* State ids (PyBullet.save_state / restore_state / remove_state, pybullet.py:79-102; reached
+ * through RobotTaskEnv.save_state / restore_state / remove_state, core.py:310-336).
+ * pgx_snapshot copies the whole state into a buffer the handle owns and returns its id: the
+ * first non-negative integer not in use (pybullet's saveState rule, so a released id is handed
+ * out again).  pgx_restore copies it back; pgx_release frees it (it synchronises the device:
+ * queued copies may still read the buffer).  Restoring or releasing an id that is not in use
+ * returns PGX_E_INVALID ("no such saved state"), as restoreState after removeState raises
+ * pybullet.error (test/save_and_restore_test.py:30-36).  pgx_destroy frees every snapshot. */
+int pgx_snapshot(pgx_handle h, int32_t* state_id, void* stream);
+int pgx_restore(pgx_handle h, int32_t state_id, void* stream);
+int pgx_release(pgx_handle h, int32_t state_id);
 
 /* ------------------------------------------------------------------------
  * Device HER replay ring: the goal-relabelling replay buffer the reference's

@@ -35,24 +35,32 @@ CONFIGS = [
 FLOP_KEYS = ("add", "mul", "div", "sqrt", "trans")
 
 
-def make_cfg(env_id: str, n: int, contacts: bool, seed: int):
+def make_cfg(env_id: str, n: int, contacts: bool, seed: int, flags: int = 0):
+    """The bench's configuration of ``env_id`` (with contacts: Bullet's per-pair manifold budget, the
+    default handle's); ``flags``: oracle modelling switches (PGX_FLAG_DYN_RECURSIVE)."""
     sys.path.insert(0, ROOT)
     from panda_gym_amd import abi, envs
     from panda_gym_amd.model import load_model
 
     model = abi.make_model(load_model("panda_custom0"), ee_link=11)
-    params = abi.default_sim_params()
-    cfg = abi.make_config(envs.spec(env_id), n, model, params, seed=seed, contacts=contacts)
+    params = abi.default_sim_params(flags=flags)
+    cfg = abi.make_config(envs.spec(env_id), n, model, params, seed=seed, contacts=contacts, full_manifold=contacts)
     return cfg, (model, params)
 
 
-def count(env_id: str, contacts: bool, seed: int, n: int, steps: int) -> dict:
+# the two formulations of the dynamics phase counted: "recursive" (composite rigid bodies +
+# Newton-Euler + Cholesky, SURVEY.md section 8d's minimal form, the one the kernel computes: the
+# roofline numerator) and "jacobian" (the oracle's default Jacobian-form M and b, kept labelled)
+FORMS = {"recursive": 16, "jacobian": 0}   # PGX_FLAG_DYN_RECURSIVE
+
+
+def count(env_id: str, contacts: bool, seed: int, n: int, steps: int, flags: int = 0) -> dict:
     """Per-phase operation counts summed over ``steps`` random-policy steps of ``n`` envs
     (the initial reset excluded), plus the number of auto-resets seen."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
 
-    cfg, keep = make_cfg(env_id, n, contacts, seed)
+    cfg, keep = make_cfg(env_id, n, contacts, seed, flags)
     env = O.OracleVecEnv(cfg, n, counting=True)
     env.reset()
     O.read_flops(clear=True)
@@ -84,23 +92,32 @@ def main():
     from oracle import oracle as O
 
     O.build()
-    with ProcessPoolExecutor(len(CONFIGS)) as ex:
-        futs = {key: ex.submit(count, eid, cont, seed, args.envs, args.steps) for key, eid, cont, seed in CONFIGS}
-        res = {key: f.result() for key, f in futs.items()}
+    with ProcessPoolExecutor(min(len(CONFIGS) * len(FORMS), os.cpu_count() or 1)) as ex:
+        futs = {(key, form): ex.submit(count, eid, cont, seed, args.envs, args.steps, fl)
+                for key, eid, cont, seed in CONFIGS for form, fl in FORMS.items()}
+        res = {k: f.result() for k, f in futs.items()}
     doc = {
         "about": "Algorithmic fp64 FLOPs per env-step, op-counted in the oracle's restatement "
                  "(oracle/count_flops.py, oracle/flops_count.cpp): add/sub, mul, div, sqrt and "
                  "transcendentals count 1 each, comparisons (cmp) are listed apart and not counted. "
-                 "Workload: device-Philox random actions from a fresh reset, auto-resets included.",
+                 "Workload: device-Philox random actions from a fresh reset, auto-resets included; "
+                 "the contact configs at Bullet's per-pair manifold budget (the default handle's). "
+                 "flops_per_env_step is the 'recursive' form: the dynamics by composite rigid bodies + "
+                 "Newton-Euler + Cholesky (SURVEY.md 8d, the kernel's formulation); 'jacobian' is the "
+                 "oracle's default Jacobian-form M and b (the same dynamics, more arithmetic), kept "
+                 "for reference only.",
         "sample": {"envs": args.envs, "steps": args.steps},
-        "configs": {key: {"env_id": eid, "contacts": cont, "seed": seed, **summarise(res[key])}
+        "configs": {key: {"env_id": eid, "contacts": cont, "seed": seed,
+                          "flops_per_env_step": summarise(res[key, "recursive"])["flops_per_env_step"],
+                          **{form: summarise(res[key, form]) for form in FORMS}}
                     for key, eid, cont, seed in CONFIGS},
     }
     with open(args.out, "w") as f:
         json.dump(doc, f, indent=1, sort_keys=False)
         f.write("\n")
     for key, v in doc["configs"].items():
-        print(f"{key:16s} {v['flops_per_env_step'] / 1e3:9.1f} kFLOP/env-step  resets {v['auto_resets']}")
+        print(f"{key:16s} {v['recursive']['flops_per_env_step'] / 1e3:9.1f} kFLOP/env-step recursive, "
+              f"{v['jacobian']['flops_per_env_step'] / 1e3:9.1f} jacobian form  resets {v['recursive']['auto_resets']}")
 
 
 if __name__ == "__main__":

@@ -183,6 +183,15 @@ def bias(model, params, q, qd, with_gravity=True, base=(0.0, 0.0, 0.0)):
     return b
 
 
+def dyn_recursive(model, params, q, qd, with_gravity=True, base=(0.0, 0.0, 0.0)):
+    """(M, b) by composite rigid bodies + Newton-Euler (pgxo_dyn_recursive): the kernel's formulation."""
+    nd = model.n_dofs
+    M, b = np.zeros((nd, nd)), np.zeros(nd)
+    lib().pgxo_dyn_recursive(C.byref(model), C.byref(params), _base(base), _p(_d(q)), _p(_d(qd)), int(with_gravity),
+                             _p(M), _p(b))
+    return M, b
+
+
 def ik(model, params, q_start, link, target_pos, target_orn, base=(0.0, 0.0, 0.0)):
     out = np.zeros(model.n_dofs)
     st = PgxoStats()
@@ -311,16 +320,24 @@ class OracleVecEnv:
         assert rc == 0, rc
         return b
 
-    def step(self, action: np.ndarray):
+    def step(self, action: np.ndarray, margins: bool = False):
+        """One vec step.  ``margins`` (ReachAO): also return, per env, the smallest |margin| of
+        check_collided over the substep checks that ran ("margin_abs") and the margin at the last
+        one ("margin_last"); collided <=> margin <= 0 (pgxo_diag_collision_margin)."""
         a = np.ascontiguousarray(action, dtype=np.float32)
         b = self._bufs()
         n = self.n
         b.update(reward=np.zeros(n, np.float32), success=np.zeros(n, np.uint8), terminated=np.zeros(n, np.uint8),
                  truncated=np.zeros(n, np.uint8), terminal_obs=np.zeros((n, self.od), np.float32))
+        if margins:
+            b.update(margin_abs=np.full(n, np.inf), margin_last=np.full(n, np.inf))
+            self._lib.pgxo_diag_collision_margin(_p(b["margin_abs"]), _p(b["margin_last"]), C.c_int64(n))
         rc = self._lib.pgxo_vec_step(C.byref(self.cfg), C.c_int64(n), _p(self.q), _p(self.qd), _p(self.goal),
                                  _p(self.obj), _p(self.elapsed), _p(self.episode), _p(a), _p(b["obs"]), _p(b["ag"]),
                                  _p(b["dg"]), _p(b["reward"]), _p(b["success"]), _p(b["terminated"]),
                                  _p(b["truncated"]), _p(b["terminal_obs"]))
+        if margins:
+            self._lib.pgxo_diag_collision_margin(None, None, C.c_int64(0))
         assert rc == 0, rc
         return b
 

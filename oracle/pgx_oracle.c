@@ -289,6 +289,157 @@ void pgxo_bias(const pgx_model* m, const pgx_sim_params* p, const double base[3]
     bias(m, p, &k, qd, with_gravity, 1, b);
 }
 
+/* The same M and b in the recursive form the HIP kernel computes them in (composite rigid
+ * bodies for M, Newton-Euler for b; SURVEY.md section 8d's "CRBA + RNEA + 7x7 Cholesky"), for the
+ * operation count of that formulation (oracle flag PGX_FLAG_DYN_RECURSIVE, oracle/count_flops.py
+ * key "recursive"); equal to mass_matrix / bias to rounding (tests/test_flops.py).  Links are in
+ * Bullet order, parents first.
+ *   b: forward pass as bias() (velocities / accelerations at the COM with qdd = 0), per link
+ *      the wrench at its COM (F, T), then one backward pass accumulating the subtree's force Fs
+ *      and moment Ns about the link's pivot: b_d = z . Ns of the dof's link.
+ *   M: backward pass of the subtree's mass Mc, first moment H = sum m p and inertia about the
+ *      world origin Io; spun about z_j through o_j the composite has momentum f = z_j x (H - Mc o_j)
+ *      and angular momentum about o_j n = Io z_j - o_j x (H x z_j) ... written as below; then
+ *      M[i][j] = z_i . (n + (o_j - o_i) x f) for every dof i on the path to the root. */
+static void dyn_recursive(const pgx_model* m, const pgx_sim_params* p, const kin_t* k, const double* qd,
+                          int with_gravity, double* M, double* b) {
+    const int nl = m->n_links, nd = m->n_dofs;
+    double w[L][3], al[L][3], v[L][3], acc[L][3];
+    for (int i = 0; i < nl; i++) {   /* forward: as bias() */
+        int par = m->parent[i];
+        double wp[3] = {0, 0, 0}, alp[3] = {0, 0, 0}, vp[3] = {0, 0, 0}, ap[3] = {0, 0, 0}, pp[3];
+        if (par >= 0) {
+            memcpy(wp, w[par], sizeof wp); memcpy(alp, al[par], sizeof alp);
+            memcpy(vp, v[par], sizeof vp); memcpy(ap, acc[par], sizeof ap);
+            memcpy(pp, k->p[par], sizeof pp);
+        } else {
+            memcpy(pp, k->o[i], sizeof pp);
+        }
+        double r[3] = {k->o[i][0] - pp[0], k->o[i][1] - pp[1], k->o[i][2] - pp[2]};
+        double vo[3], ao[3], t1[3], t2[3];
+        v3_cross(wp, r, t1);
+        for (int c = 0; c < 3; c++) vo[c] = vp[c] + t1[c];
+        v3_cross(alp, r, t1);
+        v3_cross(wp, r, t2);
+        v3_cross(wp, t2, t2);
+        for (int c = 0; c < 3; c++) ao[c] = ap[c] + t1[c] + t2[c];
+        int d = m->dof_of_link[i];
+        double qdi = d >= 0 ? qd[d] : 0.0;
+        double sz[3] = {k->z[i][0] * qdi, k->z[i][1] * qdi, k->z[i][2] * qdi};
+        memcpy(w[i], wp, sizeof wp);
+        memcpy(al[i], alp, sizeof alp);
+        if (d >= 0 && m->jtype[i] == PGX_JOINT_REVOLUTE) {
+            for (int c = 0; c < 3; c++) w[i][c] += sz[c];
+            v3_cross(wp, sz, t1);
+            for (int c = 0; c < 3; c++) al[i][c] += t1[c];
+        } else if (d >= 0 && m->jtype[i] == PGX_JOINT_PRISMATIC) {
+            v3_cross(wp, sz, t1);
+            for (int c = 0; c < 3; c++) { vo[c] += sz[c]; ao[c] += 2.0 * t1[c]; }
+        }
+        double rc[3] = {k->p[i][0] - k->o[i][0], k->p[i][1] - k->o[i][1], k->p[i][2] - k->o[i][2]};
+        v3_cross(w[i], rc, t1);
+        for (int c = 0; c < 3; c++) v[i][c] = vo[c] + t1[c];
+        v3_cross(al[i], rc, t1);
+        v3_cross(w[i], rc, t2);
+        v3_cross(w[i], t2, t2);
+        for (int c = 0; c < 3; c++) acc[i][c] = ao[c] + t1[c] + t2[c];
+    }
+    /* backward: subtree force Fs and moment Ns about the pivot o_i; composite Mc, H, Io */
+    double Fs[L][3], Ns[L][3], Mc[L], H[L][3], Io[L][9];
+    for (int i = 0; i < nl; i++) {
+        Mc[i] = 0.0;
+        for (int c = 0; c < 3; c++) { Fs[i][c] = 0.0; Ns[i][c] = 0.0; H[i][c] = 0.0; }
+        for (int c = 0; c < 9; c++) Io[i][c] = 0.0;
+    }
+    for (int i = nl - 1; i >= 0; i--) {
+        const double mi = m->mass[i];
+        if (mi != 0.0) {
+            double F[3], T[3], Iw[9], Iww[3], Ial[3], t1[3], rc[3];
+            double vn = v3_norm(v[i]), wn = v3_norm(w[i]);
+            for (int c = 0; c < 3; c++) {
+                F[c] = mi * acc[i][c];
+                if (with_gravity) F[c] -= mi * p->gravity[c];
+                F[c] += mi * v[i][c] * (p->lin_damping + p->lin_damping * vn);
+            }
+            world_inertia(k->R[i], m->inertia[i], Iw);
+            m3_v(Iw, w[i], Iww);
+            m3_v(Iw, al[i], Ial);
+            v3_cross(w[i], Iww, t1);
+            for (int c = 0; c < 3; c++) T[c] = Ial[c] + t1[c] + Iww[c] * (p->ang_damping + p->ang_damping * wn);
+            for (int c = 0; c < 3; c++) rc[c] = k->p[i][c] - k->o[i][c];
+            v3_cross(rc, F, t1);
+            for (int c = 0; c < 3; c++) { Fs[i][c] += F[c]; Ns[i][c] += T[c] + t1[c]; }
+            /* composite: mass, first moment, inertia about the world origin (Steiner) */
+            const double* pc = k->p[i];
+            const double pp = v3_dot(pc, pc);
+            Mc[i] += mi;
+            for (int c = 0; c < 3; c++) H[i][c] += mi * pc[c];
+            for (int a = 0; a < 3; a++)
+                for (int c = 0; c < 3; c++) Io[i][a * 3 + c] += Iw[a * 3 + c] + mi * ((a == c ? pp : 0.0) - pc[a] * pc[c]);
+        }
+        const int par = m->parent[i];
+        if (par >= 0) {   /* hand the subtree to the parent: the moment moves from o_i to o_par */
+            double r[3] = {k->o[i][0] - k->o[par][0], k->o[i][1] - k->o[par][1], k->o[i][2] - k->o[par][2]}, t1[3];
+            v3_cross(r, Fs[i], t1);
+            for (int c = 0; c < 3; c++) { Fs[par][c] += Fs[i][c]; Ns[par][c] += Ns[i][c] + t1[c]; H[par][c] += H[i][c]; }
+            Mc[par] += Mc[i];
+            for (int c = 0; c < 9; c++) Io[par][c] += Io[i][c];
+        }
+    }
+    for (int d = 0; d < nd; d++) {
+        const int i = m->link_of_dof[d];
+        b[d] = m->jtype[i] == PGX_JOINT_REVOLUTE ? v3_dot(k->z[i], Ns[i]) : v3_dot(k->z[i], Fs[i]);
+    }
+    /* M by composite rigid bodies (revolute dofs; a prismatic dof's column is f alone) */
+    memset(M, 0, sizeof(double) * nd * nd);
+    for (int dj = 0; dj < nd; dj++) {
+        const int j = m->link_of_dof[dj];
+        const double* z = k->z[j];
+        const double* o = k->o[j];
+        double f[3], n[3], t1[3], t2[3];
+        if (m->jtype[j] == PGX_JOINT_REVOLUTE) {
+            /* f = z x (H - Mc o); angular momentum about o: Io z - o x (z x H) - H x (z x o)
+             *   + Mc o x (z x o)  (the composite's inertia moved from the origin to o) */
+            double hm[3] = {H[j][0] - Mc[j] * o[0], H[j][1] - Mc[j] * o[1], H[j][2] - Mc[j] * o[2]};
+            v3_cross(z, hm, f);
+            m3_v(Io[j], z, n);
+            double zh[3], zo[3];
+            v3_cross(z, H[j], zh);
+            v3_cross(z, o, zo);
+            v3_cross(o, zh, t1);
+            v3_cross(H[j], zo, t2);
+            double t3[3];
+            v3_cross(o, zo, t3);
+            for (int c = 0; c < 3; c++) n[c] = n[c] - t1[c] - t2[c] + Mc[j] * t3[c];
+        } else {
+            for (int c = 0; c < 3; c++) { f[c] = Mc[j] * z[c]; n[c] = 0.0; }
+            double t3[3];
+            v3_cross(H[j], z, t3);   /* moment about o of the translating composite: (c - o) x Mc z */
+            v3_cross(o, f, t1);
+            for (int c = 0; c < 3; c++) n[c] = t3[c] - t1[c];
+        }
+        /* up the chain: dof i on the path from link j to the root */
+        for (int a = j; a >= 0; a = m->parent[a]) {
+            const int di = m->dof_of_link[a];
+            if (di < 0) continue;
+            double r[3] = {o[0] - k->o[a][0], o[1] - k->o[a][1], o[2] - k->o[a][2]};
+            v3_cross(r, f, t1);
+            double val = m->jtype[a] == PGX_JOINT_REVOLUTE
+                             ? k->z[a][0] * (n[0] + t1[0]) + k->z[a][1] * (n[1] + t1[1]) + k->z[a][2] * (n[2] + t1[2])
+                             : v3_dot(k->z[a], f);
+            M[di * nd + dj] = val;
+            M[dj * nd + di] = val;
+        }
+    }
+}
+
+void pgxo_dyn_recursive(const pgx_model* m, const pgx_sim_params* p, const double base[3], const double* q,
+                        const double* qd, int with_gravity, double* M, double* b) {
+    kin_t k;
+    fk(m, base, q, &k);
+    dyn_recursive(m, p, &k, qd, with_gravity, M, b);
+}
+
 /* SPD solve / inverse via Cholesky (fp64) */
 static int chol(int n, const double* A, double* Lm) {
     for (int i = 0; i < n; i++)
@@ -345,7 +496,8 @@ static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x >
  *    vs cube: spheres sampled along the capsule axis at <= r/2 spacing vs the box;
  *  - rows per point: normal (impulse >= 0; rhs from ERP 0.2 when penetrating, from
  *    -distance/dt when separated), two friction rows along btPlaneSpace1(normal) with
- *    |impulse| <= mu * normal impulse (mu = 0.5 * 0.5); solved after the joint rows in
+ *    |impulse| <= mu * normal impulse (mu: the two bodies' lateral frictions multiplied, 0.5 * 0.5,
+ *    but 1.0 * 0.5 for panda_ee's capsules -- panda.py:69-70); solved after the joint rows in
  *    every sweep (normal rows, then friction rows; a friction row is skipped while its
  *    normal impulse is 0), same residual exit;
  *  - body A is the robot (or the cube against the table), B the table (or the cube):
@@ -622,8 +774,12 @@ static void substep_impl(const pgx_model* m, const pgx_sim_params* p, const doub
     int ncon = W ? detect(m, p, W, &k, obj, con) : 0;
     PGXO_PHASE(2);
     double M[D * D], Lm[D * D], b[D], qdd[D], Minv[D * D];
-    mass_matrix(m, &k, M);
-    bias(m, p, &k, qd, 1, 1, b);
+    if (p->flags & PGX_FLAG_DYN_RECURSIVE) {
+        dyn_recursive(m, p, &k, qd, 1, M, b);
+    } else {
+        mass_matrix(m, &k, M);
+        bias(m, p, &k, qd, 1, 1, b);
+    }
     memset(Lm, 0, sizeof Lm);
     chol(nd, M, Lm);
     double nb[D] = {0};
@@ -774,8 +930,11 @@ static void substep_impl(const pgx_model* m, const pgx_sim_params* p, const doub
                     if (pass) { /* friction: bounds from the normal impulse, skipped while it is 0 */
                         double ln = cr[3 * c].lam;
                         if (!(ln > 0.0)) continue;
-                        R->lo = -p->friction * ln;
-                        R->hi = p->friction * ln;
+                        /* combined lateral friction (btManifoldResult: the product): the cube
+                         * against the table / plane, or the robot link against any body */
+                        const double mu = con[c].grp == 0 ? p->friction : p->link_friction[con[c].link];
+                        R->lo = -mu * ln;
+                        R->hi = mu * ln;
                     }
                     double jdv = 0;
                     for (int d = 0; d < nd; d++) jdv += R->Jr[d] * dv[d];
@@ -1565,6 +1724,28 @@ double pgxo_ao_link_distances(const pgx_config* c, const double* q, const double
 }
 int pgxo_ao_collided(const pgx_config* c, const double* q, const double* obst) { return ao_collided(c, q, obst); }
 
+/* check_collided's margin at q: min over the collision links of the obstacle distance and over
+ * links 2..ee of the table distance (collided <=> margin <= 0), every distance measured */
+static double ao_margin(const pgx_config* c, const double* q, const double* obst) {
+    kin_t k;
+    fk(c->model, c->base_pos, q, &k);
+    double dist[PGX_AO_LINKS], pa[PGX_AO_LINKS][3], pb[PGX_AO_LINKS][3];
+    double mg = ao_link_distances(c, &k, obst, dist, pa, pb);
+    for (int l = 0; l < PGX_AO_LINKS; l++) mg = dist[l] < mg ? dist[l] : mg;
+    return mg;
+}
+/* Diagnostics (tests): with a buffer set, pgxo_vec_step records per ReachAO env the collision
+ * margin of every substep check that ran, as the smallest |margin| of the step -- how close the
+ * step's collision decisions came to their threshold -- and the margin at the last check. */
+static double* diag_margin_abs;
+static double* diag_margin_last;
+static int64_t diag_margin_n;
+void pgxo_diag_collision_margin(double* min_abs, double* last, int64_t n) {
+    diag_margin_abs = min_abs;
+    diag_margin_last = last;
+    diag_margin_n = n;
+}
+
 /* RobotTaskEnv.step (core.py:352-368) for one env + TimeLimit + VecEnv auto-reset */
 int pgxo_vec_step(const pgx_config* c, int64_t n, double* q, double* qd, double* goal, double* obj, int32_t* elapsed,
                   uint32_t* episode, const float* action, float* obs, float* ag, float* dg, float* reward,
@@ -1612,11 +1793,18 @@ int pgxo_vec_step(const pgx_config* c, int64_t n, double* q, double* qd, double*
         }
         const int ao = c->task == PGX_TASK_REACH_AO;
         int collided = 0;
+        const int diag_m = ao && diag_margin_abs && e < diag_margin_n;
+        if (diag_m) diag_margin_abs[e] = diag_margin_last[e] = 1e300;
         for (int s = 0; s < p->n_substeps; s++) {
             memcpy(oe + OBJ_QC, qe, 7 * sizeof(double));   /* the link cache: the pose this substep solves at */
             pgxo_world_substep(c, qe, qde, oe, mot, NULL);
             /* ReachAO step_check_collision (reach_ao.py:182-188) */
             PGXO_PHASE(8);
+            if (diag_m) {
+                const double mg = ao_margin(c, qe, oe + OBJ_AO);
+                diag_margin_last[e] = mg;
+                if (fabs(mg) < diag_margin_abs[e]) diag_margin_abs[e] = fabs(mg);
+            }
             if (ao && ao_collided(c, qe, oe + OBJ_AO)) { collided = 1; break; }
         }
         PGXO_PHASE(6);

@@ -40,6 +40,10 @@ void pgxo_link_velocity(const pgx_model* m, const double base[3], const double* 
 void pgxo_mass_matrix(const pgx_model* m, const double base[3], const double* q, double* M);
 void pgxo_bias(const pgx_model* m, const pgx_sim_params* p, const double base[3], const double* q,
                const double* qd, int with_gravity, double* b);
+/* M and b in the recursive form (CRBA + Newton-Euler), the formulation the kernel computes; the
+ * substeps use it with the oracle flag PGX_FLAG_DYN_RECURSIVE (operation count) */
+void pgxo_dyn_recursive(const pgx_model* m, const pgx_sim_params* p, const double base[3], const double* q,
+                        const double* qd, int with_gravity, double* M, double* b);
 int pgxo_ik(const pgx_model* m, const pgx_sim_params* p, const double base[3], const double* q_start,
             int link, const double target_pos[3], const double target_orn[4], double* q_out,
             pgxo_stats* st);
@@ -72,6 +76,10 @@ double pgxo_ao_capsule_box(const double* A, const double* B, double r, const dou
 double pgxo_ao_link_distances(const pgx_config* cfg, const double* q, const double* obst, double* dist, double* pa,
                               double* pb);
 int pgxo_ao_collided(const pgx_config* cfg, const double* q, const double* obst);
+/* diagnostics: per env of the following pgxo_vec_step calls (ReachAO), the smallest |margin| of
+ * check_collided over the substep checks that ran and the margin at the last one (collided <=>
+ * margin <= 0); NULL buffers switch it off */
+void pgxo_diag_collision_margin(double* min_abs, double* last, int64_t n);
 
 /* reward / success, reference utils.distance + Reach.is_success / compute_reward */
 double pgxo_distance_f32_f64(const float ag[3], const double g[3]);

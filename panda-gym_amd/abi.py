@@ -35,10 +35,12 @@ FLAG_CONSTRAINT_PASS_BIAS = 1
 FLAG_IK_COM = 2
 FLAG_NO_RESIDUAL_EXIT = 4
 FLAG_LINKSTATE_CURRENT = 8   # getLinkState at the pose after the last substep (rejected hypothesis)
+FLAG_DYN_RECURSIVE = 16      # oracle: M, b by CRBA + Newton-Euler (the kernel's formulation), for the op count
 
 HER_FUTURE, HER_FINAL, HER_EPISODE = 0, 1, 2
 
 PGX_OK = 0
+PGX_E_INVALID, PGX_E_HIP, PGX_E_UNSUPPORTED, PGX_E_NOMEM = -1, -2, -3, -4
 
 
 class PgxModel(C.Structure):
@@ -68,7 +70,7 @@ class PgxSimParams(C.Structure):
         ("ik_max_angle", C.c_double), ("n_substeps", C.c_int32), ("num_iterations", C.c_int32),
         ("ik_max_iters", C.c_int32), ("flags", C.c_int32),
         ("contact_distance", C.c_double), ("contact_erp", C.c_double), ("friction", C.c_double),
-        ("warmstart", C.c_double),
+        ("warmstart", C.c_double), ("link_friction", C.c_double * MAX_LINKS),
     ]
 
 
@@ -201,10 +203,15 @@ def default_sim_params(n_substeps: int = 20, flags: int = 0) -> PgxSimParams:
     p.contact_erp = 0.2                      # btMultiBodyConstraintSolver: contacts use m_erp
     p.friction = 0.5 * 0.5                   # default lateral friction 0.5 per body, product combine
     p.warmstart = 0.85                       # btContactSolverInfo m_warmstartingFactor
+    # robot links against the scene (0.5 each): 0.5 x the link's lateral friction; Panda.__init__
+    # sets links 9, 10 (fingers_indices: panda_ee, panda_leftfinger in custom_0) to 1.0 (panda.py:69-70)
+    for i in range(MAX_LINKS):
+        p.link_friction[i] = 0.5 * (1.0 if i in FINGER_FRICTION_LINKS else 0.5)
     return p
 
 
 NEUTRAL_Q = [0.0, -0.3, 0.0, -2.2, 0.0, 2.0, math.pi / 4, 0.0, 0.0]        # panda.py:67
+FINGER_FRICTION_LINKS = (9, 10)   # Panda.fingers_indices (panda.py:66), lateral friction 1.0 (panda.py:69-70)
 JOINT_FORCES = [87.0, 87.0, 87.0, 87.0, 12.0, 120.0, 120.0, 170.0, 170.0]  # panda.py:63
 
 

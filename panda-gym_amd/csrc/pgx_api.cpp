@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/pgx.h"
 #include "pgx_default_model.h"
@@ -71,6 +72,8 @@ struct pgx_env {
     PgxDevState ds;
     void* blob;
     size_t blob_bytes;
+    /* device snapshots by id (pgx_snapshot): slot i holds state id i, nullptr = free */
+    std::vector<void*> snaps;
 };
 
 extern "C" {
@@ -280,6 +283,10 @@ static int build_dev_model(const pgx_config* cfg, PgxDevModel* dm) {
     dm->contact_erp = (float)p->contact_erp;
     dm->friction = (float)p->friction;
     dm->warmstart = (float)p->warmstart;
+    for (int c = 0; c < m->n_capsules && c < 16; c++) {
+        const int li = m->cap_link[c];
+        dm->cap_mu[c] = (float)(li >= 0 && li < PGX_MAX_LINKS ? p->link_friction[li] : p->friction);
+    }
     if (p->flags != 0) return fail(PGX_E_UNSUPPORTED, "modelling flags are oracle-only");
     int rc = check_compiled_tables(*dm);
     if (!rc) rc = check_capsules(m, R, O);
@@ -456,6 +463,8 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
 void pgx_destroy(pgx_handle h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
+    for (void* p : h->snaps)
+        if (p) (void)hipFree(p);
     (void)hipFree(h->blob);
     delete h;
 }
@@ -541,6 +550,52 @@ int pgx_restore_state(pgx_handle h, const void* src, void* stream) {
     if (!h || !src) return fail(PGX_E_INVALID, "null argument");
     return hip_check(hipMemcpyAsync(h->blob, src, h->blob_bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream),
                      "restore_state copy");
+}
+
+/* Snapshot ids (PyBullet.save_state / restore_state / remove_state, pybullet.py:79-102): an id
+ * is the first non-negative integer not in use, restoring or removing an id that is not in use
+ * fails (pybullet raises pybullet.error, test/save_and_restore_test.py:30-36).  The snapshot is
+ * a device copy of the whole state blob on the caller's stream; the buffer is allocated here
+ * (hipMalloc: not a step-path call) and freed by pgx_release or pgx_destroy. */
+int pgx_snapshot(pgx_handle h, int32_t* state_id, void* stream) {
+    if (!h || !state_id) return fail(PGX_E_INVALID, "null argument");
+    *state_id = -1;
+    size_t id = 0;
+    while (id < h->snaps.size() && h->snaps[id]) id++;
+    int rc = hip_check(hipSetDevice(h->device), "hipSetDevice");
+    void* buf = nullptr;
+    if (!rc) rc = hip_check(hipMalloc(&buf, h->blob_bytes), "hipMalloc(snapshot)");
+    if (rc) return rc;
+    rc = hip_check(hipMemcpyAsync(buf, h->blob, h->blob_bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream),
+                   "snapshot copy");
+    if (rc) { (void)hipFree(buf); return rc; }
+    if (id == h->snaps.size()) h->snaps.push_back(buf);
+    else h->snaps[id] = buf;
+    *state_id = (int32_t)id;
+    return PGX_OK;
+}
+
+static bool snap_valid(pgx_handle h, int32_t id) {
+    return id >= 0 && (size_t)id < h->snaps.size() && h->snaps[id] != nullptr;
+}
+
+int pgx_restore(pgx_handle h, int32_t state_id, void* stream) {
+    if (!h) return fail(PGX_E_INVALID, "null handle");
+    if (!snap_valid(h, state_id)) return fail(PGX_E_INVALID, "Couldn't restore state %d: no such saved state", state_id);
+    return hip_check(hipMemcpyAsync(h->blob, h->snaps[state_id], h->blob_bytes, hipMemcpyDeviceToDevice,
+                                    (hipStream_t)stream),
+                     "restore copy");
+}
+
+int pgx_release(pgx_handle h, int32_t state_id) {
+    if (!h) return fail(PGX_E_INVALID, "null handle");
+    if (!snap_valid(h, state_id)) return fail(PGX_E_INVALID, "Couldn't remove state %d: no such saved state", state_id);
+    /* the copies that read or write the buffer were queued on a stream: wait for them */
+    int rc = hip_check(hipSetDevice(h->device), "hipSetDevice");
+    if (!rc) rc = hip_check(hipDeviceSynchronize(), "release sync");
+    if (!rc) rc = hip_check(hipFree(h->snaps[state_id]), "hipFree(snapshot)");
+    h->snaps[state_id] = nullptr;
+    return rc;
 }
 
 }  // extern "C"

@@ -42,6 +42,8 @@ struct PgxDevModel {
     float contact_dist, contact_erp, friction, warmstart;
     float residual_abs;       /* largest t >= 0 with fl(t * t) <= residual_thr: the sweep exit
                                  test resid * resid <= residual_thr as one compare, resid <= t */
+    float cap_mu[16];         /* combined lateral friction of capsule c's link against the scene
+                                 (pgx_sim_params.link_friction of its link; PGX_NCAP used) */
 };
 
 struct PgxDevEnv {

@@ -709,6 +709,25 @@ static_assert(PGX_ROBOT_POINTS_ONE_LANE == CG, "the one-lane solver holds CG rob
 constexpr int CACHE_N = 2 * PGX_CONTACT_SLOTS;
 constexpr int CACHE1 = 2 * CG;           /* robot slots of the cache */
 constexpr float kTableIdLimit = 32.0f;   /* robot feature ids < 32: capsule end vs table/plane */
+static_assert(PGX_NCAP <= 16, "PgxDevModel.cap_mu holds 16 capsules");
+
+/* Combined lateral friction of a robot contact point: its capsule's link against the other body
+ * (PgxDevModel.cap_mu: pgx_sim_params.link_friction -- 0.25, and 0.5 for panda_ee, whose lateral
+ * friction Panda.__init__ raises to 1.0, panda.py:69-70).  The capsule from the feature id: table /
+ * plane 2c + end, cube 32 + 16c + sample, obstacle 32 + 6c + obstacle (AO).  In the default build
+ * the table is a compile-time constant, so the chain folds to the capsules that differ from the
+ * cube's pair (m.friction). */
+template <int AO>
+__device__ __forceinline__ float point_mu(MRef m, float id) {
+    const float cf = id < kTableIdLimit ? id * 0.5f : (id - kTableIdLimit) * (AO ? (1.0f / 6.0f) : 0.0625f);
+    const int cap = (int)(cf + 1e-3f);   /* (ids are exact small integers; the margin covers 1/6's rounding) */
+    float mu = m.friction;
+    sfor<0, PGX_NCAP>([&](auto kc) __attribute__((always_inline)) {
+        constexpr int K = decltype(kc)::value;
+        mu = cap == K ? m.cap_mu[K] : mu;
+    });
+    return mu;
+}
 
 template <int W, int OBJ = 1, int FULL = 0>
 struct ContactLdsT {
@@ -736,12 +755,14 @@ struct ContactLdsT {
     /* ReachAO: obstacle centres, per collision link the closest distance and unit vector */
     float aoC[PGX_AO_OBSTACLES][3][W];
     float aoD[PGX_AO_LINKS][W], aoU[PGX_AO_LINKS][3][W];
-    /* wide layout: the contact rows' J (13 coordinates) and M^-1 J^T (arm part) per env,
-     * row-major [row q][coordinate], so lane q reads its row back with ds_read_b128 (a transpose) */
-    /* the extra rows (robot points CG..RB-1, the rare path) keep J and M^-1 J^T jinv here for
-     * the whole solve (lane c reads coordinate c), and per row rhs', lambda', lambda' at the
+    /* wide layout: the register rows' J (13 coordinates) and M^-1 J^T (arm part) per env,
+     * row-major [row q][coordinate], so lane q reads its row back with ds_read_b128 (a transpose);
+     * J stays through the sweeps (the register rows' velocities after an extra-row block) */
+    float4 wJ[W == 64 ? 1 : W][W == 64 ? 1 : NQR][4], wR[W == 64 ? 1 : W][W == 64 ? 1 : NQR][2];
+    /* the extra rows (robot points CG..RB-1) for the whole solve: per coordinate lane c the
+     * pair (J_c, (M^-1 J^T)_c jinv), one ds_read_b64; per row rhs', lambda', lambda' at the
      * solve's start, the friction bound factor fk and jinv */
-    float4 wJ[W == 64 ? 1 : W][W == 64 ? 1 : NQX][4], wR[W == 64 ? 1 : W][W == 64 ? 1 : NQX][2];
+    float2 xd[(W == 64 || XR == 1) ? 1 : W][XR][16];
     float xrhs[XR][W], xlam[XR][W], xlam0[XR][W], xfk[XR][W], xjinv[XR][W];
     /* wide layout, the register points' normal rows: jinv (the cache's impulse lambda' jinv)
      * and lambda' at the solve's start (a redo), kept here through the sweeps */
@@ -754,9 +775,6 @@ struct ContactLdsT {
      * double-buffered: getLinkState's cached pose is the last completed substep's start) */
     float ltq[W == 64 ? 1 : PGX_NJ][W], lqs[W == 64 ? 1 : 2][W == 64 ? 1 : PGX_NJ][W];
     float lkc[W == 64 ? 1 : 16][W == 64 ? 1 : 16];   /* the lane constants (LaneK fields x lane c) */
-    /* the register rows' Delassus entries against the extra rows: lane l of Delassus register b
-     * reads W[16 b + l][extra row] jinv (its gw update for that row's impulse) */
-    float wx[W == 64 ? 1 : W][XR > 1 ? 2 : 1][XR][16];
     /* one-lane speculative solve: the sweep's start velocities (dv, dvl, dvw) for a redo */
     float spec0[W == 64 ? NJ + 6 : 1][W == 64 ? W : 1];
 };
@@ -1777,6 +1795,9 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
 
     /* ---- contact rows (setup + warm start) */
     int n0 = 0, n1 = 0;
+    float mu1[CG];   /* the robot points' combined friction (point_mu) */
+#pragma unroll
+    for (int k = 0; k < CG; k++) mu1[k] = m.friction;
     if (CONT) {
         ContactLds& L = *Lp;
         n0 = L.cnt[0][ln];
@@ -1814,6 +1835,7 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
                 const V3 rb = v3(L.g1rb[k][0][ln], L.g1rb[k][1][ln], L.g1rb[k][2][ln]);
                 const int jl = L.g1j[k][ln];
                 const float id = L.g1id[k][ln];
+                mu1[k] = point_mu<AO>(m, id);
                 const bool vs_obj = OBJ && id >= kTableIdLimit;
                 const float warm = warm_lookup<CG>(L, ln, CACHE1, id, m.warmstart);
                 V3 t1, t2;
@@ -2010,8 +2032,8 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
                         const float4 q2 = L.g1q[k][dir][2][ln], q3 = L.g1q[k][dir][3][ln];
                         const float4 q4 = L.g1q[k][dir][4][ln], q5 = L.g1q[k][dir][5][ln];
                         const float jv = q1.w, dn = q3.w, rh = q4.w, lm = lam1[k][dir];
-                        const float lo = fr ? -mu * ln_n : 0.0f;
-                        const float hi = fr ? mu * ln_n : 1e10f;
+                        const float lo = fr ? -mu1[k] * ln_n : 0.0f;
+                        const float hi = fr ? mu1[k] * ln_n : 1e10f;
                         /* two partial sums: half the dependent-FMA chain */
                         float ja = q0.x * dv[0] + q0.z * dv[2] + q1.x * dv[4] + q1.z * dv[6];
                         float jb = q0.y * dv[1] + q0.w * dv[3] + q1.y * dv[5];
@@ -2238,9 +2260,12 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     constexpr int RB = CONT ? ContactLdsGT<OBJ, FULL>::RB : CG;   /* robot budget: points CG.. are the extra rows */
     constexpr int NQR = ContactLdsGT<OBJ, FULL>::NQR;
     constexpr int NC_ = OBJ ? 13 : NJ;          /* generalized coordinates in lanes */
+    constexpr int XSTEP = 4;                    /* extra points run in the sweep: multiples of XSTEP */
     int n1x = 0;                                /* the wave's largest robot point count, when above CG */
+    int nxr = 0;                                /* extra points the sweep runs: n1x - CG rounded up to XSTEP */
     float cJ[NP > 0 ? NP : 1][3], cR[NP > 0 ? NP : 1][3], crhs[NP > 0 ? NP : 1][3], cjinv[NP > 0 ? NP : 1][3];
     float cden[NP > 0 ? NP : 1][3], clam[NP > 0 ? NP : 1][3];
+    float pmu[NP > 0 ? NP : 1];   /* the points' combined lateral friction (object scene: m.friction) */
     bool act[NP > 0 ? NP : 1];
     int n0 = 0, n1 = 0;
     if (CONT) {
@@ -2263,6 +2288,8 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             for (int s2 = 0; s2 < CG; s2++) w = ids[s2] == id ? m.warmstart * ims[s2] : w;
             return w;
         };
+#pragma unroll
+        for (int p = 0; p < NP; p++) pmu[p] = m.friction;
 #pragma unroll
         for (int k = 0; k < P0; k++) { /* object vertices vs the box top: object coordinates only */
             act[k] = k < n0;
@@ -2330,6 +2357,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 const V3 rb = gRb[k];
                 const int jl = gJ[k];
                 const float id = gId[k];
+                pmu[p] = point_mu<AO>(m, id);
                 const bool vs_obj = OBJ && id >= kTableIdLimit;
                 const float warm = warm_of(cid1, cim1, id);
                 V3 t1, t2;
@@ -2371,15 +2399,28 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         }
         /* ---- robot points CG..RB-1 (an env with more than CG robot points: fp64 oracle under
          * the random policy, Push / PickAndPlace 1.2 % of substeps, Reach 1e-5): the same row
-         * setup, kept in LDS for the solve -- J and M^-1 J^T jinv per coordinate lane in the
-         * wJ / wR rows after the register rows, the row scalars per env -- and solved after
-         * the register rows of each half-sweep (extra_rows below) */
+         * setup, kept in LDS for the solve -- (J, M^-1 J^T jinv) per coordinate lane in xd, the
+         * row scalars per env -- and solved after the register rows of each half-sweep
+         * (extra_rows below).  The sweep runs a compile-time number of extra points, the wave's
+         * count rounded up to XSTEP: the rows past an env's own count are zero rows (bounds 0,
+         * delta' = 0 exactly), so the points the wave lacks are written as zero rows too. */
         if constexpr (RB > CG) {
             for (int k = CG; k < RB && __any(k < n1); k++) n1x = k + 1;
             n1x = __builtin_amdgcn_readfirstlane(n1x);
-            float* wj = &L.wJ[es][0][0].x;
-            float* wr = &L.wR[es][0][0].x;
-            for (int k = CG; k < n1x; k++) {   /* wave-uniform */
+            nxr = n1x > CG ? (n1x - CG + XSTEP - 1) / XSTEP * XSTEP : 0;
+            for (int k = CG; k < CG + nxr; k++) {   /* wave-uniform */
+                if (k >= n1x) {
+#pragma unroll
+                    for (int dir = 0; dir < 3; dir++) {
+                        const int xq = 3 * (P0 + k) + dir - NQR;
+                        L.xd[es][xq][c] = make_float2(0.0f, 0.0f);
+                        L.xrhs[xq][es] = 0.0f;
+                        L.xlam[xq][es] = L.xlam0[xq][es] = 0.0f;
+                        L.xfk[xq][es] = 0.0f;
+                        L.xjinv[xq][es] = 0.0f;
+                    }
+                    continue;
+                }
                 const bool a = k < n1;
                 const V3 P = v3(L.g1p[k][0][es], L.g1p[k][1][es], L.g1p[k][2][es]);
                 const V3 n = v3(L.g1n[k][0][es], L.g1n[k][1][es], L.g1n[k][2][es]);
@@ -2425,12 +2466,11 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                     const bool rok = a && ja != 0.0f;
                     const bool rok_n = a && jinv_n != 0.0f;
                     const int q = 3 * (P0 + k) + dir, xq = q - NQR;
-                    if (c < 16) wj[16 * q + c] = c < NC_ ? Ja : 0.0f;
-                    if (c < 8) wr[8 * q + c] = Ra * ja;
+                    L.xd[es][xq][c] = make_float2(c < NC_ ? Ja : 0.0f, Ra * ja);
                     /* every lane of the env writes the same (row-uniform) values */
                     L.xrhs[xq][es] = (a ? rhs : 0.0f) * da;
                     L.xlam[xq][es] = L.xlam0[xq][es] = rok_n && dir == 0 ? lam * da : 0.0f;
-                    L.xfk[xq][es] = dir == 0 ? (rok ? 3.0e38f : 0.0f) : (rok ? m.friction * jinv_n * da : 0.0f);
+                    L.xfk[xq][es] = dir == 0 ? (rok ? 3.0e38f : 0.0f) : (rok ? point_mu<AO>(m, id) * jinv_n * da : 0.0f);
                     L.xjinv[xq][es] = ja;
                 }
             }
@@ -2516,21 +2556,6 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                     w = fmaf(Jq[l], bcast16<l>(gv), w);
                 });
                 gwr = w;
-                if constexpr (RB > CG) {   /* W[q][x] jinv_x against the extra rows x (rare) */
-                    for (int xq = 0; xq < 3 * (n1x - CG); xq++) {
-                        const int sx = NQR + xq;
-                        const float* js = &L.wJ[es][sx][0].x;
-                        const float* rs = &L.wR[es][sx][0].x;   /* M^-1 J^T jinv, coordinates 0..7 */
-                        const float jv = L.xjinv[xq][es];
-                        float wq = 0.0f;
-                        sfor<0, NC>([&](auto lc) __attribute__((always_inline)) {
-                            constexpr int l = decltype(lc)::value;
-                            const float rl_ = l < 8 ? rs[l] : (l < 10 ? inv_m : inv_i) * js[l] * jv;
-                            wq = fmaf(Jq[l], rl_, wq);
-                        });
-                        L.wx[es][decltype(reg_c)::value][xq][c] = rl ? wq : 0.0f;
-                    }
-                }
             };
             build(IC<0>{}, Wm, Wc, gw);
             /* rows 16..23 belong to robot points 1..3 (slots fill from 0): idle in every env of
@@ -2548,7 +2573,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
 #pragma unroll
             for (int b = 0; b < XB; b++) {
                 const int xq = GW * b + c;
-                const bool ok = xq < 3 * (n1x - CG);
+                const bool ok = xq < 3 * nxr;
                 const int xr = ok ? xq : 0;
                 xs_lam[b] = ok ? L.xlam0[xr][es] : 0.0f;
                 if (start) {
@@ -2561,7 +2586,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     };
 #pragma unroll
     for (int b = 0; b < XB; b++) { xs_rhs[b] = 0.0f; xs_lam[b] = 0.0f; xs_fk[b] = 0.0f; xs_jinv[b] = 0.0f; }
-    if (RB > CG && n1x > CG) load_xs(true);
+    if (RB > CG && nxr > 0) load_xs(true);
     PGX_PROF_MARK(23);
 
     /* ---- motor / limit rows (as substep()): per row rhs and lambda, per dof jinv / den */
@@ -2643,7 +2668,9 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         }
     };
     init_bounds();
-    auto mrow = [&](auto rc, float& resid) __attribute__((always_inline)) {
+    /* G2 (g2_c): the second Delassus register holds live rows in this solve (rows 16.. exist:
+     * robot points past the first in the object tasks); without them its updates are skipped */
+    auto mrow = [&](auto rc, auto g2_c, float& resid) __attribute__((always_inline)) {
         constexpr int r = decltype(rc)::value;
         constexpr int kind = kPgxRowCode[r] >> 4, d = kPgxRowCode[r] & 15;
         /* delta' = clamp(rhs' - s v_d, lo' - lambda', hi' - lambda'): the shifted bounds are
@@ -2670,13 +2697,9 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         const float sd = kind == 2 ? -delta : delta;
         gv += mcs[d] * sd;
         if constexpr (WROWS) gw += wms[d] * sd;
-        if constexpr (TWO) gw2 += wms2[d] * sd;
+        if constexpr (TWO && decltype(g2_c)::value) gw2 += wms2[d] * sd;
         resid = fmaxf(resid, fabsf(delta));
     };
-    /* friction coefficient in a register: a model load inside the bound selects makes the
-     * compiler branch around it (a scalar load + wait per friction row) */
-    float mu = m.friction;
-    asm("" : "+s"(mu));
     /* contact rows in scaled units too: lambda' = lambda den, friction bounds
      * +-mu lambda_n den_f = +-lambda'_n (mu jinv_n den_f); an idle row (inactive point, no
      * usable den, or a friction row while the normal impulse is 0) gets the bounds
@@ -2689,7 +2712,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
 #pragma unroll
         for (int dir = 0; dir < 3; dir++) {
             rok[p][dir] = act[p] && cjinv[p][dir] != 0.0f;
-            fk[p][dir] = rok[p][dir] ? mu * cjinv[p][0] * cden[p][dir] : 0.0f;   /* unusable row: bounds 0 */
+            fk[p][dir] = rok[p][dir] ? pmu[p] * cjinv[p][0] * cden[p][dir] : 0.0f;   /* unusable row: bounds 0 */
             crhs[p][dir] *= cden[p][dir];
             clam[p][dir] *= cden[p][dir];
             cR[p][dir] *= cjinv[p][dir];
@@ -2743,7 +2766,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         chi[p] = rok[p][0] ? 3.0e38f : 0.0f;
         if (WROWS && !rok[p][0]) clam[p][0] = 0.0f;   /* already applied to gv; the cache stores lambda' jinv = 0 */
     }
-    auto crow = [&](auto pc, auto dc, const bool fr, float& resid) __attribute__((always_inline)) {
+    auto crow = [&](auto pc, auto dc, const bool fr, auto g2_c, float& resid) __attribute__((always_inline)) {
         constexpr int p = decltype(pc)::value, dir = decltype(dc)::value, q = 3 * p + dir;
         const float ln_n = clam[p][0], lm = clam[p][dir];
         float lo, hi;
@@ -2763,7 +2786,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         clam[p][dir] = lm + delta;
         gv += cR[p][dir] * delta;
         gw += Wc[q] * delta;
-        if constexpr (TWO) gw2 += Wc2[q] * delta;
+        if constexpr (TWO && decltype(g2_c)::value) gw2 += Wc2[q] * delta;
         resid = fmaxf(resid, fabsf(delta));
     };
     /* the wave's largest robot-point count, a scalar: the per-point branches in the sweep
@@ -2779,73 +2802,97 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
      * [lambda', lambda'] with lambda' = 0 -> delta' = 0, bit for bit), so no per-point branch
      * sits inside the sweep.  The object-scene rows (P0 points, a resting cube has 4) run in
      * every sweep of the object tasks, idle points predicated the same way. */
-    /* the extra rows (robot points CG..n1x-1) of one half-sweep, after the register rows in the
+    /* the extra rows (robot points CG..CG+NX-1) of one half-sweep, after the register rows in the
      * same order as the oracle's (normal rows, then friction rows; points by id): the row
-     * velocity by a 16-lane reduction (no Delassus lane), J and M^-1 J^T jinv per coordinate
-     * lane and the register rows' couplings from LDS (loads independent of the chain), the row
-     * scalars in lanes of registers (row x: lane x % 16 of xs_*[x / 16]), read by broadcast */
+     * velocity by a 16-lane reduction (no Delassus lane), (J, M^-1 J^T jinv) per coordinate lane
+     * from LDS (one ds_read_b64, independent of the chain: straight-line code, no branch, so the
+     * reads issue ahead), the row scalars in lanes of registers (row x: lane x % 16 of
+     * xs_*[x / 16]), read by broadcast.  The register rows' Delassus lanes are not updated per
+     * extra row: after the block, every register row's x' = rhs' - J_q.dv drops by J_q . (the
+     * block's change of dv) -- one 13-term dot product per lane and Delassus register, with J_q
+     * from the transpose rows (wJ) -- instead of an LDS coupling and an fma per extra row. */
     int rcol = c;   /* the coordinate of lane c's R entry (MODE 3 slot lanes: their dof's) */
-    auto extra_rows = [&](auto fr_c, float& resid) __attribute__((always_inline)) {
-        if constexpr (WROWS && RB > CG) {
-            constexpr int FR = decltype(fr_c)::value;
+    auto extra_rows = [&](auto fr_c, auto nx_c, auto g2_c, float& resid) __attribute__((always_inline)) {
+        constexpr int FR = decltype(fr_c)::value, NX = decltype(nx_c)::value;
+        if constexpr (WROWS && RB > CG && NX > 0) {
             ContactLdsGT<OBJ, FULL>& L = *Lp;
-            const float* wj = &L.wJ[es][0][0].x;
-            const float* wr = &L.wR[es][0][0].x;
-            sfor<0, RB - CG>([&](auto kc) __attribute__((always_inline)) {
+            const float gvb = gv;
+            sfor<0, NX>([&](auto kc) __attribute__((always_inline)) {
                 constexpr int kx = decltype(kc)::value;
-                if (CG + kx < n1x) {
-                    sfor<FR ? 1 : 0, FR ? 3 : 1>([&](auto dc) __attribute__((always_inline)) {
-                        constexpr int dir = decltype(dc)::value, xq = 3 * kx + dir, q = NQR + xq;
-                        constexpr int b = xq / GW, l = xq % GW, bn = (3 * kx) / GW, ln_ = (3 * kx) % GW;
-                        const float J = wj[16 * q + c];
-                        const float jv = bcast16<l>(xs_jinv[b]);
-                        const float Rs = rcol < 8 ? wr[8 * q + rcol] : kobj * J * jv;
-                        const float w = sum16(J * gv);
-                        const float lm = bcast16<l>(xs_lam[b]), fkv = bcast16<l>(xs_fk[b]);
-                        float lo, hi;
-                        if constexpr (dir != 0) {
-                            const float ln_n = bcast16<ln_>(xs_lam[bn]);
-                            const float mk = ln_n > 0.0f ? 1.0f : 0.0f;
-                            const f2 bb = ((f2){-fkv, fkv} * ln_n - lm) * mk;
-                            lo = bb.x;
-                            hi = bb.y;
-                        } else {
-                            lo = -lm;
-                            hi = fkv;
-                        }
-                        const float delta = __builtin_amdgcn_fmed3f(bcast16<l>(xs_rhs[b]) - w, lo, hi);
-                        xs_lam[b] = lane_sel<l>(lm + delta, xs_lam[b]);
-                        gv += Rs * delta;
-                        gw = fmaf(-L.wx[es][0][xq][c], delta, gw);   /* x = rhs' - w: negated coupling */
-                        if constexpr (TWO) gw2 = fmaf(-L.wx[es][1][xq][c], delta, gw2);
-                        resid = fmaxf(resid, fabsf(delta));
-                    });
-                }
+                sfor<FR ? 1 : 0, FR ? 3 : 1>([&](auto dc) __attribute__((always_inline)) {
+                    constexpr int dir = decltype(dc)::value, xq = 3 * kx + dir;
+                    constexpr int b = xq / GW, l = xq % GW, bn = (3 * kx) / GW, ln_ = (3 * kx) % GW;
+                    const float J = L.xd[es][xq][c].x;
+                    const float Rs = L.xd[es][xq][rcol].y;
+                    const float w = sum16(J * gv);
+                    const float lm = bcast16<l>(xs_lam[b]), fkv = bcast16<l>(xs_fk[b]);
+                    float lo, hi;
+                    if constexpr (dir != 0) {
+                        const float ln_n = bcast16<ln_>(xs_lam[bn]);
+                        const float mk = ln_n > 0.0f ? 1.0f : 0.0f;
+                        const f2 bb = ((f2){-fkv, fkv} * ln_n - lm) * mk;
+                        lo = bb.x;
+                        hi = bb.y;
+                    } else {
+                        lo = -lm;
+                        hi = fkv;
+                    }
+                    const float delta = __builtin_amdgcn_fmed3f(bcast16<l>(xs_rhs[b]) - w, lo, hi);
+                    xs_lam[b] = lane_sel<l>(lm + delta, xs_lam[b]);
+                    gv += Rs * delta;
+                    resid = fmaxf(resid, fabsf(delta));
+                });
             });
+            /* the register rows' velocities: x'_q -= J_q . (gv - gvb) */
+            const float dgv = gv - gvb;
+            auto correct = [&](auto reg_c, float& gwr) __attribute__((always_inline)) {
+                constexpr int R0 = decltype(reg_c)::value * GW;
+                const int qr = R0 + c < NQR ? R0 + c : NQR - 1;
+                const float4* jrow = &L.wJ[es][qr][0];
+                float Jq[NC];
+#pragma unroll
+                for (int v4 = 0; v4 < (NC + 3) / 4; v4++) {
+                    const float4 t = jrow[v4];
+                    const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (4 * v4 + u < NC) Jq[4 * v4 + u] = tv[u];
+                }
+                float d = Jq[0] * bcast16<0>(dgv);
+                sfor<1, NC>([&](auto lc) __attribute__((always_inline)) {
+                    constexpr int l2 = decltype(lc)::value;
+                    d = fmaf(Jq[l2], bcast16<l2>(dgv), d);
+                });
+                gwr -= R0 + c < NQR ? d : 0.0f;
+            };
+            correct(IC<0>{}, gw);
+            if constexpr (TWO && decltype(g2_c)::value) correct(IC<1>{}, gw2);
         }
     };
-    auto contact_rows = [&](auto nw_c, float& resid) __attribute__((always_inline)) {
+    auto contact_rows = [&](auto nw_c, auto nx_c, auto g2_c, float& resid) __attribute__((always_inline)) {
         constexpr int NW = decltype(nw_c)::value;
 #pragma unroll
         for (int fr = 0; fr < 2; fr++) {
             if (OBJ && g0_any) {
                 sfor<0, P0>([&](auto kc) __attribute__((always_inline)) {
-                    if (fr) { crow(kc, IC<1>{}, true, resid); crow(kc, IC<2>{}, true, resid); }
-                    else crow(kc, IC<0>{}, false, resid);
+                    if (fr) { crow(kc, IC<1>{}, true, g2_c, resid); crow(kc, IC<2>{}, true, g2_c, resid); }
+                    else crow(kc, IC<0>{}, false, g2_c, resid);
                 });
             }
             if (NW < 0 && !g1_any) continue;
             sfor<0, (CONT ? (NW >= 0 ? NW : CG) : 0)>([&](auto kc) __attribute__((always_inline)) {
                 constexpr int k = decltype(kc)::value;
                 if (NW >= 0 || k < n1w) {
-                    if (fr) { crow(IC<P0 + k>{}, IC<1>{}, true, resid); crow(IC<P0 + k>{}, IC<2>{}, true, resid); }
-                    else crow(IC<P0 + k>{}, IC<0>{}, false, resid);
+                    if (fr) {
+                        crow(IC<P0 + k>{}, IC<1>{}, true, g2_c, resid);
+                        crow(IC<P0 + k>{}, IC<2>{}, true, g2_c, resid);
+                    } else {
+                        crow(IC<P0 + k>{}, IC<0>{}, false, g2_c, resid);
+                    }
                 }
             });
-            if (RB > CG && NW == CG && n1x > CG) {
-                if (fr) extra_rows(IC<1>{}, resid);
-                else extra_rows(IC<0>{}, resid);
-            }
+            if (fr) extra_rows(IC<1>{}, nx_c, g2_c, resid);
+            else extra_rows(IC<0>{}, nx_c, g2_c, resid);
         }
     };
     const bool any_contact = CONT && __any(n0 > 0 || n1 > 0);
@@ -2886,7 +2933,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     constexpr int SL0 = OBJ ? 13 : NJ;   /* first slot lane: the first lane past the coordinates */
     unsigned dmask = 0u;
     float smcs[KMAX], swms[KMAX], swms2[KMAX], srh[KMAX][2], slhi[KMAX], slam[KMAX][2];
-    auto srow = [&](auto sc, auto kc, float& resid) __attribute__((always_inline)) {
+    auto srow = [&](auto sc, auto kc, auto g2_c, float& resid) __attribute__((always_inline)) {
         constexpr int S = decltype(sc)::value, KIND = decltype(kc)::value;   /* 1 lower, 2 upper */
         const float x = KIND == 2 ? srh[S][1] + bcast16<SL0 + S>(gv) : srh[S][0] - bcast16<SL0 + S>(gv);
         const float delta = __builtin_amdgcn_fmed3f(x, -slam[S][KIND - 1], slhi[S] - slam[S][KIND - 1]);
@@ -2894,62 +2941,75 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         const float sd = KIND == 2 ? -delta : delta;
         gv += smcs[S] * sd;
         if constexpr (WROWS) gw += swms[S] * sd;
-        if constexpr (TWO) gw2 += swms2[S] * sd;
+        if constexpr (TWO && decltype(g2_c)::value) gw2 += swms2[S] * sd;
         resid = fmaxf(resid, fabsf(delta));
     };
     static_assert(limit_rows_paired(), "limit rows come as (lower, upper) pairs of one dof after the motor rows");
-    auto solve = [&](auto mode_c, auto nw_c, auto k_c) __attribute__((always_inline)) {
+    auto solve = [&](auto mode_c, auto nw_c, auto k_c, auto nx_c) __attribute__((always_inline)) {
         constexpr int MODE = decltype(mode_c)::value;   /* 0 far, 1 speculative, 2 all rows, 3 partial */
         constexpr int NW = decltype(nw_c)::value;
         constexpr int K = decltype(k_c)::value;         /* MODE 3: slots in use */
+        /* NX: extra robot points (past CG) the sweep runs, 0 or a multiple of XSTEP */
+        constexpr bool G2 = TWO && (NW < 0 || 3 * (P0 + NW) > GW);
+        const IC<G2 ? 1 : 0> g2_c{};
         for (int it = 0; it < n_it; it += 2) {
             float resid = 0.0f;
             if constexpr (MODE == 1 || MODE == 3) limit_check();
             if constexpr (MODE == 3) {   /* the limit block leads the reversed sweep */
                 sfor<0, K>([&](auto i) __attribute__((always_inline)) {
                     constexpr int S = K - 1 - decltype(i)::value;
-                    srow(IC<S>{}, IC<2>{}, resid);
-                    srow(IC<S>{}, IC<1>{}, resid);
+                    srow(IC<S>{}, IC<2>{}, g2_c, resid);
+                    srow(IC<S>{}, IC<1>{}, g2_c, resid);
                     limit_check();
                 });
             }
             sfor<0, PGX_N_ROWS>([&](auto i) __attribute__((always_inline)) {
                 constexpr int r = PGX_N_ROWS - 1 - decltype(i)::value;
-                if constexpr (MODE == 2 || (kPgxRowCode[r] >> 4) == 0) mrow(IC<r>{}, resid);
+                if constexpr (MODE == 2 || (kPgxRowCode[r] >> 4) == 0) mrow(IC<r>{}, g2_c, resid);
             });
-            if (CONT && (OBJ || NW > 0 || (NW < 0 && any_contact))) contact_rows(nw_c, resid);
+            if (CONT && (OBJ || NW > 0 || (NW < 0 && any_contact))) contact_rows(nw_c, nx_c, g2_c, resid);
             PGX_PROF_SWEEP();
             if (resid <= res_thr || it + 1 >= n_it) break;
             resid = 0.0f;
             sfor<0, PGX_N_ROWS>([&](auto i) __attribute__((always_inline)) {
                 constexpr int r = decltype(i)::value;
-                if constexpr (MODE == 2 || (kPgxRowCode[r] >> 4) == 0) mrow(IC<r>{}, resid);
+                if constexpr (MODE == 2 || (kPgxRowCode[r] >> 4) == 0) mrow(IC<r>{}, g2_c, resid);
             });
             if constexpr (MODE == 1 || MODE == 3) limit_check();
             if constexpr (MODE == 3) {
                 sfor<0, K>([&](auto sc) __attribute__((always_inline)) {
-                    srow(sc, IC<1>{}, resid);
-                    srow(sc, IC<2>{}, resid);
+                    srow(sc, IC<1>{}, g2_c, resid);
+                    srow(sc, IC<2>{}, g2_c, resid);
                     limit_check();
                 });
             }
-            if (CONT && (OBJ || NW > 0 || (NW < 0 && any_contact))) contact_rows(nw_c, resid);
+            if (CONT && (OBJ || NW > 0 || (NW < 0 && any_contact))) contact_rows(nw_c, nx_c, g2_c, resid);
             PGX_PROF_SWEEP();
             if (resid <= res_thr) break;
         }
     };
-    /* the robot point count fixed at compile time (above) for every mode but far */
+    /* the robot point count fixed at compile time (above) for every mode but far; the extra
+     * points (past CG) only in the speculative and all-rows solves (the partial one hands a wave
+     * with extra points to the all-rows solve) */
     auto solve_w = [&](auto mode_c, auto k_c) __attribute__((always_inline)) {
+        constexpr int MODE = decltype(mode_c)::value;
         if constexpr (WROWS) {
-            if (n1w == 0) solve(mode_c, IC<0>{}, k_c);
-            else if (n1w <= 2) solve(mode_c, IC<2>{}, k_c);
-            else solve(mode_c, IC<4>{}, k_c);
+            if (n1w == 0) solve(mode_c, IC<0>{}, k_c, IC<0>{});
+            else if (n1w <= 2) solve(mode_c, IC<2>{}, k_c, IC<0>{});
+            else if constexpr (RB > CG && MODE != 3) {
+                if (nxr == 0) solve(mode_c, IC<CG>{}, k_c, IC<0>{});
+                else if constexpr (RB - CG <= XSTEP) solve(mode_c, IC<CG>{}, k_c, IC<XSTEP>{});
+                else if (nxr <= XSTEP) solve(mode_c, IC<CG>{}, k_c, IC<XSTEP>{});
+                else solve(mode_c, IC<CG>{}, k_c, IC<RB - CG>{});
+            } else {
+                solve(mode_c, IC<CG>{}, k_c, IC<0>{});
+            }
         } else {
-            solve(mode_c, IC<-1>{}, k_c);
+            solve(mode_c, IC<-1>{}, k_c, IC<0>{});
         }
     };
     if (__all(far)) {   /* (far implies no robot point in the wave) */
-        solve(IC<0>{}, IC<0>{}, IC<0>{});
+        solve(IC<0>{}, IC<0>{}, IC<0>{}, IC<0>{});
     } else {
         PGX_PROF_COUNT(10, 1);
         init_limit_rows();
@@ -2980,7 +3040,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
 #pragma unroll
                 for (int p = 0; p < NP; p++) Lp->pl0[p][es] = clam[p][0];
             }
-            if (PART && !NO_PART && !spec_all && nk <= KMAX) {   /* (NO_PART: all rows instead, fewer registers) */
+            if (PART && !NO_PART && !spec_all && nk <= KMAX && nxr == 0) {   /* (NO_PART: all rows instead, fewer registers) */
                 PGX_PROF_COUNT(7, 1);
                 /* slots in the pairs' table order; slot lane SL0 + S mirrors dof d_S */
                 int ds[2] = {0, 0};
@@ -3046,7 +3106,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                     clam[p][1] = 0.0f;
                     clam[p][2] = 0.0f;
                 }
-                if (RB > CG && n1x > CG) load_xs(false);
+                if (RB > CG && nxr > 0) load_xs(false);
                 init_bounds();
                 solve_w(IC<2>{}, IC<0>{});
             }
@@ -3989,9 +4049,9 @@ int pgx_launch_step_arm(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevSt
     const int per_block = wide ? EPW : 64;
     dim3 block(64), grid((e.n_envs + per_block - 1) / per_block);
     const bool two = e.wave_mode == 2 || (e.wave_mode == 0 && wide && grid.x > 1024);   /* more waves than SIMDs */
-    if (wide && e.contacts && e.full_manifold) {   /* one wave per SIMD: the extra rows' state would spill */
+    if (wide && e.contacts && e.full_manifold) {   /* Bullet's per-pair manifolds (the default budget) */
         if (e.control) PGX_STEP(1, 0, 1, 0, 2);
-        else PGX_STEP(0, 0, 1, 0, 2);
+        else PGX_STEP2(0, 0, 1, 0, 2);
         return (int)hipGetLastError();
     }
     switch ((e.control * 4 + (e.contacts ? 1 : 0)) * 2 + wide) {
@@ -4020,9 +4080,9 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
     const int variant = e.ao ? 13 : e.control * 4 + (e.has_object ? 2 : 0) + (e.contacts ? 1 : 0);
     if (wide && e.full_manifold) {
         switch (variant) {
-            case 3: PGX_STEP(0, 1, 1, 0, 2); break;
-            case 7: PGX_STEP(1, 1, 1, 0, 2); break;
-            case 13: PGX_STEP(1, 0, 1, 1, 2); break;
+            case 3: PGX_STEP2(0, 1, 1, 0, 2); break;
+            case 7: PGX_STEP2(1, 1, 1, 0, 2); break;
+            case 13: PGX_STEP2(1, 0, 1, 1, 2); break;
             default: return (int)hipErrorInvalidValue;
         }
         return (int)hipGetLastError();

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 from dataclasses import replace
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -147,14 +148,15 @@ class PandaVecEnv:
     each env a 16-lane DPP row (the solver's coordinates split over the lanes; fastest
     while the batch is too small to fill the chip one lane per env), 1 one env per lane,
     0 (default) chooses: 16 with contacts at every batch size, and up to 8192 envs without).
-    ``full_manifold`` keeps Bullet's per-pair manifolds (<= 4 points per colliding pair) up to 8
-    robot points per env in Reach / ReachAO and 12 in Push / PickAndPlace (16-lane layout only);
-    the default keeps the 4 deepest robot points (budget, rates, cost)."""
+    ``full_manifold`` (default: on wherever the layout has it, i.e. with contacts in the 16-lane
+    layout) keeps Bullet's per-pair manifolds (<= 4 points per colliding pair) up to 8 robot points
+    per env in Reach / ReachAO and 12 in Push / PickAndPlace; ``False`` keeps the 4 deepest robot
+    points (the one-lane layout's budget; DESIGN.md section 4: budget, rates, cost)."""
 
     def __init__(self, env_id: str = "PandaReach-v3", num_envs: int = 4096, device: Any = "cuda:0", seed: int = 0,
                  env_id_offset: int = 0, max_episode_steps: Optional[int] = None, auto_reset: bool = True,
                  n_substeps: int = 20, model_name: str = "panda_custom0", contacts: bool = True,
-                 lanes_per_env: int = 0, full_manifold: bool = False):
+                 lanes_per_env: int = 0, full_manifold: Optional[bool] = None):
         if torch is None:
             raise PgxError("PandaVecEnv needs torch for device buffers")
         self.lib = load()
@@ -169,6 +171,8 @@ class PandaVecEnv:
             raise PgxError("PandaVecEnv runs on a HIP device only (no CPU physics fallback)")
         self._model = abi.make_model(load_model(model_name), ee_link=11)
         self._params = abi.default_sim_params(n_substeps=n_substeps)
+        if full_manifold is None:   # the per-pair manifold budget wherever the 16-lane kernels run
+            full_manifold = bool(contacts) and lanes_per_env != 1 and os.environ.get("PGX_LANES_PER_ENV") != "1"
         self._cfg = abi.make_config(self.spec, self.num_envs, self._model, self._params, seed=seed,
                                     env_id_offset=env_id_offset, contacts=contacts, lanes_per_env=lanes_per_env,
                                     full_manifold=full_manifold)
@@ -215,8 +219,6 @@ class PandaVecEnv:
             self.reward_type = "sparse_ao"   # ReachAO.compute_reward sparse/reach (reach_ao.py:1317-1320)
         else:
             self.reward_type = "dense" if self.spec.reward == abi.REWARD_DENSE else "sparse"
-        self._snapshots: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
-        self._next_snap = 0
         self._pending: Optional[torch.Tensor] = None
         self._pending_seed: Optional[int] = None
         self._step_index = 0
@@ -462,26 +464,21 @@ class PandaVecEnv:
 
     # ----------------------------------------------------- save / restore
     def save_state(self) -> int:
-        """Device snapshot of the whole SoA state (RobotTaskEnv.save_state, core.py:310-321)."""
-        nb = C.c_int64()
-        check(self.lib.pgx_state_bytes(self._h, C.byref(nb)), "pgx_state_bytes")
-        buf = torch.empty(nb.value, dtype=torch.uint8, device=self.device)
-        check(self.lib.pgx_save_state(self._h, C.c_void_p(buf.data_ptr()), self._stream()), "pgx_save_state")
-        sid = self._next_snap
-        self._next_snap += 1
-        self._snapshots[sid] = buf
-        return sid
+        """Device snapshot of the whole SoA state (RobotTaskEnv.save_state, core.py:310-321 ->
+        PyBullet.save_state, pybullet.py:79-86): the id is libpgx's, the first non-negative
+        integer not in use."""
+        sid = C.c_int32()
+        check(self.lib.pgx_snapshot(self._h, C.byref(sid), self._stream()), "pgx_snapshot")
+        return int(sid.value)
 
     def restore_state(self, state_id: int) -> None:
-        if state_id not in self._snapshots:
-            raise PgxError(f"Could not restore state {state_id}: no such saved state")
-        buf = self._snapshots[state_id]
-        check(self.lib.pgx_restore_state(self._h, C.c_void_p(buf.data_ptr()), self._stream()), "pgx_restore_state")
+        """Restore a snapshot; an id that was removed (or never saved) raises PgxError, as
+        pybullet.error in the reference (test/save_and_restore_test.py:30-36)."""
+        check(self.lib.pgx_restore(self._h, int(state_id), self._stream()), "pgx_restore")
 
     def remove_state(self, state_id: int) -> None:
-        if state_id not in self._snapshots:
-            raise PgxError(f"Could not remove state {state_id}: no such saved state")
-        del self._snapshots[state_id]
+        """Free a snapshot; its id becomes available again (PyBullet.remove_state, pybullet.py:96-102)."""
+        check(self.lib.pgx_release(self._h, int(state_id)), "pgx_release")
 
 
 _INFO_TEMPLATES = [{"is_success": s, "is_truncated": c} for c in (False, True) for s in (False, True)]

@@ -331,9 +331,10 @@ def test_partial_limit_rows_are_exact(pg, monkeypatch, env_id, contacts, n):
 @pytest.mark.parametrize("env_id", ["PandaPush-v3", "PandaPickAndPlace-v3"])
 def test_object_kernel_two_waves_per_simd_exact(pg, monkeypatch, env_id):
     """The object kernel's two-waves-per-SIMD build (256 registers, taken above 4096 envs; its
-    all-rows solve an out-of-line call, pgs_all_rows) equals the one-wave build bit for bit, in
-    the default solve and with every substep forced through the all-rows call (PGX_PGS_MODE=2)
-    or through a redo after the speculative solve (PGX_PGS_MODE=3)."""
+    all-rows solve inline, with the limit rows' rhs' and lambda' in LDS, and no partial solve)
+    equals the one-wave build bit for bit, in the default solve and with every substep forced
+    through the all-rows solve (PGX_PGS_MODE=2) or through a redo after the speculative solve
+    (PGX_PGS_MODE=3)."""
     runs = {}
     for wm in ("1", "2"):
         for mode in ("0", "2", "3"):

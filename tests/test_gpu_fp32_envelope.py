@@ -5,8 +5,9 @@ should they be?  oracle/fp32_emul.cpp builds the same oracle with every operatio
 float: the restated algorithm evaluated at the device's precision, in the oracle's own order.  Per
 step, from the device state copied into all three, this test records |device - fp64| and
 |fp32 oracle - fp64| on the same inputs and the same actions, and asserts the device is at
-least as close to fp64 as the fp32 evaluation of the algorithm is (to sampling noise, SLACK) --
-99th and 99.9th percentiles of the positions (EE, object) and the 99th of the EE velocity.
+least as close to fp64 as the fp32 evaluation of the algorithm is -- 99th and 99.9th percentiles
+of the positions (EE, object) and the 99th of the EE velocity; only for joint-controlled ReachAO,
+where both sit at rounding level and the two distributions coincide, to sampling noise (SLACK).
 Measured (profiles/r03/fp32_envelope.log): position p99 device 2.3e-7-9.5e-7 vs fp32 oracle
 3.8e-5-5.5e-5 (ReachAO 2.4e-7), EE velocity p99 1e-5-6.5e-5 vs 1.5e-3-2.1e-3 (ReachAO 9.4e-6).  The kernels' other bars
 (test_gpu_parity.py, test_gpu_contacts.py, test_gpu_reach_ao.py) sit inside this envelope; the
@@ -35,7 +36,10 @@ def _copy_state(src, dst):
         getattr(dst, k)[:] = getattr(src, k)
 
 
-SLACK = 1.25   # sampling noise of a percentile of ~10^4 samples when the two distributions are equal
+# sampling noise of a percentile of ~10^4 samples when the two distributions are equal: ReachAO only
+# (joint control, no IK to amplify rounding: velocity p99 9.44e-6 device vs 9.42e-6 fp32 oracle,
+# profiles/r03/fp32_envelope.log); the IK tasks are held to the envelope itself (15-100x inside)
+SLACK = {"PandaReachAO-v3": 1.25}
 CASES = [("PandaReach-v3", True), ("PandaReach-v3", False), ("PandaPush-v3", True), ("PandaPickAndPlace-v3", True),
          ("PandaReachAO-v3", True)]
 
@@ -71,7 +75,6 @@ def test_device_inside_fp32_envelope(pg, oracle, env_id, contacts):
     print(f"\n{env_id} contacts={contacts}: position device p99 {q(dp, 99):.2e} p99.9 {q(dp, 99.9):.2e} "
           f"max {dp.max():.2e} | fp32 oracle p99 {q(fp, 99):.2e} p99.9 {q(fp, 99.9):.2e} max {fp.max():.2e}; "
           f"EE velocity device p99 {q(dv, 99):.2e} max {dv.max():.2e} | fp32 oracle p99 {q(fv, 99):.2e} max {fv.max():.2e}")
-    # SLACK: where both sit at rounding level (ReachAO, joint control: no IK to amplify) the two
-    # distributions coincide (velocity p99 9.44e-6 vs 9.42e-6); elsewhere the device is 15-100x inside
-    assert q(dp, 99) <= SLACK * q(fp, 99) and q(dp, 99.9) <= SLACK * q(fp, 99.9)
-    assert q(dv, 99) <= SLACK * q(fv, 99)
+    k = SLACK.get(env_id, 1.0)
+    assert q(dp, 99) <= k * q(fp, 99) and q(dp, 99.9) <= k * q(fp, 99.9)
+    assert q(dv, 99) <= k * q(fv, 99)

@@ -215,6 +215,46 @@ def test_remove_state(pg):
     env.close()
 
 
+def test_snapshot_ids_through_the_c_abi(pg):
+    """pgx_snapshot / pgx_restore / pgx_release called through ctypes (include/pgx.h): ids are the
+    first non-negative integer not in use (pybullet saveState, pybullet.py:79-86), a released id
+    is handed out again, restoring or releasing an id not in use returns PGX_E_INVALID
+    (save_and_restore_test.py:30-36: pybullet.error), and a restore brings back every state bit."""
+    import ctypes as C
+
+    import torch
+
+    from panda_gym_amd import _native
+
+    venv = pg.PandaVecEnv("PandaPush-v3", num_envs=64, device="cuda:0", seed=3)
+    lib, h, st = venv.lib, venv._h, venv._stream()
+    venv.reset_tensors()
+    before = {k: v.clone() for k, v in venv.state().items()}
+    ids = []
+    for _ in range(3):
+        sid = C.c_int32(-7)
+        assert lib.pgx_snapshot(h, C.byref(sid), st) == 0
+        ids.append(sid.value)
+    assert ids == [0, 1, 2]
+    assert lib.pgx_release(h, 1) == 0
+    assert lib.pgx_restore(h, 1, st) == _native.PGX_E_INVALID
+    assert b"no such saved state" in lib.pgx_last_error()
+    assert lib.pgx_release(h, 1) == _native.PGX_E_INVALID
+    assert lib.pgx_restore(h, 7, st) == _native.PGX_E_INVALID
+    assert lib.pgx_restore(h, -1, st) == _native.PGX_E_INVALID
+    sid = C.c_int32(-7)
+    assert lib.pgx_snapshot(h, C.byref(sid), st) == 0 and sid.value == 1   # the freed id again
+    for t in range(5):
+        venv.step_tensors(venv.sample_actions(t))
+    assert lib.pgx_restore(h, 0, st) == 0
+    torch.cuda.synchronize()
+    for k, v in venv.state().items():
+        assert torch.equal(v, before[k]), k
+    for i in (0, 1, 2):
+        assert lib.pgx_release(h, i) == 0
+    venv.close()
+
+
 def test_single_env_time_limit(pg):
     env = pg.make("PandaReach-v3", max_episode_steps=5)
     env.reset(seed=0)

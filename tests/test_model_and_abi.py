@@ -127,6 +127,8 @@ def test_constants_match_header():
     for name in ("OBJECT_POINTS", "ROBOT_POINTS", "ROBOT_POINTS_ARM", "ROBOT_POINTS_ONE_LANE"):
         assert getattr(abi, name) == define("PGX_" + name), name
     assert orc.OBJECT_POINTS == abi.OBJECT_POINTS and orc.ROBOT_MAX >= abi.ROBOT_POINTS
+    for name in ("PGX_E_INVALID", "PGX_E_HIP", "PGX_E_UNSUPPORTED", "PGX_E_NOMEM"):
+        assert getattr(abi, name) == int(re.search(rf"#define {name} (-\d+)", hdr).group(1)), name
     assert abi.AO_OBSTACLES == define("PGX_AO_OBSTACLES") and abi.MAX_CAPSULES == define("PGX_MAX_CAPSULES")
 
 

@@ -311,3 +311,28 @@ def test_obstacle_sampling_failure_is_flagged(oracle, monkeypatch):
     monkeypatch.setattr(reach_ao, "TABLE_HALF", np.array([10.0, 10.0, 10.0]))
     with pytest.raises(StopIteration, match="collision free obstacle"):
         reach_ao.seeded_reset(0, reach_ao.RobotGeometry(load_model("panda_custom0")))
+
+
+def test_collision_margin_diagnostic(oracle):
+    """pgxo_diag_collision_margin: the margin at the last substep check is <= 0 exactly on the step
+    that collides (it stops the substep loop), > 0 on every other; the smallest |margin| of the
+    colliding step is at rounding level (the contact holds the bar at the surface)."""
+    from oracle import oracle as O
+
+    cfg = _cfg(n=1)
+    env = O.OracleVecEnv(cfg, 1)
+    q0 = np.array(abi.NEUTRAL_Q[:7])
+    com, _, _ = O.fk(cfg.model.contents, q0)
+    obst = np.array([[99.9, 99.9, -99.9]] * 6)
+    obst[3] = com[11] + np.array([0.0, 0.14, -0.06])
+    env.reset(inject_goal=np.array([[0.5, 0.3, 0.3]]), inject_obj=obst[None])
+    for _ in range(30):
+        b = env.step(np.array([[1.0, 0, 0, 0, 0, 0, 0]], np.float32), margins=True)
+        assert bool(b["truncated"][0]) == bool(b["margin_last"][0] <= 0.0)
+        assert b["margin_abs"][0] <= abs(b["margin_last"][0])
+        if b["truncated"][0]:
+            assert b["margin_abs"][0] <= 1e-5
+            break
+    assert b["truncated"][0]
+    b = env.step(np.zeros((1, 7), np.float32))   # the diagnostic is off again
+    assert "margin_abs" not in b

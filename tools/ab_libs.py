@@ -6,14 +6,21 @@ import os
 import subprocess
 import sys
 
-CASES = [("PandaReach-v3", 4096, 1), ("PandaPush-v3", 4096, 1), ("PandaReachAO-v3", 8192, 1), ("PandaReach-v3", 4096, 0), ("PandaReach-v3", 8192, 1),
-         ("PandaReach-v3", 16384, 1)]
+# (env id, envs, contacts, full manifold: -1 = the library's default)
+CASES = [("PandaReach-v3", 4096, 1, -1), ("PandaPush-v3", 4096, 1, -1), ("PandaReachAO-v3", 8192, 1, -1),
+         ("PandaReach-v3", 4096, 0, -1), ("PandaReach-v3", 8192, 1, -1), ("PandaReach-v3", 16384, 1, -1)]
 CHILD = r'''
 import os, sys, json, torch
 sys.path.insert(0, os.getcwd())
+import ctypes
+from panda_gym_amd import _native
+lib = ctypes.CDLL(_native.LIB_PATH)   # an older build may lack newer exports: check the ones it has
+_native.EXPORTS = [e for e in _native.EXPORTS if hasattr(lib, e)]
 import panda_gym_amd as pg
-env_id, n, contacts = sys.argv[1], int(sys.argv[2]), bool(int(sys.argv[3]))
-kw = json.loads(os.environ.get("AB_KW", "{}"))   # e.g. AB_KW='{"full_manifold": true}'
+env_id, n, contacts, full = sys.argv[1], int(sys.argv[2]), bool(int(sys.argv[3])), int(sys.argv[4])
+kw = json.loads(os.environ.get("AB_KW", "{}"))   # e.g. AB_KW='{"lanes_per_env": 16}'
+if full >= 0:
+    kw["full_manifold"] = bool(full)
 venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=0, contacts=contacts, **kw)
 venv.reset_tensors()
 for t in range(30):
@@ -29,13 +36,25 @@ print(e0.elapsed_time(e1) / 100)
 if __name__ == "__main__":
     libs = sys.argv[1:]
     if os.environ.get("AB_CASES"):   # e.g. AB_CASES="PandaReach-v3:4096:1,PandaPush-v3:4096:1"
-        CASES = [(a, int(b), int(c)) for a, b, c in (x.split(":") for x in os.environ["AB_CASES"].split(","))]
-    res = {lib: {c[0] + str(c[1]) + ("" if c[2] else "-free"): [] for c in CASES} for lib in libs}
+        # e.g. AB_CASES="PandaReach-v3:4096:1:0,PandaPush-v3:4096:1:1" (env:envs:contacts[:full])
+        CASES = [(f[0], int(f[1]), int(f[2]), int(f[3]) if len(f) > 3 else -1)
+                 for f in (x.split(":") for x in os.environ["AB_CASES"].split(","))]
+
+    def key(env_id, n, contacts, full):
+        return env_id + str(n) + ("" if contacts else "-free") + {-1: "", 0: "-4pt", 1: "-full"}[full]
+
+    res = {lib: {key(*c): [] for c in CASES} for lib in libs}
     for rep in range(3):
         for lib in libs:
-            for env_id, n, contacts in CASES:
-                out = subprocess.run([sys.executable, "-c", CHILD, env_id, str(n), str(contacts)], capture_output=True,
-                                     text=True, env={**os.environ, "PGX_LIB": os.path.abspath(lib)}, timeout=120)
-                res[lib][env_id + str(n) + ("" if contacts else "-free")].append(float(out.stdout.strip().split()[-1]))
+            for env_id, n, contacts, full in CASES:
+                out = subprocess.run([sys.executable, "-c", CHILD, env_id, str(n), str(contacts), str(full)],
+                                     capture_output=True, text=True,
+                                     env={**os.environ, "PGX_LIB": os.path.abspath(lib)}, timeout=120)
+                try:
+                    res[lib][key(env_id, n, contacts, full)].append(float(out.stdout.strip().split()[-1]))
+                except (ValueError, IndexError):
+                    print(f"{lib} {env_id} {n}: {out.stderr[-400:]}", file=sys.stderr)
+                    res[lib][key(env_id, n, contacts, full)].append(float("nan"))
     for lib in libs:
-        print(json.dumps({"lib": os.path.basename(lib), **{k: round(sorted(v)[1], 4) for k, v in res[lib].items()}}))
+        print(json.dumps({"lib": os.path.basename(lib), **{k: round(sorted(v)[1], 4) for k, v in res[lib].items()}}),
+              flush=True)
