@@ -176,6 +176,10 @@ typedef struct pgx_sim_params {
 #define PGX_FLAG_DYN_RECURSIVE 16         /* M and b by composite rigid bodies + Newton-Euler (the
                                              kernel's formulation; same dynamics) instead of the
                                              Jacobian form: for the operation count */
+#define PGX_FLAG_PERSISTENT_MANIFOLD 32   /* robot contacts from Bullet's persistent manifolds (points
+                                             kept across substeps, refreshed, broken past 0.02,
+                                             replaced by largest area) instead of each pair's 4
+                                             deepest candidates of the substep */
 
 typedef struct pgx_config {
     int32_t task;                 /* PGX_TASK_* */

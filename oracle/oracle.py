@@ -105,7 +105,9 @@ OBJ_CACHE = 13
 OBJ_CACHE1 = OBJ_CACHE + 2 * OBJECT_POINTS
 OBJ_AO = OBJ_CACHE1 + 2 * ROBOT_MAX   # ReachAO: obstacle centres [6][3], active flags [6] at OBJ_AO + 18
 OBJ_QC = OBJ_AO + 24
-OBJ_N = OBJ_QC + 7
+MAN, MAN_PT = 16, 11          # PGX_FLAG_PERSISTENT_MANIFOLD: manifolds per env, doubles per point
+OBJ_MAN = OBJ_QC + 7          # [MAN][key + 1, count, 4 x (local A, local B, normal, distance, impulse)]
+OBJ_N = OBJ_MAN + MAN * (2 + 4 * MAN_PT)
 ROBOT_HIST = 33
 
 
@@ -131,6 +133,28 @@ def last_contacts():
     d = np.zeros(m)
     n = lib().pgxo_last_contacts(*(a.ctypes.data_as(C.c_void_p) for a in (g, i, l, d)))
     return g[:n], i[:n], l[:n], d[:n]
+
+
+def manifold_add(M: np.ndarray, point: np.ndarray, thr: float = 0.02) -> int:
+    """btPersistentManifold addContactPoint on one manifold M [2 + 4 * MAN_PT] (in place); the slot."""
+    lib().pgxo_manifold_add.argtypes = [C.c_void_p, C.c_void_p, C.c_double]
+    return int(lib().pgxo_manifold_add(_p(M), _p(_d(point)), thr))
+
+
+def manifold_refresh_static(M: np.ndarray, thr: float = 0.02) -> None:
+    """refreshContactPoints of one manifold whose bodies did not move (local = world), in place."""
+    lib().pgxo_manifold_refresh_static.argtypes = [C.c_void_p, C.c_double]
+    lib().pgxo_manifold_refresh_static(_p(M), thr)
+
+
+def manifolds(obj_row: np.ndarray) -> list:
+    """The persistent manifolds of one env's obj row: [(key, points [n, MAN_PT])]."""
+    out = []
+    for mi in range(MAN):
+        M = obj_row[OBJ_MAN + mi * (2 + 4 * MAN_PT):OBJ_MAN + (mi + 1) * (2 + 4 * MAN_PT)]
+        if M[0] != 0:
+            out.append((int(M[0]) - 1, M[2:2 + int(M[1]) * MAN_PT].reshape(-1, MAN_PT).copy()))
+    return out
 
 
 def set_contact_cache(obj: np.ndarray, cache: np.ndarray) -> None:

@@ -514,7 +514,13 @@ static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x >
 #define OBJ_CACHE1 (OBJ_CACHE + 2 * PGX_OBJECT_POINTS)
 #define OBJ_AO (OBJ_CACHE1 + 2 * PGXO_ROBOT_MAX)
 #define OBJ_QC (OBJ_AO + 4 * PGX_AO_OBSTACLES)
-#define OBJ_N (OBJ_QC + 7)
+/* PGX_FLAG_PERSISTENT_MANIFOLD: the robot pairs' persistent manifolds, PGXO_MAN x (key + 1 (0 =
+ * free), point count, MANIFOLD_CACHE_SIZE x point: local A [3], local B [3], normal on B [3],
+ * distance, applied normal impulse) */
+#define MAN_PT 11
+#define MAN_SZ (2 + 4 * MAN_PT)
+#define OBJ_MAN (OBJ_QC + 7)
+#define OBJ_N (OBJ_MAN + PGXO_MAN * MAN_SZ)
 #define N_CACHE (PGX_OBJECT_POINTS + PGXO_ROBOT_MAX)
 typedef char obj_layout_check[(OBJ_N == PGXO_OBJ_N) ? 1 : -1];
 static void quat_mul(const double* a, const double* b, double* o);
@@ -543,6 +549,8 @@ int pgxo_last_contacts(int32_t* grp, int32_t* id, int32_t* link, double* dist) {
 typedef struct {
     int grp, id, link;
     double n[3], pa[3], pb[3], dist;
+    double* mp;   /* persistent mode: the manifold point the solved impulse goes back to, else NULL */
+    double imp;   /* persistent mode: the point's applied impulse (warm start) */
 } contact_t;
 
 typedef struct {
@@ -619,9 +627,179 @@ static int capsule_samples(const double* a, const double* b, double r) {
     return (int)ceil(len / (0.5 * r) - 1e-9) + 1;
 }
 
-/* contact detection; returns the number of contacts (grouped, each group sorted by id) */
 enum { PAIR_TABLE = 0, PAIR_PLANE = 1, PAIR_CUBE = 2, PAIR_OBSTACLE = 3 };   /* + 16 x capsule */
-static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W, const kin_t* k, const double* obj,
+/* ---- Bullet's persistent contact manifold (oracle flag PGX_FLAG_PERSISTENT_MANIFOLD): the
+ * robot pairs' points persist across substeps.  Restated from btPersistentManifold /
+ * btManifoldResult (Bullet 3, the algorithm pybullet 3.2.6 runs; not vendored): per colliding
+ * pair (a capsule's end sphere against the table or the plane -- each sphere is a child shape of
+ * the link compound with a manifold of its own --, the capsule against the cube or an obstacle)
+ * the narrow phase reports one new point per stepSimulation (a sphere's closest point; for the
+ * convex capsule vs a box GJK's closest pair, restated as the deepest sample), which
+ * addContactPoint either merges into the cached point nearest to it within the breaking
+ * threshold in A's local frame (getCacheEntry: the new point replaces it and keeps its applied
+ * impulse) or appends -- with 4 points cached, sortCachedPoints replaces the one whose removal
+ * leaves the largest area, never the deepest -- then refreshContactPoints moves every cached
+ * point with its bodies (local -> world), recomputes its distance along the stored normal and
+ * drops it past the breaking threshold (0.02) or when it slid more than that sideways.  Every
+ * manifold point is a solver row; its normal impulse is written back and warm-starts it in the
+ * next substep (x 0.85). */
+static void man_world(const kin_t* k, const double* obj, int li, int code, const double* P, double* pa, double* pb) {
+    m3_v(k->R[li], P, pa);
+    for (int i = 0; i < 3; i++) pa[i] += k->o[li][i];
+    if (code == 4) {   /* cube: B's local frame moves with it */
+        double Rc[9];
+        quat_to_mat(obj + 3, Rc);
+        m3_v(Rc, P + 3, pb);
+        for (int i = 0; i < 3; i++) pb[i] += obj[i];
+    } else {           /* table / plane / obstacle: static, local = world */
+        memcpy(pb, P + 3, 3 * sizeof(double));
+    }
+}
+static int man_sort_cached(const double* M, const double* np) {   /* btPersistentManifold::sortCachedPoints */
+    const double* c[4];
+    for (int i = 0; i < 4; i++) c[i] = M + 2 + MAN_PT * i;
+    int maxi = -1;
+    double maxpen = np[9];
+    for (int i = 0; i < 4; i++)
+        if (c[i][9] < maxpen) { maxi = i; maxpen = c[i][9]; }
+    double res[4] = {0, 0, 0, 0};
+    static const int ia[4] = {1, 0, 0, 0}, ib[4] = {3, 3, 3, 2}, ic[4] = {2, 2, 1, 1};
+    for (int i = 0; i < 4; i++) {
+        if (i == maxi) continue;
+        double a[3], b[3], x[3];
+        for (int j = 0; j < 3; j++) { a[j] = np[j] - c[ia[i]][j]; b[j] = c[ib[i]][j] - c[ic[i]][j]; }
+        v3_cross(a, b, x);
+        res[i] = v3_dot(x, x);
+    }
+    int best = 0;
+    for (int i = 1; i < 4; i++)
+        if (res[i] > res[best]) best = i;
+    return best;
+}
+/* addContactPoint: merge into the cached point nearest in A's local frame within the breaking
+ * threshold (getCacheEntry; replaceContactPoint keeps its applied impulse), else append, else
+ * (4 cached) replace by sortCachedPoints; returns the slot.  M = (key + 1, count, points). */
+static int man_add(double* M, const double* np, double thr2) {
+    const int n = (int)M[1];
+    int near = -1;
+    double sh = thr2;
+    for (int i = 0; i < n; i++) {   /* getCacheEntry */
+        const double* P = M + 2 + MAN_PT * i;
+        double e[3] = {P[0] - np[0], P[1] - np[1], P[2] - np[2]};
+        const double dd = v3_dot(e, e);
+        if (dd < sh) { sh = dd; near = i; }
+    }
+    if (near >= 0) {           /* replaceContactPoint: the cached impulse stays */
+        double* P = M + 2 + MAN_PT * near;
+        const double imp = P[10];
+        memcpy(P, np, MAN_PT * sizeof(double));
+        P[10] = imp;
+        return near;
+    }
+    if (n < 4) {
+        memcpy(M + 2 + MAN_PT * n, np, MAN_PT * sizeof(double));
+        M[1] = n + 1;
+        return n;
+    }
+    const int slot = man_sort_cached(M, np);
+    memcpy(M + 2 + MAN_PT * slot, np, MAN_PT * sizeof(double));
+    return slot;
+}
+/* refreshContactPoints with the cached points' world positions pa, pb: distance along the
+ * stored normal, then (in reverse order) drop a point past the breaking threshold or one whose
+ * B point slid more than it sideways off A's (removeContactPoint: the last point fills the hole) */
+static void man_refresh(double* M, const double (*pa)[3], const double (*pb)[3], double thr) {
+    int n = (int)M[1];
+    double wa[4][3], wb[4][3];
+    for (int i = 0; i < n; i++) {
+        double* P = M + 2 + MAN_PT * i;
+        memcpy(wa[i], pa[i], sizeof wa[i]);
+        memcpy(wb[i], pb[i], sizeof wb[i]);
+        P[9] = (pa[i][0] - pb[i][0]) * P[6] + (pa[i][1] - pb[i][1]) * P[7] + (pa[i][2] - pb[i][2]) * P[8];
+    }
+    for (int i = n - 1; i >= 0; i--) {
+        double* P = M + 2 + MAN_PT * i;
+        int drop = P[9] > thr;
+        if (!drop) {
+            double e[3];
+            for (int j = 0; j < 3; j++) e[j] = wb[i][j] - (wa[i][j] - P[6 + j] * P[9]);
+            drop = v3_dot(e, e) > thr * thr;
+        }
+        if (drop) {
+            if (i != n - 1) {
+                memcpy(P, M + 2 + MAN_PT * (n - 1), MAN_PT * sizeof(double));
+                memcpy(wa[i], wa[n - 1], sizeof wa[i]);
+                memcpy(wb[i], wb[n - 1], sizeof wb[i]);
+            }
+            n--;
+        }
+    }
+    M[1] = n;
+}
+/* test entry points: one manifold whose bodies do not move (local = world) */
+int pgxo_manifold_add(double* M, const double* point, double thr) { return man_add(M, point, thr * thr); }
+void pgxo_manifold_refresh_static(double* M, double thr) {
+    double pa[4][3], pb[4][3];
+    for (int i = 0; i < (int)M[1]; i++)
+        for (int j = 0; j < 3; j++) { pa[i][j] = M[2 + MAN_PT * i + j]; pb[i][j] = M[2 + MAN_PT * i + 3 + j]; }
+    man_refresh(M, pa, pb, thr);
+}
+static void persistent_manifolds(const pgx_model* m, const pgx_sim_params* p, const kin_t* k, double* obj,
+                                 const cands_t* s1) {
+    const double thr = p->contact_distance, thr2 = thr * thr;
+    double* man = obj + OBJ_MAN;
+    /* 1. the pairs' new points: per pair its deepest candidate (the first on a tie) */
+    int nk = 0, keys[CAND_MAX], best[CAND_MAX];
+    for (int i = 0; i < s1->n; i++) {
+        const int ci = s1->pair[i] >> 4, code = s1->pair[i] & 15;
+        const int key = (code == PAIR_TABLE || code == PAIR_PLANE) ? ci * 32 + 2 * code + (s1->c[i].id & 1)
+                      : code == PAIR_CUBE ? ci * 32 + 4 : ci * 32 + 8 + (code - PAIR_OBSTACLE);
+        int j = 0;
+        while (j < nk && keys[j] != key) j++;
+        if (j == nk) { keys[nk] = key; best[nk] = i; nk++; }
+        else if (s1->c[i].dist < s1->c[best[j]].dist) best[j] = i;
+    }
+    /* 2. addContactPoint: merge into the nearest cached point or add */
+    for (int j = 0; j < nk; j++) {
+        const contact_t* c = &s1->c[best[j]];
+        const int key = keys[j], code = key & 31, li = c->link;
+        double* M = NULL;
+        for (int mi = 0; mi < PGXO_MAN && !M; mi++)
+            if ((int)man[MAN_SZ * mi] == key + 1) M = man + MAN_SZ * mi;
+        for (int mi = 0; mi < PGXO_MAN && !M; mi++)
+            if (man[MAN_SZ * mi] == 0.0) { M = man + MAN_SZ * mi; M[0] = key + 1; M[1] = 0; }
+        if (!M) continue;   /* (more pairs than PGXO_MAN: not reached in the configs) */
+        double np[MAN_PT], d[3];
+        for (int i = 0; i < 3; i++) d[i] = c->pa[i] - k->o[li][i];
+        for (int i = 0; i < 3; i++) np[i] = k->R[li][i] * d[0] + k->R[li][3 + i] * d[1] + k->R[li][6 + i] * d[2];
+        if (code == 4) {
+            double Rc[9], e[3] = {c->pb[0] - obj[0], c->pb[1] - obj[1], c->pb[2] - obj[2]};
+            quat_to_mat(obj + 3, Rc);
+            for (int i = 0; i < 3; i++) np[3 + i] = Rc[i] * e[0] + Rc[3 + i] * e[1] + Rc[6 + i] * e[2];
+        } else {
+            memcpy(np + 3, c->pb, 3 * sizeof(double));
+        }
+        memcpy(np + 6, c->n, 3 * sizeof(double));
+        np[9] = c->dist;
+        np[10] = 0.0;
+        man_add(M, np, thr2);
+    }
+    /* 3. refreshContactPoints: move the points with their bodies, drop the broken ones */
+    for (int mi = 0; mi < PGXO_MAN; mi++) {
+        double* M = man + MAN_SZ * mi;
+        if (M[0] == 0.0) continue;
+        const int key = (int)M[0] - 1, code = key & 31;
+        int n = (int)M[1];
+        const int li = m->cap_link[key >> 5];
+        double pa[4][3], pb[4][3];
+        for (int i = 0; i < n; i++) man_world(k, obj, li, code, M + 2 + MAN_PT * i, pa[i], pb[i]);
+        man_refresh(M, pa, pb, thr);
+        if (M[1] == 0.0) M[0] = 0.0;   /* (a manifold without points: the slot is free again) */
+    }
+}
+
+/* contact detection; returns the number of contacts (grouped, each group sorted by id) */
+static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W, const kin_t* k, double* obj,
                   contact_t* out) {
     const double tau = p->contact_distance;
     static cands_t s0, s1;   /* single-threaded checker */
@@ -637,7 +815,7 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
             double zt = ground_z(W, P);
             double d = P[2] - zt;
             if (d < tau) {
-                contact_t c = {0, v, -1, {0, 0, 1}, {P[0], P[1], P[2]}, {P[0], P[1], zt}, d};
+                contact_t c = {0, v, -1, {0, 0, 1}, {P[0], P[1], P[2]}, {P[0], P[1], zt}, d, NULL, 0.0};
                 cand_add(&s0, &c, zt == W->plane_z ? PAIR_PLANE : PAIR_TABLE);
             }
         }
@@ -658,7 +836,7 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
                 double zt = ground_z(W, P);
                 double d = P[2] - r - zt;
                 if (d < tau) {
-                    contact_t c = {1, 2 * ci + e, li, {0, 0, 1}, {P[0], P[1], P[2] - r}, {P[0], P[1], zt}, d};
+                    contact_t c = {1, 2 * ci + e, li, {0, 0, 1}, {P[0], P[1], P[2] - r}, {P[0], P[1], zt}, d, NULL, 0.0};
                     cand_add(&s1, &c, 16 * ci + (zt == W->plane_z ? PAIR_PLANE : PAIR_TABLE));
                 }
             }
@@ -691,6 +869,7 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
                 if (depth < tau) {
                     contact_t c;
                     c.grp = 2; c.id = 32 + ci * 16 + s; c.link = li; c.dist = depth;
+                    c.mp = NULL; c.imp = 0.0;
                     m3_v(Rc, nl, c.n);
                     m3_v(Rc, qb, c.pb);
                     for (int i = 0; i < 3; i++) { c.pb[i] += obj[i]; c.pa[i] = C[i] - r * c.n[i]; }
@@ -711,7 +890,7 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
                 const cdist_t cd = ao_capsule_obstacle(A, B, r, o, W->obst);
                 if (cd.d < tau) {
                     contact_t c = {1, 32 + 6 * ci + o, li, {-cd.n[0], -cd.n[1], -cd.n[2]},
-                                   {cd.pa[0], cd.pa[1], cd.pa[2]}, {cd.pb[0], cd.pb[1], cd.pb[2]}, cd.d};
+                                   {cd.pa[0], cd.pa[1], cd.pa[2]}, {cd.pb[0], cd.pb[1], cd.pb[2]}, cd.d, NULL, 0.0};
                     cand_add(&s1, &c, 16 * ci + PAIR_OBSTACLE + o);
                 }
             }
@@ -720,6 +899,30 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
     int np1;
     const int n0 = select_points(&s0, PGX_OBJECT_POINTS, out, NULL);
     const int budget = robot_budget >= 0 ? robot_budget : W->robot_points;
+    if (p->flags & PGX_FLAG_PERSISTENT_MANIFOLD) {   /* the robot group from the persistent manifolds */
+        persistent_manifolds(m, p, k, obj, &s1);
+        cands_t* sm = &s1;   /* reuse: the manifold points as the group's candidates */
+        sm->n = 0;
+        double* man = obj + OBJ_MAN;
+        for (int mi = 0; mi < PGXO_MAN; mi++) {
+            double* M = man + MAN_SZ * mi;
+            if (M[0] == 0.0) continue;
+            const int key = (int)M[0] - 1, ci = key >> 5, code = key & 31, li = m->cap_link[ci];
+            for (int sl = 0; sl < (int)M[1]; sl++) {
+                double* P = M + 2 + MAN_PT * sl;
+                contact_t c;
+                c.grp = code == 4 ? 2 : 1;
+                c.id = 4 * key + sl;
+                c.link = li;
+                man_world(k, obj, li, code, P, c.pa, c.pb);
+                memcpy(c.n, P + 6, sizeof c.n);
+                c.dist = P[9];
+                c.mp = P;
+                c.imp = P[10];
+                cand_add(sm, &c, mi);   /* each manifold its own pair (<= 4 points already) */
+            }
+        }
+    }
     const int n1 = select_points(&s1, budget, out + n0, &np1);
     pgxo_pair_hist[np1 < PGXO_ROBOT_HIST - 1 ? np1 : PGXO_ROBOT_HIST - 1]++;
     sort_by_id(out, n0);
@@ -893,10 +1096,13 @@ static void substep_impl(const pgx_model* m, const pgx_sim_params* p, const doub
                 R->rhs = (perr + verr) * R->jinv;
                 R->lo = 0.0;
                 R->hi = 1e10;
-                /* warm start from the same feature's impulse of the previous step */
+                /* warm start from the same feature's impulse of the previous step (persistent
+                 * manifold: the point's own applied impulse) */
                 const double* cache = obj + (ct->grp != 0 ? OBJ_CACHE1 : OBJ_CACHE);
-                for (int s = 0; s < (ct->grp != 0 ? PGXO_ROBOT_MAX : PGX_OBJECT_POINTS); s++)
-                    if ((int)cache[2 * s] == ct->id) R->lam = p->warmstart * cache[2 * s + 1];
+                if (ct->mp) R->lam = p->warmstart * ct->imp;
+                else
+                    for (int s = 0; s < (ct->grp != 0 ? PGXO_ROBOT_MAX : PGX_OBJECT_POINTS); s++)
+                        if ((int)cache[2 * s] == ct->id) R->lam = p->warmstart * cache[2 * s + 1];
                 if (R->lam != 0.0) {
                     for (int d = 0; d < nd; d++) dv[d] += R->Rr[d] * R->lam;
                     for (int i = 0; i < 6; i++) dvc[i] += R->Rc[i] * R->lam;
@@ -978,6 +1184,8 @@ static void substep_impl(const pgx_model* m, const pgx_sim_params* p, const doub
         qd[d] = vn[d];
         q[d] += dt * vn[d];
     }
+    for (int c = 0; c < ncon; c++)   /* persistent manifold: the applied impulse back to its point */
+        if (con[c].mp) con[c].mp[10] = cr[3 * c].lam;
     if (W) { /* contact cache: this step's features and normal impulses, per group */
         double* cache = obj + OBJ_CACHE;
         for (int s = 0; s < N_CACHE; s++) { cache[2 * s] = -1.0; cache[2 * s + 1] = 0.0; }
@@ -1338,6 +1546,7 @@ static void reset_one(const pgx_config* c, int64_t e, const double* inject_goal,
     if (obj) {
         for (int s = 0; s < N_CACHE; s++) { obj[OBJ_CACHE + 2 * s] = -1.0; obj[OBJ_CACHE + 2 * s + 1] = 0.0; }
         memcpy(obj + OBJ_QC, q, 7 * sizeof(double));   /* resetJointState refreshes the link cache */
+        memset(obj + OBJ_MAN, 0, PGXO_MAN * MAN_SZ * sizeof(double));   /* (resetBasePosition... clears them) */
     }
     *elapsed = 0;
     *episode += 1;
@@ -1698,6 +1907,7 @@ static void ao_reset_one(const pgx_config* c, int64_t e, const double* inject_go
         }
     for (int s = 0; s < N_CACHE; s++) { obj[OBJ_CACHE + 2 * s] = -1.0; obj[OBJ_CACHE + 2 * s + 1] = 0.0; }
     memcpy(obj + OBJ_QC, q, 7 * sizeof(double));
+    memset(obj + OBJ_MAN, 0, PGXO_MAN * MAN_SZ * sizeof(double));
     *elapsed = 0;
     *episode += 1;
 }

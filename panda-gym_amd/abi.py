@@ -36,6 +36,7 @@ FLAG_IK_COM = 2
 FLAG_NO_RESIDUAL_EXIT = 4
 FLAG_LINKSTATE_CURRENT = 8   # getLinkState at the pose after the last substep (rejected hypothesis)
 FLAG_DYN_RECURSIVE = 16      # oracle: M, b by CRBA + Newton-Euler (the kernel's formulation), for the op count
+FLAG_PERSISTENT_MANIFOLD = 32  # oracle: Bullet's persistent contact manifolds for the robot pairs (study mode)
 
 HER_FUTURE, HER_FINAL, HER_EPISODE = 0, 1, 2
 

@@ -215,3 +215,79 @@ def test_link_on_cube_keeps_all_points_per_pair_cap(oracle):
     cfg.contacts = 1
     pts4, _ = _detect(oracle, cfg, q, _obj(tuple(ee)))
     assert len(_robot(pts4)[0]) == 4
+
+
+# ---------------------------------------------------------------- persistent manifold (study mode)
+# PGX_FLAG_PERSISTENT_MANIFOLD restates Bullet's btPersistentManifold for the robot pairs (oracle
+# only; DESIGN.md section 2 records how far it moves Push / PickAndPlace from the default rule).
+def _pt(a, dist, normal=(0.0, 0.0, 1.0), imp=0.0):
+    a, n = np.asarray(a, float), np.asarray(normal, float)
+    return np.concatenate([a, a - n * dist, n, [dist, imp]])
+
+
+def _man(oracle):
+    M = np.zeros(2 + 4 * oracle.MAN_PT)
+    M[0] = 1.0
+    return M
+
+
+def test_manifold_merges_appends_and_replaces_by_area(oracle):
+    M = _man(oracle)
+    assert oracle.manifold_add(M, _pt((0, 0, 0), -0.003)) == 0 and M[1] == 1
+    M[2 + 10] = 5.0                                            # the solver wrote an impulse back
+    # within the breaking threshold (0.02) of the cached point in A's frame: replaces it, impulse kept
+    assert oracle.manifold_add(M, _pt((0.01, 0, 0), -0.002)) == 0 and M[1] == 1
+    assert M[2 + 10] == 5.0 and M[2] == 0.01
+    for a in ((0.05, 0, 0), (0, 0.05, 0), (0.05, 0.05, 0)):   # farther apart: appended
+        oracle.manifold_add(M, _pt(a, -0.001))
+    assert M[1] == 4
+    P = M[2:].reshape(4, -1)
+    # a fifth point: sortCachedPoints -- never the deepest (slot 0), else the largest remaining area
+    new = _pt((0.1, 0.1, 0), -0.0005)
+    res = []
+    for i, (ia, ib, ic) in enumerate(((1, 3, 2), (0, 3, 2), (0, 3, 1), (0, 2, 1))):
+        x = np.cross(new[:3] - P[ia, :3], P[ib, :3] - P[ic, :3])
+        res.append(0.0 if i == 0 else float(x @ x))
+    want = int(np.argmax(res))
+    assert want != 0 and oracle.manifold_add(M, new) == want and M[1] == 4
+    assert np.array_equal(M[2:].reshape(4, -1)[want], new)
+
+
+def test_manifold_refresh_breaks_points(oracle):
+    M = _man(oracle)
+    for a in ((0, 0, 0), (0.05, 0, 0), (0, 0.05, 0)):
+        oracle.manifold_add(M, _pt(a, -0.001))
+    P = M[2:].reshape(4, -1)
+    P[1, 3:6] = P[1, 0:3] - np.array([0, 0, 0.03])              # B point 0.03 below A: separated past 0.02
+    P[2, 3:6] = P[2, 0:3] + np.array([0.03, 0, 0.001])          # slid 0.03 sideways
+    oracle.manifold_refresh_static(M)
+    assert M[1] == 1 and np.allclose(M[2:5], 0.0) and abs(M[2 + 9] - (-0.001)) < 1e-15
+
+
+def test_persistent_manifold_builds_over_substeps(oracle):
+    """The cube at the closed fingertips (test_link_on_cube_keeps_all_points_per_pair_cap): the
+    default rule gives each colliding capsule its 4 deepest samples at once; Bullet's manifold
+    starts from the pair's one closest point and gains at most one point per pair per substep,
+    never more than 4."""
+    from oracle import oracle as orc
+
+    cfg = _cfg(task=abi.TASK_PUSH)
+    cfg.contacts = abi.CONTACTS_FULL
+    env = oracle.OracleVecEnv(cfg, 1)
+    env.reset()
+    ee = env.step(np.zeros((1, 3)))["obs"][0, :3]
+    q0 = env.q[0].copy()
+    cfgp = _cfg(task=abi.TASK_PUSH)
+    cfgp.contacts = abi.CONTACTS_FULL
+    cfgp.params.contents.flags = abi.FLAG_PERSISTENT_MANIFOLD
+    q, qd, obj, mot = q0.copy(), np.zeros(7), _obj(tuple(ee)), _motors(oracle, q0)
+    counts = []
+    for t in range(12):
+        q, qd, obj, _ = oracle.world_substep(cfgp, q, qd, obj, mot)
+        cube = {key: len(pts) for key, pts in orc.manifolds(obj) if key & 31 == 4}
+        counts.append(cube)
+    assert counts[0] and all(v == 1 for v in counts[0].values())      # one closest point per pair first
+    for a, b in zip(counts, counts[1:]):
+        for key, v in b.items():
+            assert v <= a.get(key, 0) + 1 and v <= 4
+    assert max(max(c.values(), default=0) for c in counts) >= 2       # and it builds up
