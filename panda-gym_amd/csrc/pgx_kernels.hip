@@ -775,6 +775,10 @@ struct ContactLdsT {
      * double-buffered: getLinkState's cached pose is the last completed substep's start) */
     float ltq[W == 64 ? 1 : PGX_NJ][W], lqs[W == 64 ? 1 : 2][W == 64 ? 1 : PGX_NJ][W];
     float lkc[W == 64 ? 1 : 16][W == 64 ? 1 : 16];   /* the lane constants (LaneK fields x lane c) */
+    /* wide layout: what waits for the end of the constraint solve -- q, the unconstrained joint
+     * velocities vu, the object's position and orientation and its unconstrained velocities
+     * (27 floats, row-uniform) -- parked through the sweeps (PARK_SOLVE) */
+    float psv[W == 64 ? 1 : 27][W == 64 ? 1 : W];
     /* one-lane speculative solve: the sweep's start velocities (dv, dvl, dvw) for a redo */
     float spec0[W == 64 ? NJ + 6 : 1][W == 64 ? W : 1];
 };
@@ -2241,8 +2245,10 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     }
     const V3 (&z)[NJ] = D.z;
     const V3 (&o)[NJ] = D.o;
-    const float (&vu)[NJ] = D.vu;
-    const V3 vcu = D.vcu, wcu = D.wcu;
+    float vu[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; j++) vu[j] = D.vu[j];
+    V3 vcu = D.vcu, wcu = D.wcu;
     PGX_PROF_MARK(2);
     const bool arm = c < NJ;
     const float inv_m = e.obj_inv_mass, inv_i = e.obj_inv_inertia;
@@ -3008,6 +3014,30 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             solve(mode_c, IC<-1>{}, k_c, IC<0>{});
         }
     };
+    /* PARK_SOLVE: the state read only after the solve waits in LDS through the sweeps (relaxed
+     * atomics: neither kept in registers nor hoisted) -- 27 registers fewer at the sweeps' peak,
+     * where the two-waves-per-SIMD object kernel spills to scratch */
+#ifndef PGX_NO_PARK_SOLVE
+    constexpr bool PARK_SOLVE = CONT && (OBJ || AO || PART == 2);
+#else
+    constexpr bool PARK_SOLVE = false;
+#endif
+    auto park = [&](int k, float v) __attribute__((always_inline)) {
+        __hip_atomic_store(&Lp->psv[k][es], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    };
+    auto unpark = [&](int k) __attribute__((always_inline)) {
+        return __hip_atomic_load(&Lp->psv[k][es], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    };
+    if constexpr (PARK_SOLVE) {
+#pragma unroll
+        for (int j = 0; j < NJ; j++) { park(j, q[j]); park(NJ + j, vu[j]); }
+        if constexpr (OBJ) {
+            park(14, ob.p.x); park(15, ob.p.y); park(16, ob.p.z);
+            park(17, ob.qx); park(18, ob.qy); park(19, ob.qz); park(20, ob.qw);
+            park(21, vcu.x); park(22, vcu.y); park(23, vcu.z);
+            park(24, wcu.x); park(25, wcu.y); park(26, wcu.z);
+        }
+    }
     if (__all(far)) {   /* (far implies no robot point in the wave) */
         solve(IC<0>{}, IC<0>{}, IC<0>{}, IC<0>{});
     } else {
@@ -3118,6 +3148,16 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     PGX_PROF_SWEEPS_DONE();
     PGX_PROF_MARK(4);
     PGX_PROF_COUNT(11, any_contact ? 1 : 0);
+    if constexpr (PARK_SOLVE) {
+#pragma unroll
+        for (int j = 0; j < NJ; j++) { q[j] = unpark(j); vu[j] = unpark(NJ + j); }
+        if constexpr (OBJ) {
+            ob.p = v3(unpark(14), unpark(15), unpark(16));
+            ob.qx = unpark(17); ob.qy = unpark(18); ob.qz = unpark(19); ob.qw = unpark(20);
+            vcu = v3(unpark(21), unpark(22), unpark(23));
+            wcu = v3(unpark(24), unpark(25), unpark(26));
+        }
+    }
     sfor<0, NJ>([&](auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
         const float vn = fminf(fmaxf(vu[j] + bcast16<j>(gv), -m.max_vel), m.max_vel);

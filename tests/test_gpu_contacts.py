@@ -76,8 +76,11 @@ def _one_step_errors(pg, oracle, env_id, n, steps, seed, actions=None, lanes=0, 
         _state_to_oracle(venv, ref)
         saved = (ref.q.copy(), ref.qd.copy(), ref.goal.copy(), ref.obj.copy(), ref.elapsed.copy(),
                  ref.episode.copy())
-        a = venv.sample_actions(t).clone() if actions is None else torch.as_tensor(
-            np.repeat(np.asarray(actions[t], np.float32)[None], n, 0), device="cuda:0")
+        if actions is None:
+            a = venv.sample_actions(t).clone()
+        else:   # one action for every env, or one per env
+            at = np.asarray(actions[t], np.float32)
+            a = torch.as_tensor(at if at.ndim == 2 else np.repeat(at[None], n, 0), device="cuda:0")
         venv.step_tensors(a)
         out = ref.step(a.cpu().numpy())
         obs, ag, dg = _obs(venv)
@@ -126,9 +129,15 @@ def _self_sensitivity(oracle, cfg, rec, trials=16, rel=1e-7, seed=0):
 
 
 def test_reach_with_table_contacts(pg, oracle, lanes):
-    """Drive the EE into the table (a = -z): the tool-bar contact holds it at z ~ 0.042."""
-    acts = [[0.3, -0.2, -1.0]] * 30
-    ee, ag, _ = _one_step_errors(pg, oracle, "PandaReach-v3", 64, 30, 3, acts, lanes=lanes)
+    """Drive the EE into the table (a = -z, each env with its own small lateral offset, so the 64
+    envs are 64 samples per step): the tool-bar contact holds it at z ~ 0.042."""
+    rng = np.random.default_rng(3)
+    off = rng.uniform(-0.2, 0.2, (64, 3)).astype(np.float32)
+    off[:, 2] = 0.0
+    acts = [np.clip(np.array([0.3, -0.2, -1.0], np.float32) + off, -1, 1)] * 30
+    outl = []
+    ee, ag, _ = _one_step_errors(pg, oracle, "PandaReach-v3", 64, 30, 3, acts, lanes=lanes, outliers=outl)
+    print(f"\ntable contacts: EE error p99 {np.percentile(ee, 99):.2e} max {ee.max():.2e}")
     assert np.percentile(ee, 99) <= 1e-5 and ee.max() <= 1e-3, (np.percentile(ee, 99), ee.max())
     venv = pg.PandaVecEnv("PandaReach-v3", num_envs=64, device="cuda:0", seed=3, lanes_per_env=lanes)
     venv.reset_tensors(seed=3)
@@ -240,9 +249,11 @@ def test_push_large_batch_properties(pg):
 def test_layouts_agree_per_step(pg, env_id):
     """The 16-lane and the one-lane kernels restate the same step; from the same state (copied
     through the state views) one random-policy step agrees to fp32 rounding (summation order
-    of the row reductions, scaled row units).  Per step, as in the oracle parity above."""
+    of the row reductions, scaled row units).  Per step, as in the oracle parity above.  Both at
+    the one-lane layout's robot budget (4 points): the 16-lane default keeps Bullet's per-pair
+    manifolds up to 8 / 12 points, which the one-lane kernels do not hold."""
     n = 512
-    a = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=4, lanes_per_env=16)
+    a = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=4, lanes_per_env=16, full_manifold=False)
     b = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=4, lanes_per_env=1)
     a.reset_tensors(seed=4)
     errs = []
