@@ -1002,6 +1002,77 @@ __device__ __forceinline__ void object_candidates(const PgxDevEnv& e, float tau,
     }
 }
 
+/* object_candidates in the wide layout, lane-parallel: capsule cn (wave-uniform) against the
+ * object, lane s of the env's row evaluating sample s (<= 13 per capsule) -- one pass instead of
+ * every lane walking every sample twice.  The same candidates and order: Bullet's manifold rule
+ * keeps the pair's MANIFOLD deepest by (depth, sample), ranked by broadcast; they are inserted
+ * (g1_insert) in sample order, every lane of the env reading the candidate lane's values.
+ * env_near: this env's cull (robot_contacts' segment test) passed for the capsule. */
+template <class LT>
+__device__ __forceinline__ void object_candidates_g(const PgxDevEnv& e, float tau, LT& L, int es, const ObjState& ob,
+                                                    const M3& Rc, int cn, int c, bool env_near) {
+    static_assert(PGX_NCAP <= 16, "capsule table");
+    const V3 A = lds3(L.capA[cn], es), B = lds3(L.capB[cn], es);
+    const float r = kCapR[cn];
+    const int jc = kCapJ[cn], ns = kCapNs[cn];
+    const float h = e.obj_half;
+    const V3 ab = B - A;
+    const float inv_n = ns > 1 ? 1.0f / (float)(ns - 1) : 0.0f;
+    const V3 C = A + ((float)c * inv_n) * ab;
+    const V3 cl = mul_t(Rc, C - ob.p);
+    V3 qb = v3(fminf(fmaxf(cl.x, -h), h), fminf(fmaxf(cl.y, -h), h), fminf(fmaxf(cl.z, -h), h));
+    const V3 diff = cl - qb;
+    const float d2 = dot(diff, diff);
+    V3 nl;
+    float depth;
+    if (d2 > 1e-24f) {
+        const float dist = fast_sqrt(d2);
+        nl = fast_rcp(dist) * diff;
+        depth = dist - r;
+    } else { /* centre inside the box: out through the nearest face */
+        const float bx = h - fabsf(cl.x), by = h - fabsf(cl.y), bz = h - fabsf(cl.z);
+        int ax = 0;
+        float best = bx;
+        if (by < best) { best = by; ax = 1; }
+        if (bz < best) { best = bz; ax = 2; }
+        const float sx = cl.x < 0.0f ? -1.0f : 1.0f, sy = cl.y < 0.0f ? -1.0f : 1.0f, sz = cl.z < 0.0f ? -1.0f : 1.0f;
+        nl = v3(ax == 0 ? sx : 0.0f, ax == 1 ? sy : 0.0f, ax == 2 ? sz : 0.0f);
+        if (ax == 0) qb.x = sx * h;
+        if (ax == 1) qb.y = sy * h;
+        if (ax == 2) qb.z = sz * h;
+        depth = -best - r;
+    }
+    const bool cand = env_near && c < ns && depth < tau;
+    bool keep = cand;
+    if constexpr (LT::RB > MANIFOLD) {   /* the pair's MANIFOLD deepest by (depth, sample) */
+        const float dd = cand ? depth : 3.0e38f;
+        int rank = 0;
+        sfor<0, 16>([&](auto uc) __attribute__((always_inline)) {
+            constexpr int U = decltype(uc)::value;
+            const float du = bcast16<U>(dd);
+            rank += (du < dd || (du == dd && U < c)) ? 1 : 0;
+        });
+        keep = cand && rank < MANIFOLD;
+    }
+    const uint64_t bm = __ballot(keep);
+    if (bm == 0) return;
+    unsigned wm = __builtin_amdgcn_readfirstlane((unsigned)((bm | (bm >> 16) | (bm >> 32) | (bm >> 48)) & 0xFFFFu));
+    const V3 n = mul(Rc, nl);
+    const V3 pa = C - r * n, rb = mul(Rc, qb);
+    const int row0 = (int)(threadIdx.x & ~(unsigned)(GW - 1));
+    while (wm) {   /* in sample order, as the sequential walk inserts them */
+        const int k = __builtin_ctz(wm);
+        wm &= wm - 1u;
+        const int src = row0 + k;
+        const bool ck = __shfl((int)keep, src) != 0;
+        const float dk = __shfl(depth, src);
+        const V3 pk = v3(__shfl(pa.x, src), __shfl(pa.y, src), __shfl(pa.z, src));
+        const V3 nk = v3(__shfl(n.x, src), __shfl(n.y, src), __shfl(n.z, src));
+        const V3 rk = v3(__shfl(rb.x, src), __shfl(rb.y, src), __shfl(rb.z, src));
+        if (ck) g1_insert(L, es, dk, (float)(32 + 16 * cn + k), jc, pk, nk, rk);
+    }
+}
+
 /* ReachAO: the obstacles are static colliders (create_obstacle_sphere / _cuboid,
  * reach_ao.py:819-860: mass 0, not ghosts), so stepSimulation resolves robot contacts with
  * them like the table's (oracle detect(), "ReachAO" branch): capsule c (wave-uniform) against
@@ -1628,7 +1699,7 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                 while (wm) {
                     const int cn = __builtin_ctz(wm);
                     wm &= wm - 1u;
-                    if ((rm >> cn) & 1u) object_candidates(e, m.contact_dist, *Lp, es, ob, Rc, cn, false);
+                    object_candidates_g(e, m.contact_dist, *Lp, es, ob, Rc, cn, c, ((rm >> cn) & 1u) != 0);
                 }
                 PGX_PROF_MARK(21);
                 sort_groups(*Lp, es);
