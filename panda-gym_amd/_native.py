@@ -26,14 +26,15 @@ class PgxError(RuntimeError):
     """A libpgx call returned a negative status (message from pgx_last_error)."""
 
 
-_lib = None
+_libs = {}
 
 
-def load(path: str = LIB_PATH):
-    """Load libpgx.so once; raise loudly if it is absent (build with __graft_entry__.build())."""
-    global _lib
-    if _lib is not None:
-        return _lib
+def load(path: str = None):
+    """Load libpgx.so (or another build of the same ABI, e.g. libpgx_rtmodel.so) once per path;
+    raise loudly if it is absent (build with __graft_entry__.build())."""
+    path = path or LIB_PATH
+    if path in _libs:
+        return _libs[path]
     if not os.path.exists(path):
         raise PgxError(f"libpgx.so not found at {path}: run `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = C.CDLL(path)
@@ -71,11 +72,11 @@ def load(path: str = LIB_PATH):
     lib.pgx_replay_sample.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.POINTER(PgxReplayBatch), C.c_void_p]
     lib.pgx_replay_episode_arrays.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                               C.POINTER(C.c_void_p)]
-    _lib = lib
+    _libs[path] = lib
     return lib
 
 
-def check(rc: int, what: str) -> None:
+def check(rc: int, what: str, lib=None) -> None:
     if rc != 0:
-        msg = load().pgx_last_error().decode(errors="replace")
+        msg = (lib or load()).pgx_last_error().decode(errors="replace")
         raise PgxError(f"{what} failed ({rc}): {msg}")

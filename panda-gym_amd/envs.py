@@ -156,10 +156,14 @@ class PandaVecEnv:
     def __init__(self, env_id: str = "PandaReach-v3", num_envs: int = 4096, device: Any = "cuda:0", seed: int = 0,
                  env_id_offset: int = 0, max_episode_steps: Optional[int] = None, auto_reset: bool = True,
                  n_substeps: int = 20, model_name: str = "panda_custom0", contacts: bool = True,
-                 lanes_per_env: int = 0, full_manifold: Optional[bool] = None):
+                 lanes_per_env: int = 0, full_manifold: Optional[bool] = None,
+                 sim_params: Optional[Dict[str, Any]] = None, lib_path: Optional[str] = None):
+        """``sim_params``: pgx_sim_params fields to override (the default library runs only the
+        compiled parameters and refuses others; ``lib_path`` = libpgx_rtmodel.so reads them from
+        the handle)."""
         if torch is None:
             raise PgxError("PandaVecEnv needs torch for device buffers")
-        self.lib = load()
+        self.lib = load(lib_path)
         self.env_id = env_id
         base_spec = spec(env_id)
         if max_episode_steps is not None:
@@ -171,6 +175,13 @@ class PandaVecEnv:
             raise PgxError("PandaVecEnv runs on a HIP device only (no CPU physics fallback)")
         self._model = abi.make_model(load_model(model_name), ee_link=11)
         self._params = abi.default_sim_params(n_substeps=n_substeps)
+        for k, v in (sim_params or {}).items():
+            field = getattr(self._params, k)
+            if hasattr(field, "__len__"):
+                for i, x in enumerate(v):
+                    field[i] = x
+            else:
+                setattr(self._params, k, v)
         if full_manifold is None:   # the per-pair manifold budget wherever the 16-lane kernels run
             full_manifold = bool(contacts) and lanes_per_env != 1 and os.environ.get("PGX_LANES_PER_ENV") != "1"
         self._cfg = abi.make_config(self.spec, self.num_envs, self._model, self._params, seed=seed,
@@ -183,7 +194,7 @@ class PandaVecEnv:
         self.action_dim = self.lib.pgx_action_dim(C.byref(self._cfg))
         h = C.c_void_p()
         torch.cuda.set_device(self.device)
-        check(self.lib.pgx_create(C.byref(self._cfg), self.device.index or 0, C.byref(h)), "pgx_create")
+        self._check(self.lib.pgx_create(C.byref(self._cfg), self.device.index or 0, C.byref(h)), "pgx_create")
         self._h = h
         self.seed_value = seed
         n, od = self.num_envs, self.obs_dim
@@ -224,6 +235,9 @@ class PandaVecEnv:
         self._step_index = 0
 
     # ---------------------------------------------------------------- core
+    def _check(self, rc: int, what: str) -> None:
+        check(rc, what, self.lib)
+
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
@@ -245,7 +259,7 @@ class PandaVecEnv:
         pos, quat (x,y,z,w), linvel, angvel; contacts [2 * abi.CONTACT_SLOTS, N] f32 warm-start cache
         (feature id, normal impulse): object-scene slots, then robot slots; elapsed, episode [N])."""
         v = abi.PgxStateView()
-        check(self.lib.pgx_get_state(self._h, C.byref(v)), "pgx_get_state")
+        self._check(self.lib.pgx_get_state(self._h, C.byref(v)), "pgx_get_state")
         n = self.num_envs
         return {
             "q": _view(v.q, (7, n), torch.float32, self.device),
@@ -265,7 +279,7 @@ class PandaVecEnv:
         """Robot contact points this handle's kernels keep per env (the deepest of Bullet's <= 4 per
         colliding pair; abi.ROBOT_POINTS / ROBOT_POINTS_ARM / ROBOT_POINTS_ONE_LANE; 0 without contacts)."""
         v = abi.PgxStateView()
-        check(self.lib.pgx_get_state(self._h, C.byref(v)), "pgx_get_state")
+        self._check(self.lib.pgx_get_state(self._h, C.byref(v)), "pgx_get_state")
         return int(v.robot_points)
 
     def raise_device_errors(self, errors: Optional[int] = None) -> None:
@@ -306,7 +320,7 @@ class PandaVecEnv:
         m = None
         if mask is not None:
             m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
-        check(self.lib.pgx_reset(self._h, None if m is None else C.c_void_p(m.data_ptr()),
+        self._check(self.lib.pgx_reset(self._h, None if m is None else C.c_void_p(m.data_ptr()),
                                  None if inj is None else C.c_void_p(inj.data_ptr()),
                                  None if inj_obj is None else C.c_void_p(inj_obj.data_ptr()), C.byref(self._out),
                                  self._stream()), "pgx_reset")
@@ -322,14 +336,14 @@ class PandaVecEnv:
             a = a.to(device=self.device, dtype=torch.float32).contiguous()
         if tuple(a.shape) != (self.num_envs, self.action_dim):
             raise ValueError(f"actions must be [{self.num_envs}, {self.action_dim}], got {tuple(a.shape)}")
-        check(self.lib.pgx_step(self._h, C.c_void_p(a.data_ptr()), C.byref(self._out), self._stream()), "pgx_step")
+        self._check(self.lib.pgx_step(self._h, C.c_void_p(a.data_ptr()), C.byref(self._out), self._stream()), "pgx_step")
         self._step_index += 1
         return self._obs_dict(), self.reward, self.terminated, self.truncated, self.success
 
     def sample_actions(self, step: Optional[int] = None) -> torch.Tensor:
         """Random policy U[-1,1) from the device Philox stream (benchmark workload)."""
         s = self._step_index if step is None else step
-        check(self.lib.pgx_sample_actions(self._h, C.c_void_p(self._actions.data_ptr()), C.c_uint64(s),
+        self._check(self.lib.pgx_sample_actions(self._h, C.c_void_p(self._actions.data_ptr()), C.c_uint64(s),
                                           self._stream()), "pgx_sample_actions")
         return self._actions
 
@@ -443,7 +457,7 @@ class PandaVecEnv:
         dg = dg.to(self.device, torch.float32).reshape(-1, 3).contiguous()
         out = torch.empty(ag.shape[0], dtype=torch.float32, device=self.device)
         rt = abi.REWARD_CODES[self.reward_type]
-        check(self.lib.pgx_compute_reward(C.c_void_p(ag.data_ptr()), C.c_void_p(dg.data_ptr()),
+        self._check(self.lib.pgx_compute_reward(C.c_void_p(ag.data_ptr()), C.c_void_p(dg.data_ptr()),
                                           C.c_int64(ag.shape[0]), rt, C.c_double(self.distance_threshold),
                                           C.c_void_p(out.data_ptr()), self._stream()), "pgx_compute_reward")
         out = out.reshape(shape)
@@ -468,17 +482,17 @@ class PandaVecEnv:
         PyBullet.save_state, pybullet.py:79-86): the id is libpgx's, the first non-negative
         integer not in use."""
         sid = C.c_int32()
-        check(self.lib.pgx_snapshot(self._h, C.byref(sid), self._stream()), "pgx_snapshot")
+        self._check(self.lib.pgx_snapshot(self._h, C.byref(sid), self._stream()), "pgx_snapshot")
         return int(sid.value)
 
     def restore_state(self, state_id: int) -> None:
         """Restore a snapshot; an id that was removed (or never saved) raises PgxError, as
         pybullet.error in the reference (test/save_and_restore_test.py:30-36)."""
-        check(self.lib.pgx_restore(self._h, int(state_id), self._stream()), "pgx_restore")
+        self._check(self.lib.pgx_restore(self._h, int(state_id), self._stream()), "pgx_restore")
 
     def remove_state(self, state_id: int) -> None:
         """Free a snapshot; its id becomes available again (PyBullet.remove_state, pybullet.py:96-102)."""
-        check(self.lib.pgx_release(self._h, int(state_id)), "pgx_release")
+        self._check(self.lib.pgx_release(self._h, int(state_id)), "pgx_release")
 
 
 _INFO_TEMPLATES = [{"is_success": s, "is_truncated": c} for c in (False, True) for s in (False, True)]

@@ -63,11 +63,13 @@ OUTLIER = 1e-3   # per-step errors above this must be explained by the oracle's 
 
 
 def _one_step_errors(pg, oracle, env_id, n, steps, seed, actions=None, lanes=0, outliers=None, full=False,
-                     over=None):
+                     over=None, **kw):
     """Per step, from the device state copied into the oracle: |device - oracle| of the EE
     position (obs 0:3) and the achieved goal (EE or object position).  With ``outliers`` (a
-    list), every sample above OUTLIER is recorded with its oracle input for _self_sensitivity."""
-    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=seed, lanes_per_env=lanes, full_manifold=full)
+    list), every sample above OUTLIER is recorded with its oracle input for _self_sensitivity.
+    ``kw``: more PandaVecEnv arguments (sim_params, lib_path)."""
+    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=seed, lanes_per_env=lanes, full_manifold=full,
+                          **kw)
     venv.reset_tensors(seed=seed)
     ref = oracle.OracleVecEnv(venv._cfg, n)
     ee_err, ag_err = [], []
@@ -422,3 +424,24 @@ def abi_budget(case):
     from panda_gym_amd import abi
 
     return abi.ROBOT_POINTS_ARM if case == "two_links_on_table" else abi.ROBOT_POINTS
+
+
+def test_runtime_model_library_other_frictions(pg, oracle):
+    """libpgx_rtmodel.so (make runtime-model: the same kernels reading the handle's physics block)
+    runs physics parameters the default library refuses -- here other lateral frictions (the
+    reference sets them per link through changeDynamics, panda.py:69-72 -> pybullet.py:880-892) --
+    and matches the oracle at the same parameters, per step from the same state."""
+    import os
+
+    from panda_gym_amd import _native
+
+    path = os.path.join(os.path.dirname(_native.LIB_PATH), "libpgx_rtmodel.so")
+    assert os.path.exists(path), "libpgx_rtmodel.so is built by __graft_entry__.build()"
+    over = {"friction": 0.36, "link_friction": [0.3] * 9 + [0.8, 0.8] + [0.3] * 5}
+    with pytest.raises(pg.PgxError):
+        pg.PandaVecEnv("PandaPush-v3", num_envs=8, device="cuda:0", sim_params=over)
+    ee, ag, _ = _one_step_errors(pg, oracle, "PandaPush-v3", 256, 40, 21, full=True, sim_params=over, lib_path=path)
+    q = lambda x, p: float(np.percentile(x, p))  # noqa: E731
+    print(f"\nruntime model, frictions {over['friction']} / {over['link_friction'][9]}: EE p99 {q(ee, 99):.2e} "
+          f"max {ee.max():.2e}, object p99 {q(ag, 99):.2e} max {ag.max():.2e}")
+    assert q(ee, 99) <= 1e-5 and q(ag, 99) <= 1e-5 and ee.max() <= 1e-2 and ag.max() <= 1e-2
