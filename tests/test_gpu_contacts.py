@@ -445,3 +445,28 @@ def test_runtime_model_library_other_frictions(pg, oracle):
     print(f"\nruntime model, frictions {over['friction']} / {over['link_friction'][9]}: EE p99 {q(ee, 99):.2e} "
           f"max {ee.max():.2e}, object p99 {q(ag, 99):.2e} max {ag.max():.2e}")
     assert q(ee, 99) <= 1e-5 and q(ag, 99) <= 1e-5 and ee.max() <= 1e-2 and ag.max() <= 1e-2
+
+
+@pytest.mark.parametrize("env_id,points", [("PandaReach-v3", 8), ("PandaReachJoints-v3", 8), ("PandaPush-v3", 12),
+                                           ("PandaPickAndPlace-v3", 12), ("PandaReachAO-v3", 8)])
+def test_default_handles_keep_the_per_pair_manifold_budget(pg, env_id, points):
+    """The default handle (PandaVecEnv / make) runs Bullet's per-pair manifold budget: 8 robot
+    points in Reach / ReachAO, 12 in Push / PickAndPlace (include/pgx.h); 4 on request or in the
+    one-lane layout; none without contacts."""
+    v = pg.PandaVecEnv(env_id, num_envs=64, device="cuda:0")
+    assert v.robot_contact_budget() == points
+    v.close()
+    if env_id != "PandaReachAO-v3":
+        v = pg.PandaVecEnv(env_id, num_envs=64, device="cuda:0", full_manifold=False)
+        assert v.robot_contact_budget() == 4
+        v.close()
+        v = pg.PandaVecEnv(env_id, num_envs=64, device="cuda:0", lanes_per_env=1)
+        assert v.robot_contact_budget() == 4
+        v.close()
+    env = pg.make(env_id)
+    assert env._vec.robot_contact_budget() == points
+    env.close()
+    if env_id.startswith("PandaReach-"):
+        v = pg.PandaVecEnv(env_id, num_envs=64, device="cuda:0", contacts=False)
+        assert v.robot_contact_budget() == 0
+        v.close()
