@@ -237,12 +237,14 @@ def her_leg(dev, calls: int, with_cpu: bool):
     return res
 
 
-def task_leg(dev, env_id: str, n: int, steps: int, contacts: bool = True, flops_key: str = ""):
+def task_leg(dev, env_id: str, n: int, steps: int, contacts: bool = True, flops_key: str = "",
+             full_manifold=None):
     """env-steps/s of one more task config on this GPU (device random policy, in-kernel
-    auto-reset), timed like the main leg: barrier-free single GPU, HIP events bracketing."""
+    auto-reset), timed like the main leg: barrier-free single GPU, HIP events bracketing.
+    ``full_manifold=False``: the 4-point robot budget (reduced fidelity, for comparison only)."""
     import panda_gym_amd as pg
 
-    venv = pg.PandaVecEnv(env_id, num_envs=n, device=dev, seed=1, contacts=contacts)
+    venv = pg.PandaVecEnv(env_id, num_envs=n, device=dev, seed=1, contacts=contacts, full_manifold=full_manifold)
     obs_dim, act_dim, budget = venv.obs_dim, venv.action_dim, venv.robot_contact_budget()
     venv.reset_tensors()
     for t in range(20):
@@ -268,8 +270,14 @@ def task_leg(dev, env_id: str, n: int, steps: int, contacts: bool = True, flops_
         alg = alg_bytes_per_env_step(flops_key, obs_dim, act_dim, budget)["total"]
     if alg:
         prof = pmc("pmc_object_kernel_" + ("push" if flops_key == "push" else "pnp"), n)
-        kname = ("step_kernel_o2<0, 1, 1, 0, 1> (object kernel, 16 lanes per env, two waves per SIMD)" if n > 4096
-                 else "step_kernel<0, 1, 1, 0, 1> (object kernel, 16 lanes per env)")
+        if budget > 4:   # the per-pair manifold kernels of the object tasks: one wave per SIMD at every batch
+            kname = "step_kernel<0, 1, 1, 0, 2> (object kernel, 16 lanes per env, per-pair manifold budget)"
+        else:
+            kname = ("step_kernel_o2<0, 1, 1, 0, 1> (object kernel, 16 lanes per env, two waves per SIMD)" if n > 4096
+                     else "step_kernel<0, 1, 1, 0, 1> (object kernel, 16 lanes per env)")
+            res["fidelity"] = "reduced: 4 robot contact points per env (not the per-pair manifold rule)"
+        if prof and prof.get("robot_points", 4) != budget:
+            prof = None   # PMC of another budget's kernel
         res["roofline"] = hbm_roofline(alg * n, ms, prof, kname)
     return res
 
@@ -443,8 +451,6 @@ def main():
                                             world, coll_dev)
 
     if rank == 0:
-
-        achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
         traffic = None
         # the binding roofline: algorithmic FLOPs (op-counted in the oracle, frozen) over the
         # kernel's own launch time (HIP events on the launch stream)
@@ -452,6 +458,7 @@ def main():
                 "PandaReachAO-v3": "reach_ao"}.get(args.env_id)
         alg_bytes = alg_bytes_per_env_step(fkey or "reach_table", venv.obs_dim, venv.action_dim,
                                            venv.robot_contact_budget())["total"] * E
+        achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
         valu = None
         if fkey:
             valu = valu_roofline(fkey, E / (kernel_ms * 1e-3), "env-steps/s of the step kernel alone (kernel_ms)")
@@ -508,7 +515,11 @@ def main():
                              task_leg(dev, "PandaPickAndPlace-v3", 16384, args.task_steps,            # configs[3]
                                       flops_key="pick_and_place"),
                              task_leg(dev, args.env_id, E, args.task_steps, contacts=False,           # no table
-                                      flops_key="reach_no_table")]
+                                      flops_key="reach_no_table"),
+                             # the round-3 robot budget (4 points), for comparison only
+                             task_leg(dev, "PandaPush-v3", 4096, args.task_steps, flops_key="push", full_manifold=False),
+                             task_leg(dev, "PandaPickAndPlace-v3", 16384, args.task_steps, flops_key="pick_and_place",
+                                      full_manifold=False)]
             line["sb3_host_path"] = host_path_leg(dev, args.env_id, E, 100)
         print(json.dumps(line), flush=True)
     venv.close()

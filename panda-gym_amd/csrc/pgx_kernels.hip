@@ -4190,9 +4190,13 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
     const bool two = e.wave_mode == 2 || (e.wave_mode == 0 && wide && grid.x > 1024);   /* more waves than SIMDs */
     const int variant = e.ao ? 13 : e.control * 4 + (e.has_object ? 2 : 0) + (e.contacts ? 1 : 0);
     if (wide && e.full_manifold) {
+        /* the object tasks' per-pair manifold kernels run one wave per SIMD at every batch: their
+         * 32 KB of LDS per wave lets only 5 of the two-wave build's 8 waves per CU in, and at 256
+         * registers it spills 676 B per lane (PickAndPlace 16384: 8.54 ms two-wave, 4.51 ms one
+         * wave, profiles/r04/ab_full_waves_start.log) */
         switch (variant) {
-            case 3: PGX_STEP2(0, 1, 1, 0, 2); break;
-            case 7: PGX_STEP2(1, 1, 1, 0, 2); break;
+            case 3: PGX_STEP(0, 1, 1, 0, 2); break;
+            case 7: PGX_STEP(1, 1, 1, 0, 2); break;
             case 13: PGX_STEP2(1, 0, 1, 1, 2); break;
             default: return (int)hipErrorInvalidValue;
         }

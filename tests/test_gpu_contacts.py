@@ -9,6 +9,15 @@ chaotically.  The bar is therefore set per step, from the same state: 99th perce
 the EE and object positions, and every deviation above 1e-4 must sit where the oracle is itself
 that sensitive to a rounding-level (1e-7 relative) change of its input (test below); plus the
 physical invariants the oracle tests pin (test_oracle_contacts.py) checked on the device.
+
+Where the tool bar slides on the table (test_reach_with_table_contacts, the runtime-model friction
+test) the step is worse conditioned since round 4 gave the tool bar its own lateral friction
+(panda.py:69-70: mu 0.5 against the table instead of 0.25): from the same state the device's p99
+went 2.4e-6 -> 2.9e-5 while the restated algorithm evaluated in fp32 (oracle/fp32_emul.cpp) moves
+by 9.0e-5 -> 1.8e-4 (tools/gpu_table_drive.py, profiles/r04/table_drive.log).  Those tests hold
+the device inside that fp32 envelope, from the same state, percentile for percentile (p99, p99.9),
+instead of an absolute p99; the tool bar at mu 0.25 (through libpgx_rtmodel.so) keeps the
+absolute 1e-5 bar.
 """
 import numpy as np
 import pytest
@@ -63,15 +72,22 @@ OUTLIER = 1e-3   # per-step errors above this must be explained by the oracle's 
 
 
 def _one_step_errors(pg, oracle, env_id, n, steps, seed, actions=None, lanes=0, outliers=None, full=False,
-                     over=None, **kw):
+                     over=None, envelope=None, **kw):
     """Per step, from the device state copied into the oracle: |device - oracle| of the EE
     position (obs 0:3) and the achieved goal (EE or object position).  With ``outliers`` (a
     list), every sample above OUTLIER is recorded with its oracle input for _self_sensitivity.
+    With ``envelope`` (a dict), the fp32 build of the oracle steps from the same state too and
+    its deviation from the fp64 oracle lands in envelope["ee"], envelope["ag"].
     ``kw``: more PandaVecEnv arguments (sim_params, lib_path)."""
     venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=seed, lanes_per_env=lanes, full_manifold=full,
                           **kw)
     venv.reset_tensors(seed=seed)
     ref = oracle.OracleVecEnv(venv._cfg, n)
+    r32 = None
+    if envelope is not None:
+        r32 = oracle.OracleVecEnv(venv._cfg, n, fp32=True)
+        oracle.fp32_lib().pgxo_set_robot_budget(venv.robot_contact_budget() or -1)
+        envelope["ee"], envelope["ag"] = [], []
     ee_err, ag_err = [], []
     n_obj = 4   # the object-scene slots ahead of the robot slots in the contact cache
     for t in range(steps):
@@ -83,8 +99,12 @@ def _one_step_errors(pg, oracle, env_id, n, steps, seed, actions=None, lanes=0, 
         else:   # one action for every env, or one per env
             at = np.asarray(actions[t], np.float32)
             a = torch.as_tensor(at if at.ndim == 2 else np.repeat(at[None], n, 0), device="cuda:0")
+        if r32 is not None:
+            for k in ("q", "qd", "qc", "goal", "obj", "elapsed", "episode"):
+                getattr(r32, k)[:] = getattr(ref, k)
         venv.step_tensors(a)
         out = ref.step(a.cpu().numpy())
+        o32 = r32.step(a.cpu().numpy()) if r32 is not None else None
         obs, ag, dg = _obs(venv)
         if over is not None:   # envs whose last substep held more than 4 robot points
             over[0] += int(((venv.state()["contacts"][2 * n_obj::2] >= 0).sum(dim=0) > 4).sum().item())
@@ -95,6 +115,9 @@ def _one_step_errors(pg, oracle, env_id, n, steps, seed, actions=None, lanes=0, 
         e_ag = np.abs(ag - out["ag"]).max(axis=1)
         ee_err.append(e_ee)
         ag_err.append(e_ag)
+        if o32 is not None:
+            envelope["ee"].append(np.abs(o32["obs"][:, :3] - out["obs"][:, :3]).max(axis=1))
+            envelope["ag"].append(np.abs(o32["ag"] - out["ag"]).max(axis=1))
         if outliers is not None:
             for i in np.nonzero(np.maximum(e_ee, e_ag) > OUTLIER)[0]:
                 outliers.append({"t": t, "env": int(i), "err_ee": float(e_ee[i]), "err_ag": float(e_ag[i]),
@@ -107,7 +130,20 @@ def _one_step_errors(pg, oracle, env_id, n, steps, seed, actions=None, lanes=0, 
     venv.close()
     if outliers is not None:
         outliers.append((cfg, keep))
+    if envelope is not None:
+        envelope["ee"], envelope["ag"] = np.stack(envelope["ee"]), np.stack(envelope["ag"])
     return np.stack(ee_err), np.stack(ag_err), final
+
+
+def _inside_envelope(name, dev, f32, pcts=(99, 99.9), floor=1e-5):
+    """The device's per-step deviation from the fp64 oracle is at most the fp32 evaluation's of
+    the restated algorithm from the same state, percentile for percentile -- or below ``floor``
+    (the absolute p99 bar), where both sit at rounding level (joint control, no IK: device
+    p99.9 3.6e-7 vs fp32 oracle 3.3e-7 on PickAndPlaceJoints) and their order is noise."""
+    for p in pcts:
+        d, f = float(np.percentile(dev, p)), float(np.percentile(f32, p))
+        print(f"{name} p{p}: device {d:.2e} | fp32 oracle {f:.2e}")
+        assert d <= max(f, floor), (name, p, d, f)
 
 
 def _self_sensitivity(oracle, cfg, rec, trials=16, rel=1e-7, seed=0):
@@ -137,14 +173,16 @@ def test_reach_with_table_contacts(pg, oracle, lanes):
     off = rng.uniform(-0.2, 0.2, (64, 3)).astype(np.float32)
     off[:, 2] = 0.0
     acts = [np.clip(np.array([0.3, -0.2, -1.0], np.float32) + off, -1, 1)] * 30
-    outl = []
-    ee, ag, _ = _one_step_errors(pg, oracle, "PandaReach-v3", 64, 30, 3, acts, lanes=lanes, outliers=outl)
+    outl, env = [], {}
+    ee, ag, _ = _one_step_errors(pg, oracle, "PandaReach-v3", 64, 30, 3, acts, lanes=lanes, outliers=outl,
+                                 envelope=env)
     print(f"\ntable contacts: EE error p99 {np.percentile(ee, 99):.2e} max {ee.max():.2e}")
-    assert np.percentile(ee, 99) <= 1e-5 and ee.max() <= 1e-3, (np.percentile(ee, 99), ee.max())
+    _inside_envelope("ee", ee, env["ee"])
+    assert np.percentile(ee, 99) <= 1e-4 and ee.max() <= 1e-3, (np.percentile(ee, 99), ee.max())
     venv = pg.PandaVecEnv("PandaReach-v3", num_envs=64, device="cuda:0", seed=3, lanes_per_env=lanes)
     venv.reset_tensors(seed=3)
-    for a in acts:
-        venv.step_tensors(torch.tensor([a] * 64, dtype=torch.float32, device="cuda:0"))
+    for a in acts:   # one action per env
+        venv.step_tensors(torch.tensor(a, dtype=torch.float32, device="cuda:0"))
     z = venv.obs[:, 2].cpu().numpy()
     assert z.min() > 0.035, z.min()
     venv.close()
@@ -152,17 +190,19 @@ def test_reach_with_table_contacts(pg, oracle, lanes):
 
 @pytest.mark.parametrize("env_id", ["PandaPush-v3", "PandaPickAndPlaceJoints-v3"])
 def test_random_policy_one_step_parity(pg, oracle, env_id, lanes):
-    """p99 <= 1e-5 and p99.9 <= 1e-4 in both layouts.  One lane per env: max <= 1e-3.  The
+    """p99 <= 1e-5 in both layouts, p99.9 inside the fp32 envelope (round 3: <= 1e-4; with the tool
+    bar's friction of round 4 the one-lane Push EE p99.9 measured 1.1e-4 against the fp32 oracle's
+    2.8e-4).  One lane per env: max <= 1e-3.  The
     16-lane layout (lane-parallel bias / CRBA: a different summation order) may exceed 1e-3 only
     at a contact bifurcation, and only where the oracle itself, from its input perturbed by 1e-7
     relative (the fp32 rounding scale), moves by at least the device's deviation (max over 32
     trials); at most one such sample per 2000."""
-    outl = []
-    ee, ag, final = _one_step_errors(pg, oracle, env_id, 256, 50, 21, lanes=lanes, outliers=outl)
+    outl, env = [], {}
+    ee, ag, final = _one_step_errors(pg, oracle, env_id, 256, 50, 21, lanes=lanes, outliers=outl, envelope=env)
     cfg, _keep = outl.pop()
-    for name, e in (("ee", ee), ("object", ag)):
+    for name, e, f in (("ee", ee, env["ee"]), ("object", ag, env["ag"])):
         assert np.percentile(e, 99) <= 1e-5, (name, np.percentile(e, 99))
-        assert np.percentile(e, 99.9) <= 1e-4, (name, np.percentile(e, 99.9))
+        _inside_envelope(name, e, f, pcts=(99.9,))
         assert e.max() <= (1e-2 if lanes == 16 else OUTLIER), (name, e.max())
     assert len(outl) <= ee.size // 2000, len(outl)
     for rec in outl:
@@ -178,13 +218,14 @@ def test_full_manifold_random_policy_one_step_parity(pg, oracle, env_id):
     """PGX_CONTACTS_FULL (16 lanes, robot budget 12): the same per-step bars as the default
     budget over a random-policy run in which envs hold more than 4 robot points (the extra
     rows in LDS), against the oracle at the same budget."""
-    outl, over = [], [0]
-    ee, ag, final = _one_step_errors(pg, oracle, env_id, 256, 50, 21, lanes=16, outliers=outl, full=True, over=over)
+    outl, over, env = [], [0], {}
+    ee, ag, final = _one_step_errors(pg, oracle, env_id, 256, 50, 21, lanes=16, outliers=outl, full=True, over=over,
+                                     envelope=env)
     cfg, _keep = outl.pop()
     assert over[0] > 0, "no env held more than 4 robot points"
-    for name, e in (("ee", ee), ("object", ag)):
+    for name, e, f in (("ee", ee, env["ee"]), ("object", ag, env["ag"])):
         assert np.percentile(e, 99) <= 1e-5, (name, np.percentile(e, 99))
-        assert np.percentile(e, 99.9) <= 1e-4, (name, np.percentile(e, 99.9))
+        _inside_envelope(name, e, f, pcts=(99.9,))
         assert e.max() <= 1e-2, (name, e.max())
     assert len(outl) <= ee.size // 2000, len(outl)
     for rec in outl:
@@ -440,11 +481,36 @@ def test_runtime_model_library_other_frictions(pg, oracle):
     over = {"friction": 0.36, "link_friction": [0.3] * 9 + [0.8, 0.8] + [0.3] * 5}
     with pytest.raises(pg.PgxError):
         pg.PandaVecEnv("PandaPush-v3", num_envs=8, device="cuda:0", sim_params=over)
-    ee, ag, _ = _one_step_errors(pg, oracle, "PandaPush-v3", 256, 40, 21, full=True, sim_params=over, lib_path=path)
+    env = {}
+    ee, ag, _ = _one_step_errors(pg, oracle, "PandaPush-v3", 256, 40, 21, full=True, sim_params=over, lib_path=path,
+                                 envelope=env)
     q = lambda x, p: float(np.percentile(x, p))  # noqa: E731
     print(f"\nruntime model, frictions {over['friction']} / {over['link_friction'][9]}: EE p99 {q(ee, 99):.2e} "
           f"max {ee.max():.2e}, object p99 {q(ag, 99):.2e} max {ag.max():.2e}")
-    assert q(ee, 99) <= 1e-5 and q(ag, 99) <= 1e-5 and ee.max() <= 1e-2 and ag.max() <= 1e-2
+    # the tool bar at mu 0.8 sliding on the table: the fp32 envelope (module docstring)
+    _inside_envelope("ee", ee, env["ee"])
+    _inside_envelope("object", ag, env["ag"])
+    assert q(ee, 99) <= 1e-4 and q(ag, 99) <= 1e-5 and ee.max() <= 1e-2 and ag.max() <= 1e-2
+
+
+@pytest.mark.parametrize("lanes_", [16, 1])
+def test_table_drive_tool_bar_mu_025_absolute_bar(pg, oracle, lanes_):
+    """The table drive of test_reach_with_table_contacts with every link at mu 0.25 against the
+    table (round 3's friction, through libpgx_rtmodel.so): the absolute bar, p99 <= 1e-5."""
+    import os
+
+    from panda_gym_amd import _native
+
+    path = os.path.join(os.path.dirname(_native.LIB_PATH), "libpgx_rtmodel.so")
+    rng = np.random.default_rng(3)
+    off = rng.uniform(-0.2, 0.2, (64, 3)).astype(np.float32)
+    off[:, 2] = 0.0
+    acts = [np.clip(np.array([0.3, -0.2, -1.0], np.float32) + off, -1, 1)] * 30
+    ee, _, _ = _one_step_errors(pg, oracle, "PandaReach-v3", 64, 30, 3, acts, lanes=lanes_,
+                                sim_params={"link_friction": [0.25] * 16}, lib_path=path)
+    print(f"\ntool bar mu 0.25: EE error p99 {np.percentile(ee, 99):.2e} max {ee.max():.2e}")
+    assert np.all(np.isfinite(ee))
+    assert np.percentile(ee, 99) <= 1e-5 and ee.max() <= 1e-3, (np.percentile(ee, 99), ee.max())
 
 
 @pytest.mark.parametrize("env_id,points", [("PandaReach-v3", 8), ("PandaReachJoints-v3", 8), ("PandaPush-v3", 12),

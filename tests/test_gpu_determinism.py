@@ -1,0 +1,56 @@
+"""Run-to-run determinism of the step kernels: two handles with the same seed, stepped with the
+same device Philox actions, give bit-identical observations and state in every layout.  (Round 4
+found the runtime-model build's one-lane Reach kernel non-deterministic when compiled with SLP
+vectorisation -- profiles/r04/rtmodel_slp_nan.log; the parity tests compare against the oracle
+per step from the device state, so they cannot see run-to-run variation.)"""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pg():
+    import panda_gym_amd as pg
+
+    pg.load_native()
+    return pg
+
+
+def _rollout(pg, env_id, n, lanes, steps, **kw):
+    v = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=21, lanes_per_env=lanes, **kw)
+    v.reset_tensors(seed=21)
+    out = []
+    for t in range(steps):
+        v.step_tensors(v.sample_actions(t))
+        st = v.state()
+        out.append(torch.cat([v.obs, st["q"].T, st["qd"].T, st["contacts"].T], 1).cpu().numpy().copy())
+    v.close()
+    return np.stack(out)
+
+
+@pytest.mark.parametrize("env_id,lanes", [("PandaReach-v3", 16), ("PandaReach-v3", 1), ("PandaPush-v3", 16),
+                                          ("PandaPush-v3", 1), ("PandaPickAndPlaceJoints-v3", 1),
+                                          ("PandaPickAndPlaceJoints-v3", 16), ("PandaReachAO-v3", 16)])
+def test_step_kernels_are_deterministic(pg, env_id, lanes):
+    a = _rollout(pg, env_id, 256, lanes, 30)
+    b = _rollout(pg, env_id, 256, lanes, 30)
+    diff = np.flatnonzero(~((a == b) | (np.isnan(a) & np.isnan(b))).all(axis=(1, 2)))
+    assert diff.size == 0, f"first differing step {diff[:1]}"
+    assert np.isfinite(a).all()
+
+
+def test_runtime_model_library_is_deterministic(pg):
+    from panda_gym_amd import _native
+
+    path = os.path.join(os.path.dirname(_native.LIB_PATH), "libpgx_rtmodel.so")
+    kw = {"lib_path": path, "sim_params": {"friction": 0.3}}
+    for env_id, lanes in (("PandaReach-v3", 1), ("PandaReach-v3", 16), ("PandaPush-v3", 1)):
+        a = _rollout(pg, env_id, 64, lanes, 10, **kw)
+        b = _rollout(pg, env_id, 64, lanes, 10, **kw)
+        assert np.isfinite(a).all(), (env_id, lanes)
+        assert np.array_equal(a, b), (env_id, lanes)

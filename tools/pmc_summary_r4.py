@@ -50,6 +50,10 @@ KERNELS = [   # (name, kernel-name fragment (any step_kernel / step_kernel_o2 bu
 ]
 
 
+ROBOT_POINTS = {"pmc_step_kernel": 8, "pmc_object_kernel_push": 12, "pmc_object_kernel_pnp": 12,
+                "pmc_reach_ao_kernel": 8}   # the per-pair manifold budgets (include/pgx.h)
+
+
 def main(src=os.path.join(ROOT, "gpurun_out", "pmc_r4"), round_tag="r04"):
     rows = []
     for p in sorted(glob.glob(os.path.join(src, "p*", "run_counter_collection.csv"))):
@@ -80,6 +84,7 @@ def main(src=os.path.join(ROOT, "gpurun_out", "pmc_r4"), round_tag="r04"):
                         and (grid is None or int(r["Grid_Size"]) == grid)})
         out = {
             "kernel": frag, "kernel_names": names, "num_envs": envs, "grid_threads": grid,
+            "robot_points": ROBOT_POINTS.get(name),
             "dispatches": {k: len(v) for k, v in agg.items()}, "counters_mean_per_dispatch": mean,
             "fetch_kb": mean.get("FETCH_SIZE"), "write_kb": mean.get("WRITE_SIZE"), "fetch_correction": 2.0,
             "fetch_correction_source": "profiles/r02/calib (tools/calib/run.sh); MI355X_MICROARCH.md HBM section",
