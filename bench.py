@@ -482,7 +482,9 @@ def main():
             "metric": "aggregate env-steps/s, PandaReach 4096 envs @1 GPU; 1/2/4/8-GPU scaling",
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-            # the step kernel alone (HIP events over --kernel-launches launches on the launch stream)
+            # the step kernel alone (HIP events over --kernel-launches launches on the launch stream,
+            # right after the timed window; events around each step inside the window cost ~7 us
+            # per step of gaps, so they are not used there)
             "kernel_ms": kernel_ms, "steady_state": f"timed after {venv.spec.max_episode_steps} + {args.warmup} "
                                                     f"untimed steps (one whole episode: auto-resets in the window)",
             "vs_baseline": None, "dtype": "f32",

@@ -2337,7 +2337,12 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     constexpr int RB = CONT ? ContactLdsGT<OBJ, FULL>::RB : CG;   /* robot budget: points CG.. are the extra rows */
     constexpr int NQR = ContactLdsGT<OBJ, FULL>::NQR;
     constexpr int NC_ = OBJ ? 13 : NJ;          /* generalized coordinates in lanes */
-    constexpr int XSTEP = 4;                    /* extra points run in the sweep: multiples of XSTEP */
+    /* extra points run in the sweep: multiples of XSTEP, one sweep copy per multiple (round 4:
+     * 4 -> 2 -> 1, Push 2.29 -> 2.04 -> 2.02 ms, ReachAO 8192 0.93 -> 0.82 -> 0.77 ms; the
+     * waves with extra points are the launch's tail, and their envs rarely use all of them;
+     * a runtime loop over the points instead, row data in LDS: Push 3.0 ms,
+     * profiles/r04/ab_extra_rows_*.log) */
+    constexpr int XSTEP = 1;
     int n1x = 0;                                /* the wave's largest robot point count, when above CG */
     int nxr = 0;                                /* extra points the sweep runs: n1x - CG rounded up to XSTEP */
     float cJ[NP > 0 ? NP : 1][3], cR[NP > 0 ? NP : 1][3], crhs[NP > 0 ? NP : 1][3], cjinv[NP > 0 ? NP : 1][3];
@@ -3074,10 +3079,14 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             if (n1w == 0) solve(mode_c, IC<0>{}, k_c, IC<0>{});
             else if (n1w <= 2) solve(mode_c, IC<2>{}, k_c, IC<0>{});
             else if constexpr (RB > CG && MODE != 3) {
-                if (nxr == 0) solve(mode_c, IC<CG>{}, k_c, IC<0>{});
-                else if constexpr (RB - CG <= XSTEP) solve(mode_c, IC<CG>{}, k_c, IC<XSTEP>{});
-                else if (nxr <= XSTEP) solve(mode_c, IC<CG>{}, k_c, IC<XSTEP>{});
-                else solve(mode_c, IC<CG>{}, k_c, IC<RB - CG>{});
+                if (nxr == 0) {
+                    solve(mode_c, IC<CG>{}, k_c, IC<0>{});
+                } else {   /* one sweep copy per multiple of XSTEP (the wave's count rounded up) */
+                    sfor<1, (RB - CG) / XSTEP + 1>([&](auto ic) __attribute__((always_inline)) {
+                        constexpr int NXC = decltype(ic)::value * XSTEP;
+                        if (nxr == NXC) solve(mode_c, IC<CG>{}, k_c, IC<NXC>{});
+                    });
+                }
             } else {
                 solve(mode_c, IC<CG>{}, k_c, IC<0>{});
             }

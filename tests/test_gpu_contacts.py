@@ -192,18 +192,18 @@ def test_reach_with_table_contacts(pg, oracle, lanes):
 def test_random_policy_one_step_parity(pg, oracle, env_id, lanes):
     """p99 <= 1e-5 in both layouts, p99.9 inside the fp32 envelope (round 3: <= 1e-4; with the tool
     bar's friction of round 4 the one-lane Push EE p99.9 measured 1.1e-4 against the fp32 oracle's
-    2.8e-4).  One lane per env: max <= 1e-3.  The
-    16-lane layout (lane-parallel bias / CRBA: a different summation order) may exceed 1e-3 only
-    at a contact bifurcation, and only where the oracle itself, from its input perturbed by 1e-7
-    relative (the fp32 rounding scale), moves by at least the device's deviation (max over 32
-    trials); at most one such sample per 2000."""
+    2.8e-4).  Either layout may exceed 1e-3 (up to 1e-2) only at a contact bifurcation, and only
+    where the oracle itself, from its input perturbed by 1e-7 relative (the fp32 rounding scale),
+    moves by at least the device's deviation (max over 32 trials); at most one such sample per
+    2000.  (Round 3 held the one-lane layout to max <= 1e-3; with the tool bar's friction one
+    one-lane Push sample of 12544 reached 1.7e-3.)"""
     outl, env = [], {}
     ee, ag, final = _one_step_errors(pg, oracle, env_id, 256, 50, 21, lanes=lanes, outliers=outl, envelope=env)
     cfg, _keep = outl.pop()
     for name, e, f in (("ee", ee, env["ee"]), ("object", ag, env["ag"])):
         assert np.percentile(e, 99) <= 1e-5, (name, np.percentile(e, 99))
         _inside_envelope(name, e, f, pcts=(99.9,))
-        assert e.max() <= (1e-2 if lanes == 16 else OUTLIER), (name, e.max())
+        assert e.max() <= 1e-2, (name, e.max())
     assert len(outl) <= ee.size // 2000, len(outl)
     for rec in outl:
         s_ee, s_ag = _self_sensitivity(oracle, cfg, rec, trials=32)
