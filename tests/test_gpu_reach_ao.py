@@ -115,7 +115,7 @@ def test_device_reset_draws_match_oracle(pg, oracle):
 # (min |margin| over the step's checks; the contact rows hold a link that touches an obstacle at
 # the surface, so a touching link's margin sits at rounding level and the substep whose rounding
 # first reads <= 0 decides the collision -- in the reference as here).
-FLIP_MARGIN = 1e-5
+FLIP_MARGIN = 1e-6   # (round 4: 0 flips in 24576 random-policy env-steps and in the driven-in case)
 
 
 def test_one_step_parity_random_actions(pg, oracle, lanes):
@@ -124,7 +124,8 @@ def test_one_step_parity_random_actions(pg, oracle, lanes):
     venv.reset_tensors(seed=1000)
     ref = oracle.OracleVecEnv(venv._cfg, n)
     errs, flips, flip_margins, colls = [], 0, [], 0
-    for t in range(6):
+    steps = 24
+    for t in range(steps):
         _state_to_oracle(venv, ref)
         a = venv.sample_actions(t).clone()
         venv.step_tensors(a)
@@ -145,9 +146,10 @@ def test_one_step_parity_random_actions(pg, oracle, lanes):
         assert np.array_equal(venv.reward.cpu().numpy()[keep], out["reward"][keep])
         errs.append(np.abs(obs[keep] - out["obs"][keep]))
     e = np.concatenate(errs)
-    print(f"collision decisions: {colls} device collisions in {6 * n} env-steps, {flips} flipped against "
+    print(f"collision decisions: {colls} device collisions in {steps * n} env-steps, {flips} flipped against "
           f"the oracle, oracle |margin| at the flips max {max(flip_margins, default=0.0):.2e}")
-    assert flips <= n * 6 // 200
+    assert colls > 0
+    assert flips <= n * steps // 200
     assert np.percentile(e[:, 0:3].max(1), 99) <= 1e-5 and e[:, 0:3].max() <= 1e-3
     assert np.percentile(e[:, 20:29].max(1), 99) <= 1e-5 and e[:, 20:29].max() <= 1e-3
     venv.close()
