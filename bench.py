@@ -438,6 +438,9 @@ def main():
     for k in range(K):
         acts[k].copy_(venv.sample_actions(base + k))   # a fresh Philox draw per launch, as in the timed loop
     stream = torch.cuda.current_stream(dev)
+    # first-to-last span of K back-to-back launches per launch (launch gaps included; event pairs
+    # around each launch measured 3 % above rocprof's kernel average: an event record adds its own
+    # gap, profiles/r04/bench_v3.json)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
     ev0.record(stream)
@@ -445,7 +448,7 @@ def main():
         venv.step_tensors(acts[k])
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    kernel_ms = ev0.elapsed_time(ev1) / args.kernel_launches
+    kernel_ms = ev0.elapsed_time(ev1) / K
     # configs[4]: ReachAO sharded over every rank (collective timing: all ranks take part)
     ao = None if args.no_ao else sharded_leg(dev, "PandaReachAO-v3", args.ao_envs, args.task_steps, 20, dist, rank,
                                             world, coll_dev)
@@ -482,9 +485,9 @@ def main():
             "metric": "aggregate env-steps/s, PandaReach 4096 envs @1 GPU; 1/2/4/8-GPU scaling",
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-            # the step kernel alone (HIP events over --kernel-launches launches on the launch stream,
-            # right after the timed window; events around each step inside the window cost ~7 us
-            # per step of gaps, so they are not used there)
+            # the step kernel alone: HIP events over --kernel-launches back-to-back launches on the launch
+            # stream right after the timed window (launch gaps included; rocprof's kernel average,
+            # profiles/, is the gap-free duration)
             "kernel_ms": kernel_ms, "steady_state": f"timed after {venv.spec.max_episode_steps} + {args.warmup} "
                                                     f"untimed steps (one whole episode: auto-resets in the window)",
             "vs_baseline": None, "dtype": "f32",

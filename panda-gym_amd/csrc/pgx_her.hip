@@ -34,6 +34,7 @@
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 
 #include "../../include/pgx.h"
 #include "pgx_common.h"
@@ -304,6 +305,122 @@ __global__ __launch_bounds__(64) void sample_kernel(RingPtrs p, RingDims d, int6
     }
 }
 
+/* sample(), records of at most 16 float4 columns (the batch row plus ep_start / ep_length: every
+ * task but ReachAO's 56-float observation): each record is read from HBM once.  Phase A: lane i
+ * draws sample i (Philox, valid-list lookup).  Phase B: 16-lane groups load the 64 records into
+ * registers (lane c of a group holds column c of 16 records, one float4 load each) and stage the
+ * fields the relabelling reads -- next_achieved_goal, ep_start, ep_length -- in LDS.  Phase C:
+ * lane i relabels sample i (future goal gather, reward) from the staged fields.  Phase D: the
+ * groups patch desired goals and reward and store the rows.  (sample_kernel above reads the
+ * episode fields in its first phase and the record again in its copy: the record's second line
+ * twice, 556 B of reads per PickAndPlace sample for 358 B of data, profiles/pmc_sample_kernel.json
+ * of round 4.)  Same draws, same arithmetic: the rows are bit-identical. */
+constexpr int REG_COLS = 16;
+__global__ __launch_bounds__(64) void sample_kernel_reg(RingPtrs p, RingDims d, int64_t B, int64_t nb_virtual,
+                                                        uint64_t seed, uint64_t draw, int32_t reward_type,
+                                                        int32_t strategy, float thr, pgx_replay_batch o) {
+    __shared__ Draw dr[64];
+    __shared__ float stg[64][6];   /* next_achieved_goal [3], ep_start, ep_length (bits) */
+    const int lane = threadIdx.x;
+    const int64_t b0 = (int64_t)blockIdx.x * 64;
+    const int N = d.n, C = d.cap;
+    const int32_t nv = *p.n_valid;
+    const int ncol = (d.epl + 4) / 4;   /* columns holding the row and the episode fields */
+    /* phase A */
+    const int64_t b = b0 + lane;
+    double u1 = 0.0;
+    {
+        Draw w{};
+        w.rec = -1;
+        if (b < B) {
+            const bool her = b < nb_virtual;
+            w.row = her ? B - nb_virtual + b : b - nb_virtual;
+            w.her = her;
+            if (nv > 0) {
+                uint32_t r[4];
+                philox((uint32_t)b, (uint32_t)(b >> 32), (uint32_t)draw, TAG_HER ^ (uint32_t)(draw >> 32),
+                       (uint32_t)seed, (uint32_t)(seed >> 32), r);
+                const double u0 = u53(r[0], r[1]);
+                u1 = u53(r[2], r[3]);
+                int64_t j = (int64_t)(u0 * (double)nv);
+                if (j >= nv) j = nv - 1;
+                w.rec = p.valid[j];
+            }
+        }
+        dr[lane] = w;
+    }
+    __syncthreads();
+    /* phase B: lane 16 q + c holds column c of records q, q + 4, ..., q + 60 */
+    const int c = lane % GROUP, q = lane / GROUP;
+    float4 v[64 / (64 / GROUP)];
+#pragma unroll
+    for (int k = 0; k < 64 / (64 / GROUP); k++) {
+        const int sm = q + k * (64 / GROUP);
+        const int64_t rec = dr[sm].rec;
+        v[k] = (c < ncol && rec >= 0 && b0 + sm < B) ? *reinterpret_cast<const float4*>(p.rec + rec * d.R + 4 * c)
+                                                    : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const float vv[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int f = 4 * c + u;
+            if (f >= d.nag && f < d.nag + 3) stg[sm][f - d.nag] = vv[u];
+            if (f == d.eps) stg[sm][3] = vv[u];
+            if (f == d.epl) stg[sm][4] = vv[u];
+        }
+    }
+    __syncthreads();
+    /* phase C: lane i relabels sample i */
+    if (b < B) {
+        Draw& w = dr[lane];
+        int32_t slot = -1, env = -1, goal_slot = -1;
+        if (w.rec >= 0) {
+            const int32_t flat = (int32_t)w.rec;
+            slot = flat / N;
+            env = flat % N;
+            if (w.her) {
+                const int32_t start = fbits(stg[lane][3]), len = fbits(stg[lane][4]);
+                const int32_t cur = ((slot - start) % C + C) % C;
+                int32_t t_in;
+                if (strategy == PGX_HER_FINAL) t_in = len - 1;
+                else if (strategy == PGX_HER_EPISODE) t_in = (int32_t)(u1 * (double)len);
+                else t_in = cur + (int32_t)(u1 * (double)(len - cur));
+                goal_slot = (t_in + start) % C;
+                const float* gr = p.rec + ((size_t)goal_slot * N + env) * d.R + d.nag;
+                w.goal[0] = gr[0]; w.goal[1] = gr[1]; w.goal[2] = gr[2];
+                const float nag[3] = {stg[lane][0], stg[lane][1], stg[lane][2]};
+                w.reward = reward_f32(distance_f32_f32(nag, w.goal), reward_type, thr);
+            }
+        }
+        if (o.slot) o.slot[w.row] = slot;
+        if (o.env) o.env[w.row] = env;
+        if (o.goal_slot) o.goal_slot[w.row] = goal_slot;
+    }
+    __syncthreads();
+    /* phase D: patch and store (as sample_kernel's finish) */
+    typedef float f4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int k = 0; k < 64 / (64 / GROUP); k++) {
+        const int sm = q + k * (64 / GROUP);
+        if (4 * c >= d.S || b0 + sm >= B) continue;
+        const Draw& w = dr[sm];
+        float vv[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+        if (w.rec >= 0 && w.her) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int f = 4 * c + u;
+                if (f >= d.dg && f < d.dg + 3) vv[u] = w.goal[f - d.dg];
+                else if (f >= d.ndg && f < d.ndg + 3) vv[u] = w.goal[f - d.ndg];
+                else if (f == d.rew) vv[u] = w.reward;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (4 * c + u >= d.eps) vv[u] = 0.0f;
+        const f4v nv4 = {vv[0], vv[1], vv[2], vv[3]};
+        __builtin_nontemporal_store(nv4, reinterpret_cast<f4v*>(o.rows + w.row * d.S + 4 * c));
+    }
+}
+
 }  // namespace
 
 struct pgx_replay {
@@ -413,9 +530,14 @@ int pgx_replay_sample(pgx_replay_handle h, int64_t batch, uint64_t draw, pgx_rep
     if (((uintptr_t)out->rows & 15) != 0) return pgx_set_error(PGX_E_INVALID, "pgx_replay_sample: rows not 16 B aligned");
     if (h->added == 0) return pgx_set_error(PGX_E_INVALID, "pgx_replay_sample: buffer is empty");
     const int64_t nb_virtual = (int64_t)(h->cfg.her_ratio * (double)batch);
-    hipLaunchKernelGGL(sample_kernel, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0, (hipStream_t)stream, h->p,
-                       h->d, batch, nb_virtual, h->cfg.seed, draw, h->cfg.reward_type, h->cfg.strategy,
-                       (float)h->cfg.distance_threshold, *out);
+    if ((h->d.epl + 4) / 4 <= REG_COLS && !std::getenv("PGX_HER_TWO_PASS"))   /* records read once */
+        hipLaunchKernelGGL(sample_kernel_reg, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
+                           h->p, h->d, batch, nb_virtual, h->cfg.seed, draw, h->cfg.reward_type, h->cfg.strategy,
+                           (float)h->cfg.distance_threshold, *out);
+    else   /* wider records (ReachAO's 56-float observation) */
+        hipLaunchKernelGGL(sample_kernel, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0, (hipStream_t)stream, h->p,
+                           h->d, batch, nb_virtual, h->cfg.seed, draw, h->cfg.reward_type, h->cfg.strategy,
+                           (float)h->cfg.distance_threshold, *out);
     return hipGetLastError() == hipSuccess ? PGX_OK : pgx_set_error(PGX_E_HIP, "pgx_replay_sample: launch failed");
 }
 

@@ -72,6 +72,23 @@ def test_sample_bit_exact_vs_oracle(her_mod, steps):
     buf.close()
 
 
+@pytest.mark.parametrize("two_pass", [False, True])
+@pytest.mark.parametrize("od,ad", [(19, 4), (18, 3), (56, 7)])
+def test_both_sample_kernels_bit_exact(her_mod, monkeypatch, od, ad, two_pass):
+    """libpgx samples records of <= 16 float4 columns with the single-read kernel (sample_kernel_reg)
+    and wider ones (ReachAO's 56-float observation) with the two-pass kernel; PGX_HER_TWO_PASS
+    forces the latter.  Both bit-exact against the restatement at PickAndPlace's, Push's and
+    ReachAO's dimensions."""
+    if two_pass:
+        monkeypatch.setenv("PGX_HER_TWO_PASS", "1")
+    rng = np.random.default_rng(od)
+    buf, orc = _pair(her_mod, N=48, C=23, od=od, ad=ad)
+    _feed(buf, orc, 60, rng)
+    for draw in range(2):
+        _compare(buf, orc, 2053, draw)
+    buf.close()
+
+
 @pytest.mark.parametrize("strategy,reward_type", [("final", "sparse"), ("episode", "dense"), ("future", "dense")])
 def test_strategies_and_dense_reward(her_mod, strategy, reward_type):
     rng = np.random.default_rng(7)
