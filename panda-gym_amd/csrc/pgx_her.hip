@@ -316,20 +316,23 @@ __global__ __launch_bounds__(64) void sample_kernel(RingPtrs p, RingDims d, int6
  * twice, 556 B of reads per PickAndPlace sample for 358 B of data, profiles/pmc_sample_kernel.json
  * of round 4.)  Same draws, same arithmetic: the rows are bit-identical. */
 constexpr int REG_COLS = 16;
+/* SPB: samples per 64-lane block (lane i < SPB draws sample i); each lane holds SPB / 4 records'
+ * columns in registers */
+template <int SPB>
 __global__ __launch_bounds__(64) void sample_kernel_reg(RingPtrs p, RingDims d, int64_t B, int64_t nb_virtual,
                                                         uint64_t seed, uint64_t draw, int32_t reward_type,
                                                         int32_t strategy, float thr, pgx_replay_batch o) {
-    __shared__ Draw dr[64];
-    __shared__ float stg[64][6];   /* next_achieved_goal [3], ep_start, ep_length (bits) */
+    __shared__ Draw dr[SPB];
+    __shared__ float stg[SPB][6];   /* next_achieved_goal [3], ep_start, ep_length (bits) */
     const int lane = threadIdx.x;
-    const int64_t b0 = (int64_t)blockIdx.x * 64;
+    const int64_t b0 = (int64_t)blockIdx.x * SPB;
     const int N = d.n, C = d.cap;
     const int32_t nv = *p.n_valid;
     const int ncol = (d.epl + 4) / 4;   /* columns holding the row and the episode fields */
     /* phase A */
     const int64_t b = b0 + lane;
     double u1 = 0.0;
-    {
+    if (lane < SPB) {
         Draw w{};
         w.rec = -1;
         if (b < B) {
@@ -350,11 +353,11 @@ __global__ __launch_bounds__(64) void sample_kernel_reg(RingPtrs p, RingDims d, 
         dr[lane] = w;
     }
     __syncthreads();
-    /* phase B: lane 16 q + c holds column c of records q, q + 4, ..., q + 60 */
+    /* phase B: lane 16 q + c holds column c of records q, q + 4, ..., q + SPB - 4 */
     const int c = lane % GROUP, q = lane / GROUP;
-    float4 v[64 / (64 / GROUP)];
+    float4 v[SPB / (64 / GROUP)];
 #pragma unroll
-    for (int k = 0; k < 64 / (64 / GROUP); k++) {
+    for (int k = 0; k < SPB / (64 / GROUP); k++) {
         const int sm = q + k * (64 / GROUP);
         const int64_t rec = dr[sm].rec;
         v[k] = (c < ncol && rec >= 0 && b0 + sm < B) ? *reinterpret_cast<const float4*>(p.rec + rec * d.R + 4 * c)
@@ -370,7 +373,7 @@ __global__ __launch_bounds__(64) void sample_kernel_reg(RingPtrs p, RingDims d, 
     }
     __syncthreads();
     /* phase C: lane i relabels sample i */
-    if (b < B) {
+    if (lane < SPB && b < B) {
         Draw& w = dr[lane];
         int32_t slot = -1, env = -1, goal_slot = -1;
         if (w.rec >= 0) {
@@ -399,7 +402,7 @@ __global__ __launch_bounds__(64) void sample_kernel_reg(RingPtrs p, RingDims d, 
     /* phase D: patch and store (as sample_kernel's finish) */
     typedef float f4v __attribute__((ext_vector_type(4)));
 #pragma unroll
-    for (int k = 0; k < 64 / (64 / GROUP); k++) {
+    for (int k = 0; k < SPB / (64 / GROUP); k++) {
         const int sm = q + k * (64 / GROUP);
         if (4 * c >= d.S || b0 + sm >= B) continue;
         const Draw& w = dr[sm];
@@ -530,10 +533,17 @@ int pgx_replay_sample(pgx_replay_handle h, int64_t batch, uint64_t draw, pgx_rep
     if (((uintptr_t)out->rows & 15) != 0) return pgx_set_error(PGX_E_INVALID, "pgx_replay_sample: rows not 16 B aligned");
     if (h->added == 0) return pgx_set_error(PGX_E_INVALID, "pgx_replay_sample: buffer is empty");
     const int64_t nb_virtual = (int64_t)(h->cfg.her_ratio * (double)batch);
-    if ((h->d.epl + 4) / 4 <= REG_COLS && !std::getenv("PGX_HER_TWO_PASS"))   /* records read once */
-        hipLaunchKernelGGL(sample_kernel_reg, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
-                           h->p, h->d, batch, nb_virtual, h->cfg.seed, draw, h->cfg.reward_type, h->cfg.strategy,
-                           (float)h->cfg.distance_threshold, *out);
+    const char* spb = std::getenv("PGX_HER_SPB");
+    if ((h->d.epl + 4) / 4 <= REG_COLS && !std::getenv("PGX_HER_TWO_PASS")) {   /* records read once */
+        if (spb && std::atoi(spb) == 64)
+            hipLaunchKernelGGL(sample_kernel_reg<64>, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0,
+                               (hipStream_t)stream, h->p, h->d, batch, nb_virtual, h->cfg.seed, draw,
+                               h->cfg.reward_type, h->cfg.strategy, (float)h->cfg.distance_threshold, *out);
+        else
+            hipLaunchKernelGGL(sample_kernel_reg<32>, dim3((unsigned)((batch + 31) / 32)), dim3(64), 0,
+                               (hipStream_t)stream, h->p, h->d, batch, nb_virtual, h->cfg.seed, draw,
+                               h->cfg.reward_type, h->cfg.strategy, (float)h->cfg.distance_threshold, *out);
+    }
     else   /* wider records (ReachAO's 56-float observation) */
         hipLaunchKernelGGL(sample_kernel, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0, (hipStream_t)stream, h->p,
                            h->d, batch, nb_virtual, h->cfg.seed, draw, h->cfg.reward_type, h->cfg.strategy,

@@ -1,5 +1,6 @@
 #!/bin/bash
-# HER sample kernel: the single-read kernel (default) against the two-pass one (PGX_HER_TWO_PASS),
+# HER sample kernel: the single-read kernel at 32 (default) and 64 samples per block (PGX_HER_SPB)
+# against the two-pass one (PGX_HER_TWO_PASS),
 # three alternating runs each of bench.py's HER leg; then the HER GPU tests on the default.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -7,12 +8,14 @@ mkdir -p gpurun_out
 OUT=gpurun_out/her_ab_r4.log
 : > $OUT
 for rep in 1 2 3; do
-  for mode in single two; do
-    if [ $mode = two ]; then export PGX_HER_TWO_PASS=1; else unset PGX_HER_TWO_PASS; fi
+  for mode in spb32 spb64 two; do
+    unset PGX_HER_TWO_PASS PGX_HER_SPB
+    if [ $mode = two ]; then export PGX_HER_TWO_PASS=1; fi
+    if [ $mode = spb64 ]; then export PGX_HER_SPB=64; fi
     timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-tasks --no-ao --no-cpu-baseline --kernel-launches 10 > gpurun_out/her_b.json 2> gpurun_out/her_b.err || { tail -5 gpurun_out/her_b.err; exit 1; }
     python -c "import json,sys; d=json.loads(open('gpurun_out/her_b.json').read().strip().splitlines()[-1])['her_relabel']; print('$mode', d['ms_per_call'], d['value'])" >> $OUT
   done
 done
-unset PGX_HER_TWO_PASS
+unset PGX_HER_TWO_PASS PGX_HER_SPB
 cat $OUT
 timeout -k 10 400 python -u -m pytest -v --timeout 240 --timeout-method thread -m gpu tests/test_gpu_her.py > gpurun_out/pytest_her.log 2>&1; tail -3 gpurun_out/pytest_her.log
