@@ -186,12 +186,18 @@ def her_leg(dev, calls: int, with_cpu: bool):
     e1.record(stream)
     torch.cuda.synchronize(dev)
     ms = e0.elapsed_time(e1) / calls
+    # 10 adds back to back (the ring holds 64 slots, 50 used: no episode is overwritten), HIP events
+    # over the span; the host's Python path per add alone (argument checks, ctypes) beside it
+    n_add = 10
     torch.cuda.synchronize(dev)
+    t_host = time.perf_counter()
     e0.record(stream)
-    buf.add_tensors(*obs_args, zero, zero)
+    for _ in range(n_add):
+        buf.add_tensors(*obs_args, zero, zero)
     e1.record(stream)
+    t_host = (time.perf_counter() - t_host) / n_add
     torch.cuda.synchronize(dev)
-    add_ms = e0.elapsed_time(e1)
+    add_ms = e0.elapsed_time(e1) / n_add
     nbv = int(buf.her_ratio * B)
     n_valid = int(buf._arrays()[2].item())
     if n_valid != N * HER_EP:
@@ -203,7 +209,7 @@ def her_leg(dev, calls: int, with_cpu: bool):
         prof = None
     res = {"metric": "HER relabels/s (virtual transitions, future, her_ratio 0.8)", "value": nbv / (ms * 1e-3),
            "unit": "relabels/s", "samples_per_s": B / (ms * 1e-3), "ms_per_call": ms, "calls": calls,
-           "ms_per_add": add_ms,
+           "ms_per_add": add_ms, "host_ms_per_add_issue": t_host * 1e3,
            "config": {"workload": f"HER ring {N} envs x {HER_EP}-step episodes ({C} slots), obs {HER_OD}, "
                                   f"action {HER_AD}, B={B} "
                                   f"(BASELINE configs[3] relabel leg)", "batch": B, "relabels_per_call": nbv},

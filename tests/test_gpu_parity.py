@@ -368,3 +368,37 @@ def test_two_wave_variant_matches_one_wave_shards(pg, env_id):
         assert torch.equal(torch.cat([v.truncated for v in parts]), big.truncated), t
     for v in [big] + parts:
         v.close()
+
+
+@pytest.mark.parametrize("env_id", ["PandaReach-v3", "PandaPush-v3", "PandaPickAndPlace-v3", "PandaReachAO-v3"])
+@pytest.mark.parametrize("n", [3, 67])
+def test_ragged_batches_match_oracle(pg, oracle, env_id, n, lanes):
+    """Batches that fill neither the 16-lane layout's 4-env waves nor the one-lane layout's 64-env
+    waves: the envs of the last, partial wave step like every other -- three random steps from the
+    same state against the oracle, every output row (observation, goals, reward, flags) checked,
+    so a write past env n - 1 into the next output array would show."""
+    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=17, lanes_per_env=lanes)
+    venv.reset_tensors(seed=17)
+    ref = oracle.OracleVecEnv(venv._cfg, n)
+    for t in range(3):
+        _state_to_oracle(venv, ref)
+        acts = venv.sample_actions(t).clone()
+        venv.step_tensors(acts)
+        ao = env_id == "PandaReachAO-v3"
+        out = ref.step(acts.cpu().numpy(), margins=ao)
+        obs, ag, dg, rew, succ = _gpu_out(venv)
+        tr = venv.truncated.cpu().numpy()
+        # ReachAO: a collision decision may differ only where the oracle's own margin sat at
+        # rounding level (test_gpu_reach_ao.py, FLIP_MARGIN)
+        same = tr == out["truncated"]
+        if ao:
+            assert np.all(same | (out["margin_abs"] < 1e-6))
+        else:
+            assert np.all(same)
+        keep = same & (tr == 0)
+        assert obs.shape == out["obs"].shape and np.all(np.isfinite(obs))
+        assert np.abs(obs[keep, :3] - out["obs"][keep, :3]).max(initial=0.0) <= OBS_TOL
+        assert np.abs(ag[keep] - out["ag"][keep]).max(initial=0.0) <= OBS_TOL
+        assert np.array_equal(dg[keep], out["dg"][keep])
+        assert np.array_equal(rew[keep], out["reward"][keep])
+    venv.close()
