@@ -510,6 +510,124 @@ def _view(addr: int, shape, dtype, device):
 
 
 # --------------------------------------------------------- single env
+class _RobotView:
+    """Read-only `env.robot` (Panda, panda.py:264-312): the state the kernels keep for the one env.
+    Control goes through `env.step` (set_action and the motors run inside the step kernel)."""
+
+    def __init__(self, env: "PandaEnv"):
+        self._env = env
+
+    def _obs(self) -> np.ndarray:
+        return self._env._vec.obs[0].cpu().numpy().copy()
+
+    @property
+    def neutral_joint_values(self) -> np.ndarray:   # panda.py:67
+        return np.array(abi.NEUTRAL_Q, dtype=np.float64)
+
+    @property
+    def block_gripper(self) -> bool:
+        return bool(self._env.spec.block_gripper)
+
+    def get_obs(self) -> np.ndarray:
+        """Panda.get_obs (panda.py:264-288): EE position, EE velocity (+ fingers width; ReachAO:
+        + q, qd, the "js" observation)."""
+        o = self._obs()
+        n = 20 if self._env.spec.task == abi.TASK_REACH_AO else 6 + (0 if self.block_gripper else 1)
+        return o[:n]
+
+    def get_ee_position(self) -> np.ndarray:   # panda.py:306-308 (getLinkState's cached pose)
+        return self._obs()[0:3]
+
+    def get_ee_velocity(self) -> np.ndarray:   # panda.py:310-312
+        return self._obs()[3:6]
+
+    def get_joint_angle(self, joint: int) -> float:   # core.py:151-160 (fixed finger joints: 0)
+        st = self._env._vec.state()
+        return float(st["q"][joint, 0].item()) if joint < st["q"].shape[0] else 0.0
+
+    def get_joint_velocity(self, joint: int) -> float:
+        st = self._env._vec.state()
+        return float(st["qd"][joint, 0].item()) if joint < st["qd"].shape[0] else 0.0
+
+    def get_fingers_width(self) -> float:   # panda.py:300-304: custom_0's finger joints are fixed
+        return 0.0
+
+
+class _TaskView:
+    """Read-only `env.task` (Reach / Push / PickAndPlace / ReachAO): goal, achieved goal, the task
+    observation, obstacles, and the task's is_success / compute_reward."""
+
+    def __init__(self, env: "PandaEnv"):
+        self._env = env
+
+    @property
+    def goal(self) -> np.ndarray:   # Task.goal: fp64, as the reference keeps it
+        return self._env._vec.state()["goal"][:, 0].cpu().numpy().astype(np.float64)
+
+    def get_goal(self) -> np.ndarray:   # core.py:236-241
+        return self.goal.copy()
+
+    def get_achieved_goal(self) -> np.ndarray:
+        return self._env._vec.achieved_goal[0].cpu().numpy().copy()
+
+    def get_obs(self) -> np.ndarray:
+        o = self._env._vec.obs[0].cpu().numpy().copy()
+        return o[len(self._env.robot.get_obs()):]
+
+    @property
+    def distance_threshold(self) -> float:
+        return float(self._env.spec.distance_threshold)
+
+    @property
+    def reward_type(self) -> str:
+        return self._env._vec.reward_type
+
+    @property
+    def obstacles(self) -> Optional[np.ndarray]:
+        """ReachAO: the obstacle centres [6, 3] (inactive ones parked at (99.9, 99.9, -99.9))."""
+        st = self._env._vec.state()
+        if "obstacles" not in st:
+            return None
+        return st["obstacles"][:18, 0].cpu().numpy().reshape(6, 3).astype(np.float64)
+
+    def is_success(self, achieved_goal, desired_goal, info=None) -> np.ndarray:
+        """utils.distance < distance_threshold (reach.py:80-82)."""
+        a, b = np.asarray(achieved_goal), np.asarray(desired_goal)   # (numpy's promotion, as utils.py:4-16)
+        d = np.round(np.linalg.norm(a - b, axis=-1), 6)
+        return np.array(d < self.distance_threshold, dtype=bool)
+
+    def compute_reward(self, achieved_goal, desired_goal, info=None):
+        return self._env.compute_reward(achieved_goal, desired_goal, info)
+
+
+class _SimView:
+    """Read-only `env.sim` (the PyBullet facade, pybullet.py:15-102): timing and the state ids."""
+
+    def __init__(self, env: "PandaEnv"):
+        self._env = env
+
+    @property
+    def timestep(self) -> float:   # pybullet.py:50
+        return float(self._env._vec._params.dt)
+
+    @property
+    def n_substeps(self) -> int:
+        return int(self._env._vec._params.n_substeps)
+
+    @property
+    def dt(self) -> float:   # pybullet.py:63-66
+        return self.timestep * self.n_substeps
+
+    def save_state(self) -> int:
+        return self._env.save_state()
+
+    def restore_state(self, state_id: int) -> None:
+        self._env.restore_state(state_id)
+
+    def remove_state(self, state_id: int) -> None:
+        self._env.remove_state(state_id)
+
+
 class PandaEnv:
     """One env with the RobotTaskEnv + TimeLimit surface (gym.make("PandaReach-v3") in the reference)."""
 
@@ -522,6 +640,8 @@ class PandaEnv:
         self.spec = self._vec.spec
         self.observation_space = self._vec.observation_space
         self.action_space = self._vec.action_space
+        # RobotTaskEnv's attributes callers read (evaluation/evaluate.py:242-247): read-only views
+        self.robot, self.task, self.sim = _RobotView(self), _TaskView(self), _SimView(self)
 
     def reset(self, seed: Optional[int] = None, options: Optional[dict] = None):
         r = seeded_reset(self.spec, seed)

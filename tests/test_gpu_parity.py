@@ -402,3 +402,35 @@ def test_ragged_batches_match_oracle(pg, oracle, env_id, n, lanes):
         assert np.array_equal(dg[keep], out["dg"][keep])
         assert np.array_equal(rew[keep], out["reward"][keep])
     venv.close()
+
+
+@pytest.mark.parametrize("env_id", ["PandaReach-v3", "PandaPickAndPlace-v3", "PandaReachAO-v3"])
+def test_single_env_robot_task_sim_views(pg, env_id):
+    """`env.robot`, `env.task`, `env.sim` of the single-env wrapper (RobotTaskEnv's attributes,
+    SURVEY.md 8b): read-only views that agree with the observation the step returned and with the
+    device state."""
+    env = pg.make(env_id)
+    obs, _ = env.reset(seed=123)
+    a = env.action_space.sample() * 0.0 + 0.3
+    obs, _, _, _, info = env.step(a)
+    o = obs["observation"]
+    assert np.array_equal(env.robot.get_ee_position(), o[0:3])
+    assert np.array_equal(env.robot.get_ee_velocity(), o[3:6])
+    assert np.array_equal(np.concatenate([env.robot.get_obs(), env.task.get_obs()]), o)
+    assert np.array_equal(env.task.get_achieved_goal(), obs["achieved_goal"])
+    assert np.array_equal(env.task.goal.astype(np.float32), obs["desired_goal"])
+    assert env.task.goal.dtype == np.float64
+    st = env._vec.state()
+    for j in range(7):
+        assert env.robot.get_joint_angle(j) == float(st["q"][j, 0].item())
+    assert env.robot.get_joint_angle(9) == 0.0 and env.robot.get_fingers_width() == 0.0
+    assert bool(env.task.is_success(obs["achieved_goal"], env.task.goal)) == info["is_success"]
+    assert env.sim.dt == pytest.approx(0.04) and env.sim.n_substeps == 20
+    if env_id == "PandaReachAO-v3":
+        assert env.task.obstacles.shape == (6, 3) and len(env.robot.get_obs()) == 20
+    else:
+        assert env.task.obstacles is None
+    sid = env.sim.save_state()
+    env.sim.restore_state(sid)
+    env.sim.remove_state(sid)
+    env.close()
