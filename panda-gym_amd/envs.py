@@ -411,6 +411,9 @@ class PandaVecEnv:
         stream = torch.cuda.current_stream(self.device)
         hs["packed"].copy_(self._outbuf, non_blocking=True)   # every output, one DMA
         hs["errors"].copy_(hs["errors_dev"], non_blocking=True)
+        # SB3's per-env infos list is built while the step kernel runs: a fresh dict per env copied
+        # in C from the common template, the few envs whose flags differ patched after the sync
+        infos: List[Dict[str, Any]] = list(map(dict.copy, [_INFO_TEMPLATES[0]] * self.num_envs))
         stream.synchronize()
         if hs["errors"].item():
             self.raise_device_errors(int(hs["errors"].item()))
@@ -420,9 +423,9 @@ class PandaVecEnv:
         fl = hs["flags"].numpy() != 0
         sc, te, tr, col = fl[0], fl[1].copy(), fl[2].copy(), fl[3]
         d = te | tr
-        # a fresh dict per env, copied in C from the four templates (30 % faster than literals)
-        code = (sc.view(np.uint8) + 2 * col.view(np.uint8)).tolist()
-        infos: List[Dict[str, Any]] = list(map(dict.copy, map(_INFO_TEMPLATES.__getitem__, code)))
+        code = sc.view(np.uint8) + 2 * col.view(np.uint8)
+        for i in np.flatnonzero(code).tolist():
+            infos[i] = _INFO_TEMPLATES[int(code[i])].copy()
         idx = np.nonzero(d)[0]
         if len(idx):
             tobs, tag, tdg = hs["t_observation"].numpy(), hs["t_achieved_goal"].numpy(), hs["t_desired_goal"].numpy()

@@ -281,7 +281,7 @@ def test_sb3_vecenv_protocol(pg):
     venv.close()
 
 
-@pytest.mark.parametrize("env_id", ["PandaReach-v3", "PandaPush-v3"])
+@pytest.mark.parametrize("env_id", ["PandaReach-v3", "PandaPush-v3", "PandaReachAO-v3"])
 def test_sb3_host_path_matches_device_path(pg, env_id):
     """step_async/step_wait (pinned staging, one sync) returns exactly the device path's
     outputs, including the terminal observations of the auto-reset at the time limit."""
@@ -303,10 +303,13 @@ def test_sb3_host_path_matches_device_path(pg, env_id):
         assert np.array_equal(r, rew.cpu().numpy())
         assert np.array_equal(d, done)
         assert [i["is_success"] for i in infos] == succ.bool().cpu().tolist()
+        assert [i["is_truncated"] for i in infos] == a_env.task_truncated().tolist()
+        te = term.bool().cpu().numpy()
         for i in np.nonzero(done)[0]:
             assert np.array_equal(infos[i]["terminal_observation"]["observation"], tobs[i])
-            assert infos[i]["TimeLimit.truncated"] is True
-        assert done.any() == ((t + 1) % 3 == 0)
+            assert infos[i]["TimeLimit.truncated"] == bool(not te[i])
+        if env_id != "PandaReachAO-v3":   # (ReachAO also ends episodes by success or collision)
+            assert done.any() == ((t + 1) % 3 == 0)
     # device actions go straight through step_async
     o, *_ = b_env.step(torch.zeros((n, b_env.action_dim), device="cuda:0"))
     assert o["observation"].shape == (n, b_env.obs_dim)
