@@ -328,6 +328,18 @@ int pgx_snapshot(pgx_handle h, int32_t* state_id, void* stream);
 int pgx_restore(pgx_handle h, int32_t state_id, void* stream);
 int pgx_release(pgx_handle h, int32_t state_id);
 
+/* Reset draws from numpy PCG64 streams instead of the device Philox counter: the goal / object
+ * draws of every later reset of env i -- pgx_reset without injection and the step's auto-reset --
+ * come from stream i in the task's order (reach.py:75-78, push.py:75-87,
+ * pick_and_place.py:71-85), as gymnasium's env.np_random (core.py:302) continues across the
+ * resets of an SB3 VecEnv.  states: [N][4] uint64 per env {state_lo, state_hi, inc_lo, inc_hi}
+ * of numpy's PCG64 (bit_generator.state["state"]), host or device memory, copied on `stream`;
+ * NULL returns to Philox.  An injected reset leaves its env's stream untouched.  Streams are not
+ * part of the saved state (restoreState keeps np_random as it is).  ReachAO: PGX_E_UNSUPPORTED.
+ * pgx_get_rng_streams copies the current records out ([N][4], host or device memory). */
+int pgx_set_rng_streams(pgx_handle h, const uint64_t* states, void* stream);
+int pgx_get_rng_streams(pgx_handle h, uint64_t* states, void* stream);
+
 /* ------------------------------------------------------------------------
  * Device HER replay ring: the goal-relabelling replay buffer the reference's
  * training uses (SB3 HerReplayBuffer / the fork's VecHerReplayBuffer,

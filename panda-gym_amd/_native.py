@@ -17,6 +17,7 @@ EXPORTS = [
     "pgx_version", "pgx_last_error", "pgx_obs_dim", "pgx_action_dim", "pgx_dev_model_bytes", "pgx_create", "pgx_destroy",
     "pgx_get_state", "pgx_reset", "pgx_step", "pgx_sample_actions", "pgx_compute_reward",
     "pgx_state_bytes", "pgx_save_state", "pgx_restore_state", "pgx_snapshot", "pgx_restore", "pgx_release",
+    "pgx_set_rng_streams", "pgx_get_rng_streams",
     "pgx_replay_create", "pgx_replay_destroy", "pgx_replay_add", "pgx_replay_size", "pgx_replay_sample",
     "pgx_replay_episode_arrays", "pgx_replay_row_dim", "pgx_replay_row_stride",
 ]
@@ -61,6 +62,8 @@ def load(path: str = None):
     lib.pgx_snapshot.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.c_void_p]
     lib.pgx_restore.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
     lib.pgx_release.argtypes = [C.c_void_p, C.c_int32]
+    lib.pgx_set_rng_streams.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.pgx_get_rng_streams.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     lib.pgx_replay_create.argtypes = [C.POINTER(PgxReplayConfig), C.c_int, C.POINTER(C.c_void_p)]
     lib.pgx_replay_row_dim.argtypes = [C.POINTER(PgxReplayConfig)]
     lib.pgx_replay_row_stride.argtypes = [C.POINTER(PgxReplayConfig)]

@@ -74,6 +74,8 @@ struct pgx_env {
     size_t blob_bytes;
     /* device snapshots by id (pgx_snapshot): slot i holds state id i, nullptr = free */
     std::vector<void*> snaps;
+    /* [N][4] numpy PCG64 streams of the reset draws (pgx_set_rng_streams), nullptr: Philox */
+    uint64_t* pcg = nullptr;
 };
 
 extern "C" {
@@ -350,6 +352,7 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     }
 #endif
     PgxDevEnv& e = h->de;
+    e.pcg = nullptr;
     e.task = cfg->task;
     e.control = cfg->control;
     e.reward = cfg->reward;
@@ -465,6 +468,7 @@ void pgx_destroy(pgx_handle h) {
     (void)hipSetDevice(h->device);
     for (void* p : h->snaps)
         if (p) (void)hipFree(p);
+    if (h->pcg) (void)hipFree(h->pcg);
     (void)hipFree(h->blob);
     delete h;
 }
@@ -596,6 +600,42 @@ int pgx_release(pgx_handle h, int32_t state_id) {
     if (!rc) rc = hip_check(hipFree(h->snaps[state_id]), "hipFree(snapshot)");
     h->snaps[state_id] = nullptr;
     return rc;
+}
+
+/* Reset draws from numpy PCG64 streams (gymnasium's env.np_random, core.py:302, continued by
+ * every later reset() -- the SB3 VecEnv auto-reset included): a copy of the caller's [N][4]
+ * records on `stream`; NULL returns to the Philox counter.  ReachAO's rejection sampler draws
+ * integers and a shuffle besides uniforms (reach_ao.py:1101-1161): not restated, refused. */
+int pgx_set_rng_streams(pgx_handle h, const uint64_t* states, void* stream) {
+    if (!h) return fail(PGX_E_INVALID, "null handle");
+    if (h->de.ao && states) return fail(PGX_E_UNSUPPORTED, "PCG64 reset streams: ReachAO's reset draws are not restated");
+    int rc = hip_check(hipSetDevice(h->device), "hipSetDevice");
+    if (rc) return rc;
+    const size_t bytes = 32 * (size_t)h->de.n_envs;
+    if (!states) {
+        if (h->pcg) {
+            /* queued resets may still read the streams */
+            rc = hip_check(hipDeviceSynchronize(), "rng streams sync");
+            if (!rc) rc = hip_check(hipFree(h->pcg), "hipFree(rng streams)");
+            h->pcg = nullptr;
+        }
+        h->de.pcg = nullptr;
+        return rc;
+    }
+    if (!h->pcg) {
+        rc = hip_check(hipMalloc((void**)&h->pcg, bytes), "hipMalloc(rng streams)");
+        if (rc) { h->pcg = nullptr; return rc; }
+    }
+    rc = hip_check(hipMemcpyAsync(h->pcg, states, bytes, hipMemcpyDefault, (hipStream_t)stream), "rng streams copy");
+    if (!rc) h->de.pcg = h->pcg;
+    return rc;
+}
+
+int pgx_get_rng_streams(pgx_handle h, uint64_t* states, void* stream) {
+    if (!h || !states) return fail(PGX_E_INVALID, "null argument");
+    if (!h->pcg) return fail(PGX_E_INVALID, "no PCG64 reset streams set (pgx_set_rng_streams)");
+    return hip_check(hipMemcpyAsync(states, h->pcg, 32 * (size_t)h->de.n_envs, hipMemcpyDefault, (hipStream_t)stream),
+                     "rng streams copy");
 }
 
 }  // extern "C"

@@ -70,6 +70,8 @@ struct PgxDevEnv {
     int32_t full_manifold;         /* contacts == PGX_CONTACTS_FULL: robot budget PGX_ROBOT_POINTS(_ARM) */
     int32_t wave_mode;             /* A/B hook (PGX_WAVES_PER_SIMD): 0 auto (two resident waves per SIMD
                                       beyond 1024 waves), 1 the one-wave build, 2 the two-wave build */
+    uint64_t* pcg;                 /* [N][4] numpy PCG64 streams of the reset draws (pgx_set_rng_streams),
+                                      nullptr: the Philox counter */
 };
 
 struct PgxDevState {

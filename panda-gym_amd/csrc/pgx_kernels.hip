@@ -3328,6 +3328,27 @@ __device__ __forceinline__ double reset_uniform(const PgxDevEnv& e, uint64_t env
     return (double)(u >> 11) * (1.0 / 9007199254740992.0);
 }
 
+/* numpy's PCG64 (XSL-RR 128/64, the generator gymnasium's seeding.np_random builds,
+ * core.py:302): state <- state * M + inc (mod 2^128), then the output of the new state:
+ * rotr64(hi ^ lo, hi >> 58).  next_double = (u >> 11) * 2^-53 as in the reset draws above.
+ * Record per env (pgx_set_rng_streams): state_lo, state_hi, inc_lo, inc_hi. */
+struct Pcg64 {
+    uint64_t lo, hi, ilo, ihi;
+};
+__device__ __forceinline__ double pcg64_next_double(Pcg64& g) {
+    constexpr uint64_t MLO = 0x4385DF649FCCF645ull, MHI = 0x2360ED051FC65DA4ull;
+    const uint64_t plo = g.lo * MLO;
+    uint64_t hi = __umul64hi(g.lo, MLO) + g.lo * MHI + g.hi * MLO;
+    const uint64_t lo = plo + g.ilo;
+    hi += g.ihi + (uint64_t)(lo < plo);
+    g.lo = lo;
+    g.hi = hi;
+    const uint64_t x = hi ^ lo;
+    const uint32_t rot = (uint32_t)(hi >> 58);
+    const uint64_t u = (x >> rot) | (x << ((64u - rot) & 63u));
+    return (double)(u >> 11) * (1.0 / 9007199254740992.0);
+}
+
 /* --------------------------------------------------------- env epilogue */
 #pragma clang fp contract(off)
 /* utils.distance on (float32 achieved, float64 goal) -> float64, rounded to 1e-6 */
@@ -3383,16 +3404,25 @@ __device__ __forceinline__ void write_obs(const PgxDevEnv& e, float* dst, V3 pos
 template <int OBJ>
 __device__ __forceinline__ void reset_env(MRef m, const PgxDevEnv& e, int i, uint32_t& episode, const double* inject,
                                           const double* inject_obj, float* q, float* qd, double* goal,
-                                          ObjState& ob) {
+                                          ObjState& ob, bool lead = true) {
 #pragma unroll
     for (int j = 0; j < NJ; j++) { q[j] = m.neutral_q[j]; qd[j] = 0.0f; }
     uint64_t env = e.env_id_offset + (uint64_t)i;
+    /* the draw source: the env's numpy PCG64 stream (pgx_set_rng_streams) advanced in draw order,
+     * or the Philox counter (env, episode, draw index) */
+    const bool pcg = e.pcg != nullptr;
+    Pcg64 g{0, 0, 0, 0};
+    if (pcg) {
+        const uint64_t* r = e.pcg + 4 * (size_t)i;
+        g = Pcg64{r[0], r[1], r[2], r[3]};
+    }
+    auto draw = [&](int k) -> double { return pcg ? pcg64_next_double(g) : reset_uniform(e, env, episode, k); };
     double noise[3];
 #pragma unroll
-    for (int c = 0; c < 3; c++) noise[c] = uniform_draw(e.goal_low[c], e.goal_high[c], reset_uniform(e, env, episode, c));
+    for (int c = 0; c < 3; c++) noise[c] = uniform_draw(e.goal_low[c], e.goal_high[c], draw(c));
     int k = 3;
     if (OBJ && e.goal_z_zero_prob > 0.0) {
-        if (reset_uniform(e, env, episode, k) < e.goal_z_zero_prob) noise[2] = 0.0;
+        if (draw(k) < e.goal_z_zero_prob) noise[2] = 0.0;
         k++;
     }
 #pragma unroll
@@ -3400,12 +3430,17 @@ __device__ __forceinline__ void reset_env(MRef m, const PgxDevEnv& e, int i, uin
     if (OBJ) {
         double p[3];
 #pragma unroll
-        for (int c = 0; c < 3; c++)
-            p[c] = inject_obj ? inject_obj[c]
-                              : goal_add(e.obj_offset[c],
-                                         uniform_draw(e.obj_low[c], e.obj_high[c], reset_uniform(e, env, episode, k + c)));
+        for (int c = 0; c < 3; c++) {
+            const double u = draw(k + c);
+            p[c] = inject_obj ? inject_obj[c] : goal_add(e.obj_offset[c], uniform_draw(e.obj_low[c], e.obj_high[c], u));
+        }
         ob.p = v3((float)p[0], (float)p[1], (float)p[2]);
         ob.qx = 0.0f; ob.qy = 0.0f; ob.qz = 0.0f; ob.qw = 1.0f;
+    }
+    /* an injected reset replaces the task's draws: its stream stays where it was */
+    if (pcg && lead && !inject && !inject_obj) {
+        uint64_t* r = e.pcg + 4 * (size_t)i;
+        r[0] = g.lo; r[1] = g.hi; r[2] = g.ilo; r[3] = g.ihi;
     }
     episode += 1;
 }
@@ -3989,7 +4024,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
             if constexpr (WIDE) ao_link_obs_g(*L, ln, c);
             else ao_link_obs(*L, ln);
         } else {
-            reset_env<OBJ>(m, e, i, episode, nullptr, nullptr, q, qd, goal, ob);
+            reset_env<OBJ>(m, e, i, episode, nullptr, nullptr, q, qd, goal, ob, lead);
             ee_state(m, q, qd, pos, vel);
 #pragma unroll
             for (int j = 0; j < NJ; j++) qprev[j] = q[j];   /* resetJointState refreshes the link cache */

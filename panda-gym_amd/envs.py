@@ -124,7 +124,12 @@ def seeded_reset(env_spec: abi.EnvSpec, seed: Optional[int]) -> Optional[Tuple[n
         return None
     if env_spec.task == abi.TASK_REACH_AO:   # (goal, obstacle centres [6, 3])
         return reach_ao.seeded_reset(seed, _ao_geometry(tuple(env_spec.base_pos)))
-    rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed)))
+    return task_draws(env_spec, np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed))))
+
+
+def task_draws(env_spec: abi.EnvSpec, rng: np.random.Generator) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+    """(goal, object position) of one Task.reset of Reach / Push / PickAndPlace drawn from ``rng``
+    (env.np_random): the order the device reset follows in its PCG64 mode (pgx_set_rng_streams)."""
     lo, hi = env_spec.goal_bounds()
     if env_spec.task == abi.TASK_REACH:
         return rng.uniform(np.array(lo), np.array(hi)), None
@@ -140,6 +145,27 @@ def seeded_reset(env_spec: abi.EnvSpec, seed: Optional[int]) -> Optional[Tuple[n
     return goal, obj
 
 
+def pcg64_records(seeds: Sequence[int]) -> np.ndarray:
+    """[N, 4] uint64 {state_lo, state_hi, inc_lo, inc_hi} of PCG64(SeedSequence(seed)) per seed:
+    gymnasium's seeding.np_random(seed) (core.py:302), the records pgx_set_rng_streams takes."""
+    out = np.empty((len(seeds), 4), dtype=np.uint64)
+    m = (1 << 64) - 1
+    for i, sd in enumerate(seeds):
+        st = np.random.PCG64(np.random.SeedSequence(int(sd))).state["state"]
+        out[i] = (st["state"] & m, st["state"] >> 64, st["inc"] & m, st["inc"] >> 64)
+    return out
+
+
+def pcg64_from_record(rec: np.ndarray) -> np.random.Generator:
+    """numpy Generator at a record's stream position (inverse of pcg64_records)."""
+    bg = np.random.PCG64()
+    st = bg.state
+    st["state"] = {"state": int(rec[0]) | (int(rec[1]) << 64), "inc": int(rec[2]) | (int(rec[3]) << 64)}
+    st["has_uint32"], st["uinteger"] = 0, 0
+    bg.state = st
+    return np.random.Generator(bg)
+
+
 # ------------------------------------------------------------ vec env
 class PandaVecEnv:
     """N independent Panda envs stepped in lockstep by one HIP kernel launch.
@@ -151,13 +177,21 @@ class PandaVecEnv:
     ``full_manifold`` (default: on wherever the layout has it, i.e. with contacts in the 16-lane
     layout) keeps Bullet's per-pair manifolds (<= 4 points per colliding pair) up to 8 robot points
     per env in Reach / ReachAO and 12 in Push / PickAndPlace; ``False`` keeps the 4 deepest robot
-    points (the one-lane layout's budget; DESIGN.md section 4: budget, rates, cost)."""
+    points (the one-lane layout's budget; DESIGN.md section 4: budget, rates, cost).
+
+    ``reset_rng``: where the reset draws (goal, object) come from.  ``"philox"`` (default): a
+    device counter stream; a seeded ``reset`` injects the reference's numpy draws for that reset
+    only.  ``"pcg64"``: every env keeps numpy's PCG64 stream on the device (env i seeded with
+    seed + i, as SB3 seeds a VecEnv) and every reset -- the auto-reset included -- continues it,
+    as the reference's env.np_random does: the goal sequence of a whole seeded run is the
+    reference's, bit for bit.  Not for ReachAO (its rejection sampler is not restated)."""
 
     def __init__(self, env_id: str = "PandaReach-v3", num_envs: int = 4096, device: Any = "cuda:0", seed: int = 0,
                  env_id_offset: int = 0, max_episode_steps: Optional[int] = None, auto_reset: bool = True,
                  n_substeps: int = 20, model_name: str = "panda_custom0", contacts: bool = True,
                  lanes_per_env: int = 0, full_manifold: Optional[bool] = None,
-                 sim_params: Optional[Dict[str, Any]] = None, lib_path: Optional[str] = None):
+                 sim_params: Optional[Dict[str, Any]] = None, lib_path: Optional[str] = None,
+                 reset_rng: str = "philox"):
         """``sim_params``: pgx_sim_params fields to override (the default library runs only the
         compiled parameters and refuses others; ``lib_path`` = libpgx_rtmodel.so reads them from
         the handle)."""
@@ -233,6 +267,11 @@ class PandaVecEnv:
         self._pending: Optional[torch.Tensor] = None
         self._pending_seed: Optional[int] = None
         self._step_index = 0
+        if reset_rng not in ("philox", "pcg64"):
+            raise ValueError(f"reset_rng must be 'philox' or 'pcg64', got {reset_rng!r}")
+        self.reset_rng = reset_rng
+        if reset_rng == "pcg64":
+            self._set_rng_streams(pcg64_records([seed + i for i in range(n)]))
 
     # ---------------------------------------------------------------- core
     def _check(self, rc: int, what: str) -> None:
@@ -300,13 +339,34 @@ class PandaVecEnv:
     def _obs_dict(self) -> Dict[str, torch.Tensor]:
         return {"observation": self.obs, "achieved_goal": self.achieved_goal, "desired_goal": self.desired_goal}
 
+    def _set_rng_streams(self, records: np.ndarray) -> None:
+        rec = torch.as_tensor(np.ascontiguousarray(records, dtype=np.uint64).view(np.int64), device=self.device)
+        self._check(self.lib.pgx_set_rng_streams(self._h, C.c_void_p(rec.data_ptr()), self._stream()),
+                    "pgx_set_rng_streams")
+        self._rng_keep = rec   # read by the queued copy
+
+    def rng_streams(self) -> np.ndarray:
+        """[N, 4] uint64 PCG64 records of the envs' reset streams (``reset_rng="pcg64"``): where each
+        env's np_random stands (pcg64_from_record rebuilds the numpy Generator)."""
+        out = torch.empty((self.num_envs, 4), dtype=torch.int64, device=self.device)
+        self._check(self.lib.pgx_get_rng_streams(self._h, C.c_void_p(out.data_ptr()), self._stream()),
+                    "pgx_get_rng_streams")
+        return out.cpu().numpy().view(np.uint64)
+
     def reset_tensors(self, seed: Optional[int] = None, mask: Optional[torch.Tensor] = None,
                       goals: Optional[np.ndarray] = None,
                       objects: Optional[np.ndarray] = None) -> Dict[str, torch.Tensor]:
         """Reset (masked) envs on device; ``seed`` reproduces the reference's PCG64 goal (and
-        object) draws for env i with seed+i (SB3 VecEnv seeding), injected into the kernel."""
+        object) draws for env i with seed+i (SB3 VecEnv seeding): injected into the kernel, or
+        with ``reset_rng="pcg64"`` the envs' device streams are reseeded and drawn from."""
         inj, inj_obj = None, None
-        if goals is None and objects is None and seed is not None:
+        if goals is None and objects is None and seed is not None and self.reset_rng == "pcg64":
+            rec = pcg64_records([seed + i for i in range(self.num_envs)])
+            if mask is not None:   # only the masked envs are reseeded
+                keep = ~mask.detach().to("cpu", torch.bool).numpy()
+                rec[keep] = self.rng_streams()[keep]
+            self._set_rng_streams(rec)
+        elif goals is None and objects is None and seed is not None:
             draws = [seeded_reset(self.spec, seed + i) for i in range(self.num_envs)]
             goals = np.stack([d[0] for d in draws])
             if self.spec.task != abi.TASK_REACH:
@@ -637,9 +697,11 @@ class PandaEnv:
     metadata = {"render_modes": []}
 
     def __init__(self, env_id: str = "PandaReach-v3", device: Any = "cuda:0", max_episode_steps: Optional[int] = None,
-                 seed: int = 0):
+                 seed: int = 0, reset_rng: str = "philox"):
+        """``reset_rng="pcg64"``: reset(seed) seeds the env's device PCG64 stream and every later
+        reset() continues it, as gymnasium's np_random does (PandaVecEnv)."""
         self._vec = PandaVecEnv(env_id, num_envs=1, device=device, seed=seed, auto_reset=False,
-                                max_episode_steps=max_episode_steps)
+                                max_episode_steps=max_episode_steps, reset_rng=reset_rng)
         self.spec = self._vec.spec
         self.observation_space = self._vec.observation_space
         self.action_space = self._vec.action_space
@@ -647,8 +709,10 @@ class PandaEnv:
         self.robot, self.task, self.sim = _RobotView(self), _TaskView(self), _SimView(self)
 
     def reset(self, seed: Optional[int] = None, options: Optional[dict] = None):
-        r = seeded_reset(self.spec, seed)
-        if r is None:
+        r = None if self._vec.reset_rng == "pcg64" else seeded_reset(self.spec, seed)
+        if self._vec.reset_rng == "pcg64":   # reseed the device stream (seed given) or continue it
+            self._vec.reset_tensors(seed=seed)
+        elif r is None:
             self._vec.reset_tensors()
         else:
             self._vec.reset_tensors(goals=r[0][None, :], objects=None if r[1] is None else r[1][None, :])

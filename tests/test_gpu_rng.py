@@ -1,0 +1,141 @@
+"""GPU: the device reset in its numpy-PCG64 mode (``reset_rng="pcg64"``, pgx_set_rng_streams)
+against numpy itself -- gymnasium's env.np_random (core.py:302), continued by every reset of an
+SB3 VecEnv (the auto-reset included) and drawn in the task's order (reach.py:75-78,
+push.py:75-87, pick_and_place.py:71-85).  Bit-exact: the fp64 goal in the device state, the
+object position (f32 of the fp64 draw) and the stream records after every reset."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pg():
+    import panda_gym_amd as pg
+
+    pg.load_native()
+    return pg
+
+
+def _gens(seed, n):
+    return [np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed + i))) for i in range(n)]
+
+
+def _check_envs(pg, venv, gens, expect):
+    st = venv.state()
+    goal = st["goal"].cpu().numpy().T
+    g_ref = np.stack([e[0] for e in expect])
+    assert np.array_equal(goal, g_ref)
+    assert np.array_equal(venv.desired_goal.cpu().numpy(), g_ref.astype(np.float32))
+    if expect[0][1] is not None:
+        o_ref = np.stack([e[1] for e in expect]).astype(np.float32)
+        assert np.array_equal(st["object"].cpu().numpy()[:3].T, o_ref)
+    rec = venv.rng_streams()
+    for r, g in zip(rec, gens):
+        s = g.bit_generator.state["state"]
+        m = (1 << 64) - 1
+        assert [int(v) for v in r] == [s["state"] & m, s["state"] >> 64, s["inc"] & m, s["inc"] >> 64]
+
+
+@pytest.mark.parametrize("env_id,lanes,contacts", [
+    ("PandaReach-v3", 16, True), ("PandaReach-v3", 1, True), ("PandaReach-v3", 0, False),
+    ("PandaPush-v3", 16, True), ("PandaPickAndPlace-v3", 16, True), ("PandaPickAndPlace-v3", 1, True)])
+def test_seeded_run_draws_the_reference_stream_across_auto_resets(pg, env_id, lanes, contacts):
+    """reset(seed) then three 2-step episodes: after each auto-reset every env's goal (and object)
+    is the next task draw of its own numpy Generator(PCG64(SeedSequence(seed + i)))."""
+    n, seed = 67, 4242
+    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=seed, max_episode_steps=2,
+                          lanes_per_env=lanes, contacts=contacts, reset_rng="pcg64")
+    gens = _gens(seed, n)
+    venv.reset_tensors(seed=seed)
+    _check_envs(pg, venv, gens, [pg.task_draws(venv.spec, g) for g in gens])
+    zero = torch.zeros((n, venv.action_dim), device="cuda:0")
+    for ep in range(3):
+        venv.step_tensors(zero)
+        assert not venv.truncated.any().item()
+        venv.step_tensors(zero)
+        assert venv.truncated.all().item()
+        _check_envs(pg, venv, gens, [pg.task_draws(venv.spec, g) for g in gens])
+    venv.close()
+
+
+def test_sb3_reset_seed_then_auto_reset(pg):
+    """SB3 protocol: seed(s) + reset() reseeds env i with s + i; step_wait's auto-reset continues."""
+    n, seed = 5, 77
+    venv = pg.PandaVecEnv("PandaPush-v3", num_envs=n, device="cuda:0", seed=0, max_episode_steps=1,
+                          reset_rng="pcg64")
+    venv.seed(seed)
+    obs = venv.reset()
+    gens = _gens(seed, n)
+    d0 = [pg.task_draws(venv.spec, g) for g in gens]
+    assert np.array_equal(obs["desired_goal"], np.stack([d[0] for d in d0]).astype(np.float32))
+    obs, _, dones, infos = venv.step(np.zeros((n, 3), np.float32))
+    assert dones.all()
+    d1 = [pg.task_draws(venv.spec, g) for g in gens]
+    assert np.array_equal(obs["desired_goal"], np.stack([d[0] for d in d1]).astype(np.float32))
+    assert np.array_equal(np.stack([i["terminal_observation"]["desired_goal"] for i in infos]),
+                          np.stack([d[0] for d in d0]).astype(np.float32))
+    venv.close()
+
+
+def test_injected_and_masked_resets_keep_the_other_streams(pg):
+    n, seed = 9, 31
+    venv = pg.PandaVecEnv("PandaReach-v3", num_envs=n, device="cuda:0", seed=seed, reset_rng="pcg64")
+    before = venv.rng_streams().copy()
+    venv.reset_tensors(goals=np.zeros((n, 3)))       # injected: the draws are replaced, streams stay
+    assert np.array_equal(venv.rng_streams(), before)
+    assert np.array_equal(venv.state()["goal"].cpu().numpy(), np.zeros((3, n)))
+    mask = torch.zeros(n, dtype=torch.uint8)
+    mask[[1, 4]] = 1
+    venv.reset_tensors(seed=1000, mask=mask)          # reseeds envs 1 and 4 only, and draws them
+    gens = _gens(seed, n)                              # construction: env i seeded seed + i
+    g1000 = _gens(1000, n)
+    goal = venv.state()["goal"].cpu().numpy().T
+    for i in range(n):
+        if mask[i]:
+            assert np.array_equal(goal[i], pg.task_draws(venv.spec, g1000[i])[0])
+        else:
+            assert np.array_equal(goal[i], np.zeros(3))
+    rec = venv.rng_streams()
+    for i in range(n):
+        exp = pg.pcg64_records([seed + i])[0] if not mask[i] else None
+        if exp is not None:
+            assert np.array_equal(rec[i], exp)
+        else:
+            assert np.array_equal(pg.pcg64_from_record(rec[i]).random(3), g1000[i].random(3))
+    venv.close()
+
+
+def test_single_env_reset_continues_np_random(pg):
+    """RobotTaskEnv.reset(seed) then reset(), reset(): the goals are three consecutive draws of one
+    Generator(PCG64(SeedSequence(seed))) -- what gymnasium's np_random gives the reference."""
+    env = pg.make("PandaPickAndPlace-v3", reset_rng="pcg64")
+    gen = _gens(12345, 1)[0]
+    for k in range(3):
+        obs, _ = env.reset(seed=12345 if k == 0 else None)
+        g, o = pg.task_draws(env.spec, gen)
+        assert np.array_equal(env.task.goal, g)
+        assert np.array_equal(obs["desired_goal"], g.astype(np.float32))
+        assert np.array_equal(obs["achieved_goal"], o.astype(np.float32))
+    # a fresh seeded reset restarts the stream
+    obs, _ = env.reset(seed=12345)
+    assert np.array_equal(env.task.goal, pg.seeded_reset(env.spec, 12345)[0])
+    env.close()
+
+
+def test_back_to_philox_and_reach_ao_refused(pg):
+    venv = pg.PandaVecEnv("PandaReach-v3", num_envs=8, device="cuda:0", seed=5, reset_rng="pcg64")
+    ref = pg.PandaVecEnv("PandaReach-v3", num_envs=8, device="cuda:0", seed=5)
+    assert venv.lib.pgx_set_rng_streams(venv._h, None, venv._stream()) == 0
+    venv.reset_rng = "philox"
+    with pytest.raises(pg.PgxError):
+        venv.rng_streams()
+    venv.reset_tensors()
+    ref.reset_tensors()
+    assert np.array_equal(venv.state()["goal"].cpu().numpy(), ref.state()["goal"].cpu().numpy())
+    venv.close()
+    ref.close()
+    with pytest.raises(pg.PgxError, match="ReachAO"):
+        pg.PandaVecEnv("PandaReachAO-v3", num_envs=4, device="cuda:0", reset_rng="pcg64")
