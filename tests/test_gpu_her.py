@@ -72,15 +72,16 @@ def test_sample_bit_exact_vs_oracle(her_mod, steps):
     buf.close()
 
 
-@pytest.mark.parametrize("two_pass", [False, True])
+@pytest.mark.parametrize("variant", ["default", "two_pass", "spb64"])
 @pytest.mark.parametrize("od,ad", [(19, 4), (18, 3), (56, 7)])
-def test_both_sample_kernels_bit_exact(her_mod, monkeypatch, od, ad, two_pass):
+def test_both_sample_kernels_bit_exact(her_mod, monkeypatch, od, ad, variant):
     """libpgx samples records of <= 16 float4 columns with the single-read kernel (sample_kernel_reg)
     and wider ones (ReachAO's 56-float observation) with the two-pass kernel; PGX_HER_TWO_PASS
-    forces the latter.  Both bit-exact against the restatement at PickAndPlace's, Push's and
-    ReachAO's dimensions."""
-    if two_pass:
-        monkeypatch.setenv("PGX_HER_TWO_PASS", "1")
+    forces the latter, PGX_HER_SPB=64 the single-read kernel's 64-samples-per-block build.  All
+    bit-exact against the restatement at PickAndPlace's, Push's and ReachAO's dimensions."""
+    env = {"two_pass": ("PGX_HER_TWO_PASS", "1"), "spb64": ("PGX_HER_SPB", "64")}
+    if variant in env:
+        monkeypatch.setenv(*env[variant])
     rng = np.random.default_rng(od)
     buf, orc = _pair(her_mod, N=48, C=23, od=od, ad=ad)
     _feed(buf, orc, 60, rng)
