@@ -108,6 +108,7 @@ def parse():
     ap.add_argument("--no-tasks", action="store_true", help="skip the Push / PickAndPlace legs (configs[2], [3])")
     ap.add_argument("--task-steps", type=int, default=200)
     ap.add_argument("--no-ao", action="store_true", help="skip the sharded ReachAO leg (configs[4])")
+    ap.add_argument("--no-graph", action="store_true", help="skip the HIP-graph replay of the headline loop")
     ap.add_argument("--ao-envs", type=int, default=8192, help="ReachAO envs per GPU (65536 over 8 GPUs)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group for N > 1 (gloo: collective tensors on the host, so several ranks "
@@ -455,6 +456,24 @@ def main():
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     kernel_ms = ev0.elapsed_time(ev1) / K
+    # the same random-policy loop replayed from a HIP graph (capture_steps: sample + step per step, no
+    # host launches in between; the replays repeat the capture's draws while the state moves on)
+    graph = None
+    if not args.no_graph:
+        G, R = venv.spec.max_episode_steps, 10
+        g = venv.capture_steps(G)
+        g.replay()
+        torch.cuda.synchronize(dev)
+        ev0.record(stream)
+        for _ in range(R):
+            g.replay()
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        gms = ev0.elapsed_time(ev1) / (R * G)
+        graph = {"ms_per_step": gms, "value": E / (gms * 1e-3), "unit": "env-steps/s per GPU",
+                 "steps_per_graph": G, "replays": R,
+                 "path": "PandaVecEnv.capture_steps: sample_actions + pgx_step x 50 in one HIP graph"}
+        del g
     # configs[4]: ReachAO sharded over every rank (collective timing: all ranks take part)
     ao = None if args.no_ao else sharded_leg(dev, "PandaReachAO-v3", args.ao_envs, args.task_steps, 20, dist, rank,
                                             world, coll_dev)
@@ -515,6 +534,8 @@ def main():
             "episode_stats_last_step": {"truncated": float(stats[0]), "success": float(stats[1]),
                                         "reward_sum": float(stats[2])},
         }
+        if graph is not None:
+            line["graph_replay"] = graph
         if ao is not None:
             line["reach_ao"] = ao
         if world == 1 and not args.no_cpu_baseline:

@@ -407,6 +407,30 @@ class PandaVecEnv:
                                           self._stream()), "pgx_sample_actions")
         return self._actions
 
+    def capture_steps(self, k: int, actions: Optional[torch.Tensor] = None):
+        """Capture ``k`` lockstep env steps into one HIP graph (torch.cuda.CUDAGraph); ``replay()``
+        runs them with no host launch in between (graph capture of the step loop).
+        ``actions``: a static [k, N, A] f32 device buffer step i reads (refill it between replays),
+        or None: the device Philox random policy, drawn inside the graph with the step counters of
+        capture time (every replay repeats those draws; the env state moves on).  The step's outputs
+        land in the env's usual buffers (obs, reward, ... of the last captured step).  Capture runs
+        nothing: the state changes only on replay."""
+        if actions is not None:
+            if tuple(actions.shape) != (k, self.num_envs, self.action_dim) or actions.dtype != torch.float32 \
+                    or actions.device != self.device or not actions.is_contiguous():
+                raise ValueError(f"actions must be a contiguous f32 [{k}, {self.num_envs}, {self.action_dim}] "
+                                 f"tensor on {self.device}")
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        base = self._step_index
+        with torch.cuda.graph(g):
+            for i in range(k):
+                a = actions[i] if actions is not None else self.sample_actions(base + i)
+                self._check(self.lib.pgx_step(self._h, C.c_void_p(a.data_ptr()), C.byref(self._out), self._stream()),
+                            "pgx_step (capture)")
+        g._pgx_keep = actions   # the graph reads the buffer at replay
+        return g
+
     # ------------------------------------------------------- SB3 VecEnv API
     def reset(self, seed: Optional[int] = None, options: Optional[dict] = None):
         """SB3 VecEnv.reset: a seed given to ``seed()`` beforehand applies to this reset only."""

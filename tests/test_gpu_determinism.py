@@ -54,3 +54,38 @@ def test_runtime_model_library_is_deterministic(pg):
         b = _rollout(pg, env_id, 64, lanes, 10, **kw)
         assert np.isfinite(a).all(), (env_id, lanes)
         assert np.array_equal(a, b), (env_id, lanes)
+
+
+@pytest.mark.parametrize("env_id", ["PandaReach-v3", "PandaPickAndPlace-v3"])
+def test_captured_steps_equal_eager_steps(pg, env_id):
+    """capture_steps: k steps replayed from a HIP graph equal the same k steps launched eagerly, bit
+    for bit (state and outputs), over two replays -- the kernels are graph-capturable (no host
+    synchronisation or allocation on the step path).  k spans an auto-reset (TimeLimit 3)."""
+    n, k = 96, 4
+    kw = dict(num_envs=n, device="cuda:0", seed=9, max_episode_steps=3)
+    eager, graphed = pg.PandaVecEnv(env_id, **kw), pg.PandaVecEnv(env_id, **kw)
+    eager.reset_tensors(seed=9)
+    graphed.reset_tensors(seed=9)
+    acts = torch.empty((k, n, eager.action_dim), device="cuda:0")
+    g = graphed.capture_steps(k, acts)
+    for rep in range(2):
+        for i in range(k):
+            acts[i].copy_(eager.sample_actions(100 * rep + i))
+        for i in range(k):
+            eager.step_tensors(acts[i])
+        g.replay()
+        torch.cuda.synchronize()
+        se, sg = eager.state(), graphed.state()
+        for key in ("q", "qd", "qc", "goal", "object", "contacts", "elapsed", "episode"):
+            assert torch.equal(se[key], sg[key]), key
+        for key in ("obs", "reward", "truncated", "terminal_obs"):
+            assert torch.equal(getattr(eager, key), getattr(graphed, key)), key
+    # the random-policy form: the draws of capture time, repeated on every replay
+    g2 = graphed.capture_steps(2)
+    g2.replay()
+    for i in range(2):
+        eager.step_tensors(eager.sample_actions(graphed._step_index + i))
+    torch.cuda.synchronize()
+    assert torch.equal(eager.state()["q"], graphed.state()["q"])
+    eager.close()
+    graphed.close()
