@@ -3824,9 +3824,12 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     const int ln = WIDE ? (int)threadIdx.x / GW : (int)threadIdx.x;   /* env slot in the wave (LDS index) */
     const int c = WIDE ? (int)threadIdx.x % GW : 0;                   /* lane within the env's row */
     const bool lead = c == 0;
-    const int i = xcd_block() * (WIDE ? EPW : 64) + ln;
     const int N = e.n_envs;
-    if (i >= N) return;
+    /* heavy-first order (e.perm, pgx_launch_step): dispatch order = block order, so the blocks are
+     * not dealt out per XCD there; an env's result does not depend on its wave mates */
+    const int slot = (e.perm ? (int)blockIdx.x : xcd_block()) * (WIDE ? EPW : 64) + ln;
+    if (slot >= N) return;
+    const int i = e.perm ? e.perm[slot] : slot;
     /* the prologue loads index by a laundered copy of i: the compiler cannot reuse their
      * 64-bit addresses for the epilogue stores and keep ~17 address pairs live across the
      * whole step (recomputing them at the end is a few adds) */
@@ -4180,6 +4183,52 @@ __global__ __launch_bounds__(256) void compute_reward_kernel(const float* __rest
     }
 }
 
+/* Heavy-first env order for the per-pair manifold kernels.  A wave costs what its heaviest env
+ * costs (the robot-point rows past the register budget dominate), and when a
+ * launch has more waves than the chip holds at once the dispatcher hands them out in block order:
+ * grouping the envs by the robot contact points they held at the end of the previous step, most
+ * first, puts the heavy envs into fewer waves and starts those first (longest-first scheduling).
+ * Key = active robot slots of the warm-start cache; a counting sort (13 bins, descending) with
+ * wave-aggregated atomics: the order inside a bin is arbitrary, which is harmless -- the step
+ * kernels give every env the same bits whatever its wave mates (test_gpu_env_order). */
+constexpr int SORT_BINS = PGX_ROBOT_POINTS + 1;
+__device__ __forceinline__ int robot_points_key(const PgxDevState& s, int N, int i, int rb) {
+    int k = 0;
+    for (int r = 0; r < rb; r++) k += s.contacts[(size_t)(CACHE1 + 2 * r) * N + i] >= 0.0f ? 1 : 0;
+    return k;
+}
+__global__ __launch_bounds__(256) void env_sort_count_kernel(PgxDevState s, int N, int rb, uint32_t* cnt) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int key = i < N ? robot_points_key(s, N, i, rb) : -1;
+    uint64_t todo = __ballot(key >= 0);
+    while (todo) {
+        const int k = __shfl(key, __ffsll((unsigned long long)todo) - 1);
+        const uint64_t mine = __ballot(key == k);
+        if (key == k && (__lane_id() == __ffsll((unsigned long long)mine) - 1)) atomicAdd(&cnt[k], (uint32_t)__popcll(mine));
+        todo &= ~mine;
+    }
+}
+__global__ __launch_bounds__(256) void env_sort_scatter_kernel(PgxDevState s, int N, int rb, uint32_t* cnt,
+                                                               int32_t* perm) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int key = i < N ? robot_points_key(s, N, i, rb) : -1;
+    uint64_t todo = __ballot(key >= 0);
+    while (todo) {
+        const int k = __shfl(key, __ffsll((unsigned long long)todo) - 1);
+        const uint64_t mine = __ballot(key == k);
+        const int leader = __ffsll((unsigned long long)mine) - 1;
+        uint32_t base = 0;
+        if (key == k && __lane_id() == leader) {
+            uint32_t off = 0;   /* the bins above k come first */
+            for (int b = SORT_BINS - 1; b > k; b--) off += cnt[b];
+            base = off + atomicAdd(&cnt[16 + k], (uint32_t)__popcll(mine));
+        }
+        base = __shfl(base, leader);
+        if (key == k) perm[base + __popcll(mine & ((1ull << __lane_id()) - 1ull))] = i;
+        todo &= ~mine;
+    }
+}
+
 }  // namespace
 
 /* PGX_TU splits the library into two translation units (Makefile): 1 holds the arm-only
@@ -4234,6 +4283,22 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
     const bool two = e.wave_mode == 2 || (e.wave_mode == 0 && wide && grid.x > 1024);   /* more waves than SIMDs */
     const int variant = e.ao ? 13 : e.control * 4 + (e.has_object ? 2 : 0) + (e.contacts ? 1 : 0);
     if (wide && e.full_manifold) {
+        /* heavy-first order when the waves do not all fit at once (one per SIMD in the object
+         * kernels, two in ReachAO's) */
+        const unsigned resident = e.ao ? 2048u : 1024u;
+        const bool sort = e.perm_buf && e.sort_cnt && (e.sort_mode == 1 || (e.sort_mode == 0 && grid.x > resident));
+        PgxDevEnv es = e;
+        es.perm = nullptr;
+        if (sort) {
+            const int rb = e.has_object ? PGX_ROBOT_POINTS : PGX_ROBOT_POINTS_ARM;
+            const dim3 sg((e.n_envs + 255) / 256), sb(256);
+            hipError_t rc = hipMemsetAsync(e.sort_cnt, 0, 32 * sizeof(uint32_t), st);
+            if (rc != hipSuccess) return (int)rc;
+            hipLaunchKernelGGL(env_sort_count_kernel, sg, sb, 0, st, s, e.n_envs, rb, e.sort_cnt);
+            hipLaunchKernelGGL(env_sort_scatter_kernel, sg, sb, 0, st, s, e.n_envs, rb, e.sort_cnt, e.perm_buf);
+            es.perm = e.perm_buf;
+        }
+        const PgxDevEnv& e = es;
         /* the object tasks' per-pair manifold kernels run one wave per SIMD at every batch: their
          * 32 KB of LDS per wave lets only 5 of the two-wave build's 8 waves per CU in, and at 256
          * registers it spills 676 B per lane (PickAndPlace 16384: 8.54 ms two-wave, 4.51 ms one

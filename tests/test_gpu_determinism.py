@@ -56,11 +56,15 @@ def test_runtime_model_library_is_deterministic(pg):
         assert np.array_equal(a, b), (env_id, lanes)
 
 
-@pytest.mark.parametrize("env_id", ["PandaReach-v3", "PandaPickAndPlace-v3"])
-def test_captured_steps_equal_eager_steps(pg, env_id):
+@pytest.mark.parametrize("env_id,sort", [("PandaReach-v3", None), ("PandaPickAndPlace-v3", None),
+                                         ("PandaPickAndPlace-v3", "1")])
+def test_captured_steps_equal_eager_steps(pg, env_id, sort, monkeypatch):
     """capture_steps: k steps replayed from a HIP graph equal the same k steps launched eagerly, bit
     for bit (state and outputs), over two replays -- the kernels are graph-capturable (no host
-    synchronisation or allocation on the step path).  k spans an auto-reset (TimeLimit 3)."""
+    synchronisation or allocation on the step path; with PGX_SORT_ENVS=1 the heavy-first order's
+    memset and sort kernels are captured too).  k spans an auto-reset (TimeLimit 3)."""
+    if sort is not None:
+        monkeypatch.setenv("PGX_SORT_ENVS", sort)
     n, k = 96, 4
     kw = dict(num_envs=n, device="cuda:0", seed=9, max_episode_steps=3)
     eager, graphed = pg.PandaVecEnv(env_id, **kw), pg.PandaVecEnv(env_id, **kw)
