@@ -354,7 +354,6 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     PgxDevEnv& e = h->de;
     e.pcg = nullptr;
     e.perm_buf = nullptr;
-    e.sort_cnt = nullptr;
     e.perm = nullptr;
     e.sort_mode = 0;   /* PGX_SORT_ENVS: 1 always, 0 never (A/B and test hook); unset: auto */
     if (const char* so = std::getenv("PGX_SORT_ENVS")) e.sort_mode = std::atoi(so) ? 1 : -1;
@@ -437,7 +436,7 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
            off_ao = align(off_ct + 2 * PGX_CONTACT_SLOTS * N * 4),
            off_el = align(off_ao + (e.ao ? 4 * PGX_AO_OBSTACLES * N * 4 : 0)), off_ep = align(off_el + N * 4),
            off_err = align(off_ep + N * 4), off_perm = align(off_err + 4),
-           off_cnt = align(off_perm + (e.full_manifold ? N * 4 : 0)), total = align(off_cnt + (e.full_manifold ? 128 : 0));
+           total = align(off_perm + (e.full_manifold ? N * 4 + (N + 3) / 4 * 4 + (N / 256 + 1) * 13 * 4 : 0));
     rc = hip_check(hipMalloc(&h->blob, total), "hipMalloc(state)");
     if (rc) { delete h; return rc; }
     h->blob_bytes = total;
@@ -452,10 +451,7 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     h->ds.elapsed = (int32_t*)(b + off_el);
     h->ds.episode = (uint32_t*)(b + off_ep);
     h->ds.errors = (uint32_t*)(b + off_err);
-    if (e.full_manifold) {   /* heavy-first env order of the per-pair manifold kernels (not state) */
-        e.perm_buf = (int32_t*)(b + off_perm);
-        e.sort_cnt = (uint32_t*)(b + off_cnt);
-    }
+    if (e.full_manifold) e.perm_buf = (int32_t*)(b + off_perm);   /* heavy-first env order (not state) */
     h->dm_dev = (PgxDevModel*)b;
     rc = hip_check(hipMemset(h->blob, 0, total), "hipMemset(state)");
     if (!rc) rc = hip_check(hipMemcpy(h->dm_dev, &h->dm, sizeof(PgxDevModel), hipMemcpyHostToDevice), "model copy");

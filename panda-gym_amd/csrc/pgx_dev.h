@@ -72,11 +72,10 @@ struct PgxDevEnv {
                                       beyond 1024 waves), 1 the one-wave build, 2 the two-wave build */
     uint64_t* pcg;                 /* [N][4] numpy PCG64 streams of the reset draws (pgx_set_rng_streams),
                                       nullptr: the Philox counter */
-    /* heavy-first env order of the per-pair manifold kernels (pgx_launch_step): perm_buf [N] and
-     * sort_cnt [32] device buffers; sort_mode (PGX_SORT_ENVS) 0 auto (more waves than fit at once),
-     * 1 always, -1 never; perm: the order a launch uses (nullptr: identity), set by the launcher */
+    /* heavy-first env order of the per-pair manifold kernels (pgx_launch_step): perm_buf device
+     * buffer (permutation [N] i32, keys [N] u8 padded to 4 B, per-block bin counts [N/256 + 1][13]); sort_mode (PGX_SORT_ENVS) 0 auto (more waves than fit at once), 1 always, -1 never;
+     * perm: the order a launch uses (nullptr: identity), set by the launcher */
     int32_t* perm_buf;
-    uint32_t* sort_cnt;
     int32_t sort_mode;
     const int32_t* perm;
 };

@@ -4188,44 +4188,85 @@ __global__ __launch_bounds__(256) void compute_reward_kernel(const float* __rest
  * launch has more waves than the chip holds at once the dispatcher hands them out in block order:
  * grouping the envs by the robot contact points they held at the end of the previous step, most
  * first, puts the heavy envs into fewer waves and starts those first (longest-first scheduling).
- * Key = active robot slots of the warm-start cache; a counting sort (13 bins, descending) with
- * wave-aggregated atomics: the order inside a bin is arbitrary, which is harmless -- the step
- * kernels give every env the same bits whatever its wave mates (test_gpu_env_order). */
+ * Key = active robot slots of the warm-start cache.  A stable counting sort (13 bins, descending)
+ * in two launches of 256-env blocks and no atomics (nothing to clear between launches): 1. each
+ * block's keys and its per-bin counts; 2. each block sums the counts of the bins above and of the
+ * blocks before it, ranks its envs inside each bin by ballot, and writes the permutation.  (Order
+ * does not matter for the results -- the step kernels give every env the same bits whatever its
+ * wave mates, test_gpu_env_order -- but a stable sort keeps every launch reproducible.) */
 constexpr int SORT_BINS = PGX_ROBOT_POINTS + 1;
-__device__ __forceinline__ int robot_points_key(const PgxDevState& s, int N, int i, int rb) {
-    int k = 0;
-    for (int r = 0; r < rb; r++) k += s.contacts[(size_t)(CACHE1 + 2 * r) * N + i] >= 0.0f ? 1 : 0;
-    return k;
-}
-__global__ __launch_bounds__(256) void env_sort_count_kernel(PgxDevState s, int N, int rb, uint32_t* cnt) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    const int key = i < N ? robot_points_key(s, N, i, rb) : -1;
-    uint64_t todo = __ballot(key >= 0);
-    while (todo) {
-        const int k = __shfl(key, __ffsll((unsigned long long)todo) - 1);
-        const uint64_t mine = __ballot(key == k);
-        if (key == k && (__lane_id() == __ffsll((unsigned long long)mine) - 1)) atomicAdd(&cnt[k], (uint32_t)__popcll(mine));
-        todo &= ~mine;
+constexpr int SORT_BLOCK = 256;
+__global__ __launch_bounds__(SORT_BLOCK) void env_sort_keys_kernel(PgxDevState s, int N, int rb, uint8_t* keys,
+                                                                   int32_t* blk) {
+    __shared__ int32_t wc[SORT_BLOCK / 64][SORT_BINS];
+    const int i = blockIdx.x * SORT_BLOCK + threadIdx.x, lane = (int)__lane_id(), w = (int)threadIdx.x / 64;
+    int key = -1;
+    if (i < N) {
+        key = 0;
+        for (int r = 0; r < rb; r++) key += s.contacts[(size_t)(CACHE1 + 2 * r) * N + i] >= 0.0f ? 1 : 0;
+        keys[i] = (uint8_t)key;
+    }
+    for (int k = 0; k < SORT_BINS; k++) {
+        const int c = __popcll(__ballot(key == k));
+        if (lane == 0) wc[w][k] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x < SORT_BINS) {
+        int c = 0;
+        for (int ww = 0; ww < SORT_BLOCK / 64; ww++) c += wc[ww][threadIdx.x];
+        blk[(size_t)blockIdx.x * SORT_BINS + threadIdx.x] = c;
     }
 }
-__global__ __launch_bounds__(256) void env_sort_scatter_kernel(PgxDevState s, int N, int rb, uint32_t* cnt,
-                                                               int32_t* perm) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    const int key = i < N ? robot_points_key(s, N, i, rb) : -1;
-    uint64_t todo = __ballot(key >= 0);
-    while (todo) {
-        const int k = __shfl(key, __ffsll((unsigned long long)todo) - 1);
-        const uint64_t mine = __ballot(key == k);
-        const int leader = __ffsll((unsigned long long)mine) - 1;
-        uint32_t base = 0;
-        if (key == k && __lane_id() == leader) {
-            uint32_t off = 0;   /* the bins above k come first */
-            for (int b = SORT_BINS - 1; b > k; b--) off += cnt[b];
-            base = off + atomicAdd(&cnt[16 + k], (uint32_t)__popcll(mine));
+__global__ __launch_bounds__(SORT_BLOCK) void env_sort_scatter_kernel(int N, const uint8_t* keys, const int32_t* blk,
+                                                                      int32_t* perm) {
+    __shared__ int32_t base[SORT_BINS];
+    __shared__ int32_t wc[SORT_BLOCK / 64][SORT_BINS];
+    const int nb = (int)gridDim.x, me = (int)blockIdx.x;
+    const int i = me * SORT_BLOCK + threadIdx.x, lane = (int)__lane_id(), w = (int)threadIdx.x / 64;
+    /* per bin: the total over all blocks and over the blocks before this one; thread t reads the
+     * counts of blocks t, t + 256, ... (independent loads), then a wave and a block reduction */
+    __shared__ int32_t red[SORT_BLOCK / 64][2][SORT_BINS];
+    int tot[SORT_BINS], pre[SORT_BINS];
+#pragma unroll
+    for (int k = 0; k < SORT_BINS; k++) { tot[k] = 0; pre[k] = 0; }
+    for (int bb = threadIdx.x; bb < nb; bb += SORT_BLOCK) {
+#pragma unroll
+        for (int k = 0; k < SORT_BINS; k++) {
+            const int c = blk[(size_t)bb * SORT_BINS + k];
+            tot[k] += c;
+            pre[k] += bb < me ? c : 0;
         }
-        base = __shfl(base, leader);
-        if (key == k) perm[base + __popcll(mine & ((1ull << __lane_id()) - 1ull))] = i;
-        todo &= ~mine;
+    }
+#pragma unroll
+    for (int k = 0; k < SORT_BINS; k++) {
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            tot[k] += __shfl_xor(tot[k], d);
+            pre[k] += __shfl_xor(pre[k], d);
+        }
+        if (lane == 0) { red[w][0][k] = tot[k]; red[w][1][k] = pre[k]; }
+    }
+    __syncthreads();
+    if (threadIdx.x < SORT_BINS) {   /* bins above k in every block, then bin k in the blocks before */
+        const int k = threadIdx.x;
+        int off = 0;
+        for (int kk = SORT_BINS - 1; kk > k; kk--)
+            for (int ww = 0; ww < SORT_BLOCK / 64; ww++) off += red[ww][0][kk];
+        for (int ww = 0; ww < SORT_BLOCK / 64; ww++) off += red[ww][1][k];
+        base[k] = off;
+    }
+    const int key = i < N ? (int)keys[i] : -1;
+    uint64_t mine_k = 0ull;
+    for (int k = 0; k < SORT_BINS; k++) {
+        const uint64_t m = __ballot(key == k);
+        if (key == k) mine_k = m;
+        if (lane == 0) wc[w][k] = __popcll(m);
+    }
+    __syncthreads();
+    if (key >= 0) {
+        int r = base[key] + __popcll(mine_k & ((1ull << lane) - 1ull));
+        for (int ww = 0; ww < w; ww++) r += wc[ww][key];
+        perm[r] = i;
     }
 }
 
@@ -4286,16 +4327,17 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
         /* heavy-first order when the waves do not all fit at once (one per SIMD in the object
          * kernels, two in ReachAO's) */
         const unsigned resident = e.ao ? 2048u : 1024u;
-        const bool sort = e.perm_buf && e.sort_cnt && (e.sort_mode == 1 || (e.sort_mode == 0 && grid.x > resident));
+        const bool sort = e.perm_buf && (e.sort_mode == 1 || (e.sort_mode == 0 && grid.x > resident));
         PgxDevEnv es = e;
         es.perm = nullptr;
         if (sort) {
             const int rb = e.has_object ? PGX_ROBOT_POINTS : PGX_ROBOT_POINTS_ARM;
-            const dim3 sg((e.n_envs + 255) / 256), sb(256);
-            hipError_t rc = hipMemsetAsync(e.sort_cnt, 0, 32 * sizeof(uint32_t), st);
-            if (rc != hipSuccess) return (int)rc;
-            hipLaunchKernelGGL(env_sort_count_kernel, sg, sb, 0, st, s, e.n_envs, rb, e.sort_cnt);
-            hipLaunchKernelGGL(env_sort_scatter_kernel, sg, sb, 0, st, s, e.n_envs, rb, e.sort_cnt, e.perm_buf);
+            const int nb = (e.n_envs + SORT_BLOCK - 1) / SORT_BLOCK;
+            uint8_t* keys = reinterpret_cast<uint8_t*>(e.perm_buf + e.n_envs);
+            int32_t* blk = e.perm_buf + e.n_envs + (e.n_envs + 3) / 4;
+            hipLaunchKernelGGL(env_sort_keys_kernel, dim3(nb), dim3(SORT_BLOCK), 0, st, s, e.n_envs, rb, keys, blk);
+            hipLaunchKernelGGL(env_sort_scatter_kernel, dim3(nb), dim3(SORT_BLOCK), 0, st, e.n_envs,
+                               (const uint8_t*)keys, (const int32_t*)blk, e.perm_buf);
             es.perm = e.perm_buf;
         }
         const PgxDevEnv& e = es;
