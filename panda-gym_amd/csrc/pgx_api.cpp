@@ -357,6 +357,9 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     e.perm = nullptr;
     e.sort_mode = 0;   /* PGX_SORT_ENVS: 1 always, 0 never (A/B and test hook); unset: auto */
     if (const char* so = std::getenv("PGX_SORT_ENVS")) e.sort_mode = std::atoi(so) ? 1 : -1;
+    e.sort_key = 1;    /* PGX_SORT_KEY=0: only the points past the register budget (A/B hook: PickAndPlace
+                          16384 3.11 -> 3.73 ms, profiles/r04/ab_env_order_key.log) */
+    if (const char* sk = std::getenv("PGX_SORT_KEY")) e.sort_key = std::atoi(sk) ? 1 : 0;
     e.task = cfg->task;
     e.control = cfg->control;
     e.reward = cfg->reward;

@@ -77,6 +77,7 @@ struct PgxDevEnv {
      * perm: the order a launch uses (nullptr: identity), set by the launcher */
     int32_t* perm_buf;
     int32_t sort_mode;
+    int32_t sort_key;              /* PGX_SORT_KEY: 1 all robot points (default), 0 only those past CG */
     const int32_t* perm;
 };
 

@@ -4196,7 +4196,7 @@ __global__ __launch_bounds__(256) void compute_reward_kernel(const float* __rest
  * wave mates, test_gpu_env_order -- but a stable sort keeps every launch reproducible.) */
 constexpr int SORT_BINS = PGX_ROBOT_POINTS + 1;
 constexpr int SORT_BLOCK = 256;
-__global__ __launch_bounds__(SORT_BLOCK) void env_sort_keys_kernel(PgxDevState s, int N, int rb, uint8_t* keys,
+__global__ __launch_bounds__(SORT_BLOCK) void env_sort_keys_kernel(PgxDevState s, int N, int rb, int all, uint8_t* keys,
                                                                    int32_t* blk) {
     __shared__ int32_t wc[SORT_BLOCK / 64][SORT_BINS];
     const int i = blockIdx.x * SORT_BLOCK + threadIdx.x, lane = (int)__lane_id(), w = (int)threadIdx.x / 64;
@@ -4204,6 +4204,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void env_sort_keys_kernel(PgxDevState s
     if (i < N) {
         key = 0;
         for (int r = 0; r < rb; r++) key += s.contacts[(size_t)(CACHE1 + 2 * r) * N + i] >= 0.0f ? 1 : 0;
+        if (!all) key = key > CG ? key - CG : 0;
         keys[i] = (uint8_t)key;
     }
     for (int k = 0; k < SORT_BINS; k++) {
@@ -4335,7 +4336,8 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
             const int nb = (e.n_envs + SORT_BLOCK - 1) / SORT_BLOCK;
             uint8_t* keys = reinterpret_cast<uint8_t*>(e.perm_buf + e.n_envs);
             int32_t* blk = e.perm_buf + e.n_envs + (e.n_envs + 3) / 4;
-            hipLaunchKernelGGL(env_sort_keys_kernel, dim3(nb), dim3(SORT_BLOCK), 0, st, s, e.n_envs, rb, keys, blk);
+            hipLaunchKernelGGL(env_sort_keys_kernel, dim3(nb), dim3(SORT_BLOCK), 0, st, s, e.n_envs, rb, e.sort_key, keys,
+                               blk);
             hipLaunchKernelGGL(env_sort_scatter_kernel, dim3(nb), dim3(SORT_BLOCK), 0, st, e.n_envs,
                                (const uint8_t*)keys, (const int32_t*)blk, e.perm_buf);
             es.perm = e.perm_buf;
