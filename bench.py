@@ -70,6 +70,21 @@ def pmc(name: str, envs=None):
     return doc
 
 
+def pmc_kernel_ok(doc, kernel: str) -> bool:
+    """The PMC summary names this kernel: its full name, or (older summaries) the tail of the
+    template argument list after '<'."""
+    k = doc.get("kernel")
+    return k is None or k == kernel or (not k.startswith("step_kernel") and kernel.endswith("<" + k))
+
+
+def pmc_for(name: str, envs: int, kernel: str):
+    """The PMC summary when it was taken on this batch and this kernel (else None)."""
+    doc = pmc(name, envs)
+    if doc and not pmc_kernel_ok(doc, kernel):
+        return None
+    return doc
+
+
 def hbm_roofline(alg_bytes: float, ms: float, prof, kernel: str) -> dict:
     """Algorithmic bytes of one launch over its time, against the HBM peak; traffic = the PMC bytes."""
     ach = alg_bytes / (ms * 1e-3) / 1e9
@@ -116,14 +131,41 @@ def parse():
     return ap.parse_args()
 
 
+def host_cores() -> dict:
+    """The host's core counts: nproc (os.cpu_count), the cores this process may run on
+    (sched_getaffinity), the CPU share the GPU box grants a one-GPU job (OMP_NUM_THREADS, which
+    the box sets to its share) and the CPU model."""
+    nproc = os.cpu_count() or 1
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:   # pragma: no cover
+        avail = nproc
+    share = os.environ.get("OMP_NUM_THREADS")
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:   # pragma: no cover
+        pass
+    return {"nproc": nproc, "affinity": avail, "omp_num_threads": int(share) if share and share.isdigit() else None,
+            "cpu_model": model}
+
+
 def cpu_baseline(venv, seconds: float):
-    """fp64 oracle on the host cores (threads; ctypes releases the GIL) over a bounded sample."""
+    """fp64 oracle on the host cores (threads; ctypes releases the GIL) over a bounded sample: one
+    thread per core this process may use, capped by the box's CPU share for a one-GPU job
+    (OMP_NUM_THREADS, set there to the share) -- the GPU box's nproc counts the whole machine."""
     import concurrent.futures as cf
 
     from oracle import oracle as O
 
     n = venv.num_envs
-    threads = max(1, min(16, os.cpu_count() or 1))
+    hc = host_cores()
+    threads = hc["affinity"] if hc["omp_num_threads"] is None else min(hc["affinity"], hc["omp_num_threads"])
+    threads = max(1, threads)
     shards = np.array_split(np.arange(n), threads)
     envs = []
     for sh in shards:
@@ -140,9 +182,11 @@ def cpu_baseline(venv, seconds: float):
             list(ex.map(lambda e: e.step(e.sample_actions(steps)), envs))
             steps += 1
     dt = time.perf_counter() - t0
-    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port", **hc,
             "sample": f"fp64 C oracle (CPU restatement, not PyBullet): {n} PandaReach envs x {steps} steps "
-                      f"= {n * steps} env-steps in {dt:.1f} s on {threads} host threads"}
+                      f"= {n * steps} env-steps in {dt:.1f} s on {threads} host threads (nproc {hc['nproc']}, "
+                      f"{hc['affinity']} in this process's affinity, OMP_NUM_THREADS {hc['omp_num_threads']}: "
+                      f"the box's CPU share for one GPU; {hc['cpu_model']})"}
 
 
 # HER relabel leg: 16384 envs x one 50-step episode each in a 64-slot ring
@@ -253,23 +297,26 @@ def task_leg(dev, env_id: str, n: int, steps: int, contacts: bool = True, flops_
 
     venv = pg.PandaVecEnv(env_id, num_envs=n, device=dev, seed=1, contacts=contacts, full_manifold=full_manifold)
     obs_dim, act_dim, budget = venv.obs_dim, venv.action_dim, venv.robot_contact_budget()
-    venv.reset_tensors()
-    for t in range(20):
+    venv.reset_tensors(episode_phase="staggered")
+    T = venv.spec.max_episode_steps
+    for t in range(T):   # one whole episode: every env has auto-reset once, at its own step
         venv.step_tensors(venv.sample_actions(t))
+    kname = venv.step_kernel()
     stream = torch.cuda.current_stream(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
     e0.record(stream)
     for t in range(steps):
-        venv.step_tensors(venv.sample_actions(20 + t))
+        venv.step_tensors(venv.sample_actions(T + t))
     e1.record(stream)
     torch.cuda.synchronize(dev)
     ms = e0.elapsed_time(e1) / steps
     venv.close()
     res = {"env_id": env_id, "envs": n, "contacts": contacts, "robot_points": budget, "value": n / (ms * 1e-3),
-           "unit": "env-steps/s",
+           "unit": "env-steps/s", "kernel": kname,
            "ms_per_step": ms, "steps": steps,
-           "policy": "device Philox random actions (sample_actions + step per step)"}
+           "policy": "device Philox random actions (sample_actions + step per step), episode phases staggered "
+                     "(every step auto-resets ~N/50 envs), timed after one whole episode"}
     if flops_key:
         res["roofline_valu"] = valu_roofline(flops_key, res["value"], "env-steps/s of this leg (sample + step)")
     alg = None
@@ -277,14 +324,10 @@ def task_leg(dev, env_id: str, n: int, steps: int, contacts: bool = True, flops_
         alg = alg_bytes_per_env_step(flops_key, obs_dim, act_dim, budget)["total"]
     if alg:
         prof = pmc("pmc_object_kernel_" + ("push" if flops_key == "push" else "pnp"), n)
-        if budget > 4:   # the per-pair manifold kernels of the object tasks: one wave per SIMD at every batch
-            kname = "step_kernel<0, 1, 1, 0, 2> (object kernel, 16 lanes per env, per-pair manifold budget)"
-        else:
-            kname = ("step_kernel_o2<0, 1, 1, 0, 1> (object kernel, 16 lanes per env, two waves per SIMD)" if n > 4096
-                     else "step_kernel<0, 1, 1, 0, 1> (object kernel, 16 lanes per env)")
+        if budget <= 4:
             res["fidelity"] = "reduced: 4 robot contact points per env (not the per-pair manifold rule)"
-        if prof and prof.get("robot_points", 4) != budget:
-            prof = None   # PMC of another budget's kernel
+        if prof and (prof.get("robot_points", 4) != budget or not pmc_kernel_ok(prof, kname)):
+            prof = None   # PMC of another budget's / another kernel
         res["roofline"] = hbm_roofline(alg * n, ms, prof, kname)
     return res
 
@@ -337,15 +380,16 @@ def sharded_leg(dev, env_id: str, n: int, steps: int, warmup: int, dist, rank: i
 
     venv = pg.PandaVecEnv(env_id, num_envs=n, device=dev, seed=1, env_id_offset=shard_offset(rank, n))
     ab = alg_bytes_per_env_step("reach_ao", venv.obs_dim, venv.action_dim, venv.robot_contact_budget())["total"]
-    venv.reset_tensors()
+    venv.reset_tensors(episode_phase="staggered")
 
     def barrier():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    for _ in range(warmup):
+    for _ in range(venv.spec.max_episode_steps + warmup):
         venv.step_tensors(venv.sample_actions())
+    kname = venv.step_kernel()
     barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -359,12 +403,13 @@ def sharded_leg(dev, env_id: str, n: int, steps: int, warmup: int, dist, rank: i
     return {"env_id": env_id, "envs_per_gpu": n, "global_envs": world * n, "n_gpus": world,
             "value": value, "unit": "env-steps/s", "ms_per_step": elapsed / steps * 1e3,
             "steps": steps, "warmup": warmup, "scaling": "weak",
-            "policy": "device Philox random actions, in-kernel collision / success / TimeLimit auto-reset",
+            "policy": "device Philox random actions, in-kernel collision / success / TimeLimit auto-reset, "
+                      "episode phases staggered, timed after one whole episode + warmup",
+            "kernel": kname,
             "obs_digest": digest,
             "roofline_valu": valu_roofline("reach_ao", value / world, "env-steps/s per GPU of this leg"),
             # state, obstacles, contact cache, 56-float obs
-            "roofline": hbm_roofline(ab * n, elapsed / steps * 1e3, pmc("pmc_reach_ao_kernel", n),
-                                     "step_kernel_o2<1, 0, 1, 1, 1> (ReachAO, 16 lanes per env)")}
+            "roofline": hbm_roofline(ab * n, elapsed / steps * 1e3, pmc_for("pmc_reach_ao_kernel", n, kname), kname)}
 
 
 def launch_ranks(n: int) -> int:
@@ -412,18 +457,21 @@ def main():
     E = args.envs
     venv = pg.PandaVecEnv(args.env_id, num_envs=E, device=dev, seed=args.seed,
                           env_id_offset=shard_offset(rank, E))
-    venv.reset_tensors()
+    # steady state: staggered episode phases (global env g starts its TimeLimit counter at g mod 50),
+    # so every step auto-resets ~E/50 envs as in a long VecEnv rollout, and one whole episode before
+    # the warmup steps, so every env has reset once and no env still holds the at-rest start pose --
+    # any window of steps is then the steady-state mix (with all envs in phase, a 20-step window is
+    # a fixed, cheaper slice of the episode; profiles/r04)
+    venv.reset_tensors(episode_phase="staggered")
 
     def barrier():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    # steady state: one whole episode (the TimeLimit, 50 steps) before the warmup steps, so the timed
-    # window sits past the first auto-resets wherever --steps / --warmup put it (the first episode's
-    # early steps are cheaper: the arm starts at rest, no env resets)
     for _ in range(venv.spec.max_episode_steps + args.warmup):
         venv.step_tensors(venv.sample_actions())
+    kname = venv.step_kernel()
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -494,7 +542,7 @@ def main():
         if os.path.exists(PROFILE_JSON):
             with open(PROFILE_JSON) as f:
                 prof = json.load(f)
-            if prof.get("num_envs") == E:
+            if prof.get("num_envs") == E and pmc_kernel_ok(prof, kname):
                 traffic = prof.get("hbm_bytes_per_launch")
                 ins = prof.get("valu_lane_ops_per_launch")
                 if ins and valu:
@@ -513,8 +561,12 @@ def main():
             # the step kernel alone: HIP events over --kernel-launches back-to-back launches on the launch
             # stream right after the timed window (launch gaps included; rocprof's kernel average,
             # profiles/, is the gap-free duration)
-            "kernel_ms": kernel_ms, "steady_state": f"timed after {venv.spec.max_episode_steps} + {args.warmup} "
-                                                    f"untimed steps (one whole episode: auto-resets in the window)",
+            "kernel_ms": kernel_ms,
+            "steady_state": f"episode phases staggered (env g starts its TimeLimit counter at g mod "
+                            f"{venv.spec.max_episode_steps}: every step auto-resets ~{E // venv.spec.max_episode_steps} "
+                            f"envs), timed after {venv.spec.max_episode_steps} + {args.warmup} untimed steps "
+                            f"(every env has auto-reset at least once)",
+            "kernel": kname,
             "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: device Philox random policy U[-1,1)^3, 50-step episodes with in-kernel auto-reset",
             "config": {"workload": f"{args.env_id} (ee control, sparse reward), {E} envs per GPU, the "
@@ -527,7 +579,7 @@ def main():
                          "binds": "dependent VALU issue of one wave per SIMD (see roofline_valu)",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "step_kernel<0, 0, 1, 0, 1> (ee control, no object, table contacts, 16 lanes per env)",
+                         "kernel": kname,
                          "kernel_ms": kernel_ms,
                          "alg_bytes_per_launch": alg_bytes},
             "roofline_valu": valu,

@@ -62,6 +62,18 @@ extern "C" {
 #define PGX_ROBOT_POINTS_ONE_LANE 4
 #define PGX_CONTACT_SLOTS (PGX_OBJECT_POINTS + PGX_ROBOT_POINTS)
 #define PGX_CONTACTS_FULL 2
+/* Bullet's persistent contact manifolds of the robot's pairs with the cube and with the obstacles
+ * (PGX_CONTACTS_FULL; btPersistentManifold): a pool of at most
+ * PGX_MANIFOLD_POOL (Push / PickAndPlace) or PGX_MANIFOLD_POOL_AO (ReachAO) points per env, kept
+ * across substeps and steps -- the point count, then per point in pool order PGX_MANIFOLD_POINT
+ * values: kid = key + slot (key 32 + 16 c for capsule c against the cube, 32 + 24 c + 4 o against
+ * obstacle o; slot = the point's index in its manifold, < 4), local A [3] (in the frame of the arm
+ * joint that carries the capsule), local B [3] (cube frame; world for a static obstacle), normal on
+ * B [3] (world, from B to the robot), distance, applied normal impulse.  The row id of a point is
+ * its kid. */
+#define PGX_MANIFOLD_POOL 16
+#define PGX_MANIFOLD_POOL_AO 8
+#define PGX_MANIFOLD_POINT 12
 
 #define PGX_OK 0
 #define PGX_E_INVALID -1
@@ -176,10 +188,13 @@ typedef struct pgx_sim_params {
 #define PGX_FLAG_DYN_RECURSIVE 16         /* M and b by composite rigid bodies + Newton-Euler (the
                                              kernel's formulation; same dynamics) instead of the
                                              Jacobian form: for the operation count */
-#define PGX_FLAG_PERSISTENT_MANIFOLD 32   /* robot contacts from Bullet's persistent manifolds (points
-                                             kept across substeps, refreshed, broken past 0.02,
-                                             replaced by largest area) instead of each pair's 4
-                                             deepest candidates of the substep */
+#define PGX_FLAG_PERSISTENT_MANIFOLD 32   /* study: with PGX_CONTACTS_FULL, the robot's table / plane
+                                             pairs through persistent manifolds too (each end sphere's
+                                             manifold holds its one re-reported point, so it equals
+                                             the fresh table rule to rounding: a test pins that) */
+#define PGX_FLAG_FRESH_MANIFOLD 64        /* study: with PGX_CONTACTS_FULL, round 4's rule for the cube /
+                                             obstacle pairs -- each pair's 4 deepest candidates of the
+                                             substep -- instead of Bullet's persistent manifolds */
 
 typedef struct pgx_config {
     int32_t task;                 /* PGX_TASK_* */
@@ -269,6 +284,12 @@ typedef struct pgx_state_view {
     uint32_t* episode;  /* [N] episodes finished (RNG counter) */
     uint32_t* errors;   /* [1] sticky PGX_ERR_* bits set by the kernels; the host clears them */
     int32_t robot_points;  /* the robot contact budget of this handle's kernels (0: no contacts) */
+    int32_t* env_order;    /* [N] the env order of the last step launch that sorted its envs heavy-first
+                              (per-pair manifold kernels; position -> env id), NULL without one;
+                              not state (the next sorted launch rewrites it) */
+    float* manifolds;      /* [1 + manifold_pool * PGX_MANIFOLD_POINT][N] the persistent manifold pool
+                              (PGX_MANIFOLD_POOL above), NULL without one */
+    int32_t manifold_pool; /* its capacity in points (0: none) */
 } pgx_state_view;
 
 /* errors word (pgx_state_view.errors): a device-side reset that cannot complete the way the
@@ -300,6 +321,10 @@ int pgx_reset(pgx_handle h, const uint8_t* env_mask, const double* inject_goal,
 
 /* One lockstep env step for all N envs: action [N,A] f32 (device). */
 int pgx_step(pgx_handle h, const float* action, pgx_step_out* out, void* stream);
+/* The step kernel the last pgx_step on h launched, as rocprof names it (e.g.
+ * "step_kernel<0, 0, 1, 0, 2>"; NULL before the first step): the label a benchmark reports beside
+ * its kernel time and profiles. */
+const char* pgx_step_kernel(pgx_handle h);
 
 /* Fill action [N,A] with U[-1,1) from the device Philox stream (benchmark
  * random policy; counter = (global env id, step)). */
@@ -328,15 +353,21 @@ int pgx_snapshot(pgx_handle h, int32_t* state_id, void* stream);
 int pgx_restore(pgx_handle h, int32_t state_id, void* stream);
 int pgx_release(pgx_handle h, int32_t state_id);
 
-/* Reset draws from numpy PCG64 streams instead of the device Philox counter: the goal / object
- * draws of every later reset of env i -- pgx_reset without injection and the step's auto-reset --
- * come from stream i in the task's order (reach.py:75-78, push.py:75-87,
- * pick_and_place.py:71-85), as gymnasium's env.np_random (core.py:302) continues across the
- * resets of an SB3 VecEnv.  states: [N][4] uint64 per env {state_lo, state_hi, inc_lo, inc_hi}
- * of numpy's PCG64 (bit_generator.state["state"]), host or device memory, copied on `stream`;
- * NULL returns to Philox.  An injected reset leaves its env's stream untouched.  Streams are not
- * part of the saved state (restoreState keeps np_random as it is).  ReachAO: PGX_E_UNSUPPORTED.
- * pgx_get_rng_streams copies the current records out ([N][4], host or device memory). */
+/* Reset draws from numpy PCG64 streams instead of the device Philox counter (a
+ * seeded reset drawn on the device, no host injection).  RobotTaskEnv.reset reseeds the task's
+ * generator on EVERY reset, task.np_random = seeding.np_random(seed) (core.py:302): a reset with
+ * seed s draws from PCG64(SeedSequence(s)), which is what a record set from s reproduces bit for bit
+ * (goal / object in the task's order, reach.py:75-78, push.py:75-87, pick_and_place.py:71-85).  A
+ * reset without a seed -- the step's auto-reset included -- gets a fresh OS-entropy generator in the
+ * reference, so no reference value exists for it: here it continues stream i, a reproducible
+ * stand-in with the same distribution, not the reference's draws.  states: [N][4] uint64 per env
+ * {state_lo, state_hi, inc_lo, inc_hi} of numpy's PCG64 (bit_generator.state["state"]), host or
+ * device memory, copied on `stream`; NULL returns to Philox.  The mode is a device word switched on
+ * `stream` and the stream buffer lives as long as the handle, so a step loop captured in a HIP graph
+ * draws in the mode of replay time.  An injected reset leaves its env's stream untouched.  Streams
+ * are not part of the saved state (restoreState keeps np_random as it is).  ReachAO:
+ * PGX_E_UNSUPPORTED.  pgx_get_rng_streams copies the current records out ([N][4], host or device
+ * memory). */
 int pgx_set_rng_streams(pgx_handle h, const uint64_t* states, void* stream);
 int pgx_get_rng_streams(pgx_handle h, uint64_t* states, void* stream);
 

@@ -105,9 +105,10 @@ OBJ_CACHE = 13
 OBJ_CACHE1 = OBJ_CACHE + 2 * OBJECT_POINTS
 OBJ_AO = OBJ_CACHE1 + 2 * ROBOT_MAX   # ReachAO: obstacle centres [6][3], active flags [6] at OBJ_AO + 18
 OBJ_QC = OBJ_AO + 24
-MAN, MAN_PT = 16, 11          # PGX_FLAG_PERSISTENT_MANIFOLD: manifolds per env, doubles per point
-OBJ_MAN = OBJ_QC + 7          # [MAN][key + 1, count, 4 x (local A, local B, normal, distance, impulse)]
-OBJ_N = OBJ_MAN + MAN * (2 + 4 * MAN_PT)
+POOL_MAX, MAN_PT = 48, 12     # PGXO_POOL_MAX, PGX_MANIFOLD_POINT: the persistent manifold pool
+OBJ_MAN = OBJ_QC + 7          # count, then POOL_MAX x (kid, local A, local B, normal, distance, impulse)
+OBJ_N = OBJ_MAN + 1 + POOL_MAX * MAN_PT
+MP_KID, MP_LA, MP_LB, MP_N, MP_D, MP_IMP = 0, 1, 4, 7, 10, 11
 ROBOT_HIST = 33
 
 
@@ -135,26 +136,42 @@ def last_contacts():
     return g[:n], i[:n], l[:n], d[:n]
 
 
-def manifold_add(M: np.ndarray, point: np.ndarray, thr: float = 0.02) -> int:
-    """btPersistentManifold addContactPoint on one manifold M [2 + 4 * MAN_PT] (in place); the slot."""
-    lib().pgxo_manifold_add.argtypes = [C.c_void_p, C.c_void_p, C.c_double]
-    return int(lib().pgxo_manifold_add(_p(M), _p(_d(point)), thr))
+def manifold_add(P: np.ndarray, key: int, point: np.ndarray, thr: float = 0.02, cap: int = POOL_MAX) -> int:
+    """btPersistentManifold addContactPoint of point (MAN_PT: kid, local A, local B, normal, distance,
+    impulse -- kid and impulse ignored) to manifold `key` of pool P [1 + cap * MAN_PT] (in place);
+    the slot it went to, -1 when the pool was full."""
+    lib().pgxo_manifold_add.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_double]
+    return int(lib().pgxo_manifold_add(_p(P), int(cap), int(key), _p(_d(point)), thr))
 
 
-def manifold_refresh_static(M: np.ndarray, thr: float = 0.02) -> None:
-    """refreshContactPoints of one manifold whose bodies did not move (local = world), in place."""
+def manifold_refresh_static(P: np.ndarray, thr: float = 0.02) -> None:
+    """refreshContactPoints of every manifold in pool P whose bodies did not move (local = world)."""
     lib().pgxo_manifold_refresh_static.argtypes = [C.c_void_p, C.c_double]
-    lib().pgxo_manifold_refresh_static(_p(M), thr)
+    lib().pgxo_manifold_refresh_static(_p(P), thr)
+
+
+def pool(obj_row: np.ndarray) -> np.ndarray:
+    """The manifold pool of one env's obj row: its points [count, MAN_PT] in pool order."""
+    n = int(obj_row[OBJ_MAN])
+    return obj_row[OBJ_MAN + 1:OBJ_MAN + 1 + n * MAN_PT].reshape(n, MAN_PT).copy()
 
 
 def manifolds(obj_row: np.ndarray) -> list:
-    """The persistent manifolds of one env's obj row: [(key, points [n, MAN_PT])]."""
-    out = []
-    for mi in range(MAN):
-        M = obj_row[OBJ_MAN + mi * (2 + 4 * MAN_PT):OBJ_MAN + (mi + 1) * (2 + 4 * MAN_PT)]
-        if M[0] != 0:
-            out.append((int(M[0]) - 1, M[2:2 + int(M[1]) * MAN_PT].reshape(-1, MAN_PT).copy()))
-    return out
+    """The persistent manifolds of one env's obj row: [(key, points [n, MAN_PT] by slot)], keys in
+    order of first appearance in the pool."""
+    pts = pool(obj_row)
+    out = {}
+    for p in pts:
+        kid = int(p[MP_KID])
+        out.setdefault(kid & ~3, {})[kid & 3] = p
+    return [(k, np.stack([v[s] for s in sorted(v)])) for k, v in out.items()]
+
+
+def set_manifolds(obj: np.ndarray, man: np.ndarray) -> None:
+    """obj[:, pool] from the kernels' pool [1 + pool * MAN_PT] per env (pgx_state_view.manifolds)."""
+    man = np.asarray(man, dtype=np.float64)
+    obj[:, OBJ_MAN:OBJ_N] = 0.0
+    obj[:, OBJ_MAN:OBJ_MAN + man.shape[1]] = man
 
 
 def set_contact_cache(obj: np.ndarray, cache: np.ndarray) -> None:

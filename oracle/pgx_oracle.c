@@ -514,13 +514,11 @@ static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x >
 #define OBJ_CACHE1 (OBJ_CACHE + 2 * PGX_OBJECT_POINTS)
 #define OBJ_AO (OBJ_CACHE1 + 2 * PGXO_ROBOT_MAX)
 #define OBJ_QC (OBJ_AO + 4 * PGX_AO_OBSTACLES)
-/* PGX_FLAG_PERSISTENT_MANIFOLD: the robot pairs' persistent manifolds, PGXO_MAN x (key + 1 (0 =
- * free), point count, MANIFOLD_CACHE_SIZE x point: local A [3], local B [3], normal on B [3],
- * distance, applied normal impulse) */
-#define MAN_PT 11
-#define MAN_SZ (2 + 4 * MAN_PT)
+/* the persistent manifold pool (pgx.h PGX_MANIFOLD_POOL): count, then PGXO_POOL_MAX points of
+ * MAN_PT doubles (kid, local A [3], local B [3], normal on B [3], distance, impulse) */
+#define MAN_PT PGX_MANIFOLD_POINT
 #define OBJ_MAN (OBJ_QC + 7)
-#define OBJ_N (OBJ_MAN + PGXO_MAN * MAN_SZ)
+#define OBJ_N (OBJ_MAN + 1 + PGXO_POOL_MAX * MAN_PT)
 #define N_CACHE (PGX_OBJECT_POINTS + PGXO_ROBOT_MAX)
 typedef char obj_layout_check[(OBJ_N == PGXO_OBJ_N) ? 1 : -1];
 static void quat_mul(const double* a, const double* b, double* o);
@@ -536,11 +534,17 @@ void pgxo_set_robot_budget(int b) { robot_budget = b < 0 ? -1 : (b > PGXO_ROBOT_
 void pgxo_pair_hist_read(int64_t* out, int clear) {
     for (int i = 0; i < PGXO_ROBOT_HIST; i++) { out[i] = pgxo_pair_hist[i]; if (clear) pgxo_pair_hist[i] = 0; }
 }
+/* per-thread scratch: bench.py's cpu_baseline steps one env shard per host thread */
+#ifdef __cplusplus
+#define PGXO_TLS thread_local
+#else
+#define PGXO_TLS _Thread_local
+#endif
 /* the last detection's points (tests): group, feature id, link, separation */
-static int last_n;
-static int last_grp[PGX_OBJECT_POINTS + PGXO_ROBOT_MAX], last_id[PGX_OBJECT_POINTS + PGXO_ROBOT_MAX],
+static PGXO_TLS int last_n;
+static PGXO_TLS int last_grp[PGX_OBJECT_POINTS + PGXO_ROBOT_MAX], last_id[PGX_OBJECT_POINTS + PGXO_ROBOT_MAX],
     last_link[PGX_OBJECT_POINTS + PGXO_ROBOT_MAX];
-static double last_dist[PGX_OBJECT_POINTS + PGXO_ROBOT_MAX];
+static PGXO_TLS double last_dist[PGX_OBJECT_POINTS + PGXO_ROBOT_MAX];
 int pgxo_last_contacts(int32_t* grp, int32_t* id, int32_t* link, double* dist) {
     for (int i = 0; i < last_n; i++) { grp[i] = last_grp[i]; id[i] = last_id[i]; link[i] = last_link[i]; dist[i] = last_dist[i]; }
     return last_n;
@@ -549,8 +553,9 @@ int pgxo_last_contacts(int32_t* grp, int32_t* id, int32_t* link, double* dist) {
 typedef struct {
     int grp, id, link;
     double n[3], pa[3], pb[3], dist;
-    double* mp;   /* persistent mode: the manifold point the solved impulse goes back to, else NULL */
-    double imp;   /* persistent mode: the point's applied impulse (warm start) */
+    double* mp;   /* a manifold point: where the solved impulse goes back to, else NULL */
+    double imp;   /* a manifold point: its applied impulse (warm start) */
+    int sub;      /* row order after id (the study mode's table manifolds: the slot) */
 } contact_t;
 
 typedef struct {
@@ -614,9 +619,11 @@ static int select_points(const cands_t* s, int budget, contact_t* out, int* n_pa
     if (n_pair) *n_pair = np;
     return n;
 }
-static void sort_by_id(contact_t* s, int n) {
+static void sort_by_id(contact_t* s, int n) {   /* by (id, sub) */
     for (int i = 1; i < n; i++)
-        for (int j = i; j > 0 && s[j].id < s[j - 1].id; j--) { contact_t t = s[j]; s[j] = s[j - 1]; s[j - 1] = t; }
+        for (int j = i; j > 0 && (s[j].id < s[j - 1].id || (s[j].id == s[j - 1].id && s[j].sub < s[j - 1].sub)); j--) {
+            contact_t t = s[j]; s[j] = s[j - 1]; s[j - 1] = t;
+        }
 }
 
 /* number of sample spheres along a capsule (spacing <= r/2) */
@@ -628,46 +635,77 @@ static int capsule_samples(const double* a, const double* b, double r) {
 }
 
 enum { PAIR_TABLE = 0, PAIR_PLANE = 1, PAIR_CUBE = 2, PAIR_OBSTACLE = 3 };   /* + 16 x capsule */
-/* ---- Bullet's persistent contact manifold (oracle flag PGX_FLAG_PERSISTENT_MANIFOLD): the
- * robot pairs' points persist across substeps.  Restated from btPersistentManifold /
- * btManifoldResult (Bullet 3, the algorithm pybullet 3.2.6 runs; not vendored): per colliding
- * pair (a capsule's end sphere against the table or the plane -- each sphere is a child shape of
- * the link compound with a manifold of its own --, the capsule against the cube or an obstacle)
- * the narrow phase reports one new point per stepSimulation (a sphere's closest point; for the
- * convex capsule vs a box GJK's closest pair, restated as the deepest sample), which
- * addContactPoint either merges into the cached point nearest to it within the breaking
- * threshold in A's local frame (getCacheEntry: the new point replaces it and keeps its applied
- * impulse) or appends -- with 4 points cached, sortCachedPoints replaces the one whose removal
- * leaves the largest area, never the deepest -- then refreshContactPoints moves every cached
- * point with its bodies (local -> world), recomputes its distance along the stored normal and
- * drops it past the breaking threshold (0.02) or when it slid more than that sideways.  Every
- * manifold point is a solver row; its normal impulse is written back and warm-starts it in the
- * next substep (x 0.85). */
-static void man_world(const kin_t* k, const double* obj, int li, int code, const double* P, double* pa, double* pb) {
-    m3_v(k->R[li], P, pa);
-    for (int i = 0; i < 3; i++) pa[i] += k->o[li][i];
-    if (code == 4) {   /* cube: B's local frame moves with it */
-        double Rc[9];
-        quat_to_mat(obj + 3, Rc);
-        m3_v(Rc, P + 3, pb);
-        for (int i = 0; i < 3; i++) pb[i] += obj[i];
-    } else {           /* table / plane / obstacle: static, local = world */
-        memcpy(pb, P + 3, 3 * sizeof(double));
-    }
+
+/* ---- Bullet's persistent contact manifold (btPersistentManifold / btManifoldResult, Bullet 3 as
+ * pybullet 3.2.6 runs it; not vendored).  The default with PGX_CONTACTS_FULL for the robot's pairs
+ * with the cube and with the obstacles: per pair (a capsule against the cube or an obstacle) the
+ * narrow phase reports one new point per stepSimulation -- GJK's closest pair of the convex
+ * capsule and the box, restated as the pair's deepest sample (ties: the lowest sample); the exact
+ * closest pair for an obstacle -- and addContactPoint (btManifoldResult) merges it:
+ *   getCacheEntry: the cached point nearest to it in A's local frame, strictly within the breaking
+ *     threshold squared (0.02^2), first in slot order -> replaceContactPoint: the new point's
+ *     positions, normal and distance, the cached applied impulse kept (MAINTAIN_PERSISTENCY);
+ *   else addManifoldPoint: appended below MANIFOLD_CACHE_SIZE = 4, else sortCachedPoints picks
+ *     the slot to overwrite (impulse 0): the slot whose replacement leaves the largest
+ *     |(pt - c_a) x (c_b - c_c)|^2 ("gContactCalcArea3Points"), never the point deeper than the
+ *     new one and every other (KEEP_DEEPEST_POINT), the first on ties (maxAxis4);
+ * then refreshContactPoints moves every cached point with its bodies (local -> world), recomputes
+ * its distance along the stored normal, and in reverse slot order removes a point past the
+ * breaking threshold (validContactDistance) or whose B point slid more than the threshold off A's
+ * projection (removeContactPoint: the last slot's point fills the hole).  Every manifold point is
+ * a solver row warm-started from its own applied impulse (x 0.85) and written back after the solve.
+ * The robot's end spheres against the table / plane keep the fresh rule: each is a child shape with
+ * a manifold of its own whose one point is re-reported every substep (merged into itself, impulse
+ * kept), i.e. the fresh candidate with its feature's warm start -- PGX_FLAG_PERSISTENT_MANIFOLD runs
+ * them through manifolds too, and a test pins the two to rounding.  Cube vs table / plane: the box-box
+ * detector re-reports all (<= 4) points every substep, restated as its 4 deepest vertices.
+ * Kept per env in a pool of at most PGX_MANIFOLD_POOL (PGX_MANIFOLD_POOL_AO) points, the kernel's
+ * layout (pgx.h): a point that would need a new pool entry when the pool is full is dropped and
+ * counted (pgxo_diag_hist[120]; not reached in the configs' random-policy runs).  Merge order:
+ * the cube pairs by capsule, the obstacle pairs obstacle-major (the kernels' lane-parallel order);
+ * a new point's pool entry goes last, removals keep the others' order. */
+enum { MP_KID = 0, MP_LA = 1, MP_LB = 4, MP_N = 7, MP_D = 10, MP_IMP = 11 };
+#define KEY_TABLE 1024   /* study mode: 1024 + 64 c + 8 (table 0 / plane 1) + 4 end */
+
+static double* pool_pt(double* P, int i) { return P + 1 + MAN_PT * i; }
+/* the arm link whose frame carries capsule ci (its own or the nearest ancestor with a moving joint:
+ * the fixed links past panda_link7 ride on it) -- the kernels' kCapJ joint frame */
+static int cap_frame_link(const pgx_model* m, int ci) {
+    int l = m->cap_link[ci];
+    while (l >= 0 && m->dof_of_link[l] < 0) l = m->parent[l];
+    return l;
 }
-static int man_sort_cached(const double* M, const double* np) {   /* btPersistentManifold::sortCachedPoints */
+/* manifold key -> capsule; its B body is the cube (has_object), an obstacle or the table */
+static int key_capsule(int key, int has_object) {
+    if (key >= KEY_TABLE) return (key - KEY_TABLE) / 64;
+    return has_object ? (key - 32) / 16 : (key - 32) / 24;
+}
+/* the points of manifold `key` by slot (idx[slot] = pool index); their count */
+static int man_points(double* P, int key, int idx[4]) {
+    int n = 0;
+    const int cnt = (int)P[0];
+    for (int i = 0; i < cnt; i++) {
+        const int kid = (int)pool_pt(P, i)[MP_KID];
+        if ((kid & ~3) == key) { idx[kid & 3] = i; n++; }
+    }
+    return n;
+}
+static int man_sort_cached(double* P, const int idx[4], const double* np) {   /* sortCachedPoints */
     const double* c[4];
-    for (int i = 0; i < 4; i++) c[i] = M + 2 + MAN_PT * i;
+    for (int i = 0; i < 4; i++) c[i] = pool_pt(P, idx[i]);
     int maxi = -1;
-    double maxpen = np[9];
+    double maxpen = np[MP_D];
     for (int i = 0; i < 4; i++)
-        if (c[i][9] < maxpen) { maxi = i; maxpen = c[i][9]; }
+        if (c[i][MP_D] < maxpen) { maxi = i; maxpen = c[i][MP_D]; }
     double res[4] = {0, 0, 0, 0};
     static const int ia[4] = {1, 0, 0, 0}, ib[4] = {3, 3, 3, 2}, ic[4] = {2, 2, 1, 1};
     for (int i = 0; i < 4; i++) {
         if (i == maxi) continue;
         double a[3], b[3], x[3];
-        for (int j = 0; j < 3; j++) { a[j] = np[j] - c[ia[i]][j]; b[j] = c[ib[i]][j] - c[ic[i]][j]; }
+        for (int j = 0; j < 3; j++) {
+            a[j] = np[MP_LA + j] - c[ia[i]][MP_LA + j];
+            b[j] = c[ib[i]][MP_LA + j] - c[ic[i]][MP_LA + j];
+        }
         v3_cross(a, b, x);
         res[i] = v3_dot(x, x);
     }
@@ -676,134 +714,119 @@ static int man_sort_cached(const double* M, const double* np) {   /* btPersisten
         if (res[i] > res[best]) best = i;
     return best;
 }
-/* addContactPoint: merge into the cached point nearest in A's local frame within the breaking
- * threshold (getCacheEntry; replaceContactPoint keeps its applied impulse), else append, else
- * (4 cached) replace by sortCachedPoints; returns the slot.  M = (key + 1, count, points). */
-static int man_add(double* M, const double* np, double thr2) {
-    const int n = (int)M[1];
+/* addContactPoint of np (MP layout; kid and impulse ignored) to manifold `key`; returns the slot
+ * it went to, -1 when the pool was full */
+static int man_add(double* P, int cap, int key, const double* np, double thr2) {
+    int idx[4];
+    const int n = man_points(P, key, idx);
     int near = -1;
     double sh = thr2;
     for (int i = 0; i < n; i++) {   /* getCacheEntry */
-        const double* P = M + 2 + MAN_PT * i;
-        double e[3] = {P[0] - np[0], P[1] - np[1], P[2] - np[2]};
+        const double* c = pool_pt(P, idx[i]);
+        double e[3] = {c[MP_LA] - np[MP_LA], c[MP_LA + 1] - np[MP_LA + 1], c[MP_LA + 2] - np[MP_LA + 2]};
         const double dd = v3_dot(e, e);
         if (dd < sh) { sh = dd; near = i; }
     }
-    if (near >= 0) {           /* replaceContactPoint: the cached impulse stays */
-        double* P = M + 2 + MAN_PT * near;
-        const double imp = P[10];
-        memcpy(P, np, MAN_PT * sizeof(double));
-        P[10] = imp;
+    if (near >= 0) {   /* replaceContactPoint: the cached impulse stays */
+        double* c = pool_pt(P, idx[near]);
+        memcpy(c + MP_LA, np + MP_LA, (MP_IMP - MP_LA) * sizeof(double));
         return near;
     }
     if (n < 4) {
-        memcpy(M + 2 + MAN_PT * n, np, MAN_PT * sizeof(double));
-        M[1] = n + 1;
+        const int cnt = (int)P[0];
+        if (cnt >= cap) { pgxo_diag_hist[120]++; return -1; }
+        double* c = pool_pt(P, cnt);
+        memcpy(c, np, MAN_PT * sizeof(double));
+        c[MP_KID] = key + n;
+        c[MP_IMP] = 0.0;
+        P[0] = cnt + 1;
         return n;
     }
-    const int slot = man_sort_cached(M, np);
-    memcpy(M + 2 + MAN_PT * slot, np, MAN_PT * sizeof(double));
+    const int slot = man_sort_cached(P, idx, np);
+    double* c = pool_pt(P, idx[slot]);
+    memcpy(c + MP_LA, np + MP_LA, (MP_IMP - MP_LA) * sizeof(double));
+    c[MP_IMP] = 0.0;
     return slot;
 }
-/* refreshContactPoints with the cached points' world positions pa, pb: distance along the
- * stored normal, then (in reverse order) drop a point past the breaking threshold or one whose
- * B point slid more than it sideways off A's (removeContactPoint: the last point fills the hole) */
-static void man_refresh(double* M, const double (*pa)[3], const double (*pb)[3], double thr) {
-    int n = (int)M[1];
-    double wa[4][3], wb[4][3];
-    for (int i = 0; i < n; i++) {
-        double* P = M + 2 + MAN_PT * i;
-        memcpy(wa[i], pa[i], sizeof wa[i]);
-        memcpy(wb[i], pb[i], sizeof wb[i]);
-        P[9] = (pa[i][0] - pb[i][0]) * P[6] + (pa[i][1] - pb[i][1]) * P[7] + (pa[i][2] - pb[i][2]) * P[8];
-    }
-    for (int i = n - 1; i >= 0; i--) {
-        double* P = M + 2 + MAN_PT * i;
-        int drop = P[9] > thr;
-        if (!drop) {
+/* refreshContactPoints of every manifold in the pool, from the points' world positions pa, pb:
+ * distance along the stored normal, then per manifold in reverse slot order the removals (the
+ * last slot's point takes a removed point's slot); the pool keeps the survivors' order */
+static void pool_refresh(double* P, const double (*pa)[3], const double (*pb)[3], double thr) {
+    const int cnt = (int)P[0];
+    int drop[PGXO_POOL_MAX];
+    for (int i = 0; i < cnt; i++) {
+        double* c = pool_pt(P, i);
+        const double* n = c + MP_N;
+        const double d = (pa[i][0] - pb[i][0]) * n[0] + (pa[i][1] - pb[i][1]) * n[1] + (pa[i][2] - pb[i][2]) * n[2];
+        c[MP_D] = d;
+        drop[i] = d > thr;
+        if (!drop[i]) {
             double e[3];
-            for (int j = 0; j < 3; j++) e[j] = wb[i][j] - (wa[i][j] - P[6 + j] * P[9]);
-            drop = v3_dot(e, e) > thr * thr;
-        }
-        if (drop) {
-            if (i != n - 1) {
-                memcpy(P, M + 2 + MAN_PT * (n - 1), MAN_PT * sizeof(double));
-                memcpy(wa[i], wa[n - 1], sizeof wa[i]);
-                memcpy(wb[i], wb[n - 1], sizeof wb[i]);
-            }
-            n--;
+            for (int j = 0; j < 3; j++) e[j] = pb[i][j] - (pa[i][j] - n[j] * d);
+            drop[i] = v3_dot(e, e) > thr * thr;
         }
     }
-    M[1] = n;
-}
-/* test entry points: one manifold whose bodies do not move (local = world) */
-int pgxo_manifold_add(double* M, const double* point, double thr) { return man_add(M, point, thr * thr); }
-void pgxo_manifold_refresh_static(double* M, double thr) {
-    double pa[4][3], pb[4][3];
-    for (int i = 0; i < (int)M[1]; i++)
-        for (int j = 0; j < 3; j++) { pa[i][j] = M[2 + MAN_PT * i + j]; pb[i][j] = M[2 + MAN_PT * i + 3 + j]; }
-    man_refresh(M, pa, pb, thr);
-}
-static void persistent_manifolds(const pgx_model* m, const pgx_sim_params* p, const kin_t* k, double* obj,
-                                 const cands_t* s1) {
-    const double thr = p->contact_distance, thr2 = thr * thr;
-    double* man = obj + OBJ_MAN;
-    /* 1. the pairs' new points: per pair its deepest candidate (the first on a tie) */
-    int nk = 0, keys[CAND_MAX], best[CAND_MAX];
-    for (int i = 0; i < s1->n; i++) {
-        const int ci = s1->pair[i] >> 4, code = s1->pair[i] & 15;
-        const int key = (code == PAIR_TABLE || code == PAIR_PLANE) ? ci * 32 + 2 * code + (s1->c[i].id & 1)
-                      : code == PAIR_CUBE ? ci * 32 + 4 : ci * 32 + 8 + (code - PAIR_OBSTACLE);
-        int j = 0;
-        while (j < nk && keys[j] != key) j++;
-        if (j == nk) { keys[nk] = key; best[nk] = i; nk++; }
-        else if (s1->c[i].dist < s1->c[best[j]].dist) best[j] = i;
+    int seen[PGXO_POOL_MAX] = {0};
+    for (int i = 0; i < cnt; i++) {
+        const int key = (int)pool_pt(P, i)[MP_KID] & ~3;
+        if (seen[i]) continue;
+        int cur[4];
+        int n = man_points(P, key, cur);
+        for (int s2 = 0; s2 < n; s2++) seen[cur[s2]] = 1;
+        for (int s2 = n - 1; s2 >= 0; s2--)
+            if (drop[cur[s2]]) { cur[s2] = cur[n - 1]; n--; }
+        for (int s2 = 0; s2 < n; s2++) pool_pt(P, cur[s2])[MP_KID] = key + s2;
     }
-    /* 2. addContactPoint: merge into the nearest cached point or add */
-    for (int j = 0; j < nk; j++) {
-        const contact_t* c = &s1->c[best[j]];
-        const int key = keys[j], code = key & 31, li = c->link;
-        double* M = NULL;
-        for (int mi = 0; mi < PGXO_MAN && !M; mi++)
-            if ((int)man[MAN_SZ * mi] == key + 1) M = man + MAN_SZ * mi;
-        for (int mi = 0; mi < PGXO_MAN && !M; mi++)
-            if (man[MAN_SZ * mi] == 0.0) { M = man + MAN_SZ * mi; M[0] = key + 1; M[1] = 0; }
-        if (!M) continue;   /* (more pairs than PGXO_MAN: not reached in the configs) */
-        double np[MAN_PT], d[3];
-        for (int i = 0; i < 3; i++) d[i] = c->pa[i] - k->o[li][i];
-        for (int i = 0; i < 3; i++) np[i] = k->R[li][i] * d[0] + k->R[li][3 + i] * d[1] + k->R[li][6 + i] * d[2];
-        if (code == 4) {
-            double Rc[9], e[3] = {c->pb[0] - obj[0], c->pb[1] - obj[1], c->pb[2] - obj[2]};
-            quat_to_mat(obj + 3, Rc);
-            for (int i = 0; i < 3; i++) np[3 + i] = Rc[i] * e[0] + Rc[3 + i] * e[1] + Rc[6 + i] * e[2];
-        } else {
-            memcpy(np + 3, c->pb, 3 * sizeof(double));
-        }
-        memcpy(np + 6, c->n, 3 * sizeof(double));
-        np[9] = c->dist;
-        np[10] = 0.0;
-        man_add(M, np, thr2);
+    int k = 0;
+    for (int i = 0; i < cnt; i++) {
+        if (drop[i]) continue;
+        if (k != i) memcpy(pool_pt(P, k), pool_pt(P, i), MAN_PT * sizeof(double));
+        k++;
     }
-    /* 3. refreshContactPoints: move the points with their bodies, drop the broken ones */
-    for (int mi = 0; mi < PGXO_MAN; mi++) {
-        double* M = man + MAN_SZ * mi;
-        if (M[0] == 0.0) continue;
-        const int key = (int)M[0] - 1, code = key & 31;
-        int n = (int)M[1];
-        const int li = m->cap_link[key >> 5];
-        double pa[4][3], pb[4][3];
-        for (int i = 0; i < n; i++) man_world(k, obj, li, code, M + 2 + MAN_PT * i, pa[i], pb[i]);
-        man_refresh(M, pa, pb, thr);
-        if (M[1] == 0.0) M[0] = 0.0;   /* (a manifold without points: the slot is free again) */
+    P[0] = k;
+}
+/* world positions of pool point i's A (robot) and B points */
+static void man_world(const pgx_model* m, const kin_t* k, const double* obj, int has_object, const double* c,
+                      double* pa, double* pb) {
+    const int key = (int)c[MP_KID] & ~3, fl = cap_frame_link(m, key_capsule(key, has_object));
+    m3_v(k->R[fl], c + MP_LA, pa);
+    for (int i = 0; i < 3; i++) pa[i] += k->o[fl][i];
+    if (key < KEY_TABLE && has_object) {   /* the cube: B's local frame moves with it */
+        double Rc[9];
+        quat_to_mat(obj + 3, Rc);
+        m3_v(Rc, c + MP_LB, pb);
+        for (int i = 0; i < 3; i++) pb[i] += obj[i];
+    } else {                                /* table / plane / obstacle: static, local = world */
+        memcpy(pb, c + MP_LB, 3 * sizeof(double));
     }
 }
+/* test entry points: a pool whose bodies do not move (local = world) */
+int pgxo_manifold_add(double* P, int cap, int key, const double* point, double thr) {
+    return man_add(P, cap, key, point, thr * thr);
+}
+void pgxo_manifold_refresh_static(double* P, double thr) {
+    double pa[PGXO_POOL_MAX][3], pb[PGXO_POOL_MAX][3];
+    for (int i = 0; i < (int)P[0]; i++)
+        for (int j = 0; j < 3; j++) { pa[i][j] = pool_pt(P, i)[MP_LA + j]; pb[i][j] = pool_pt(P, i)[MP_LB + j]; }
+    pool_refresh(P, pa, pb, thr);
+}
+
+/* a pair's new point: the contact, its manifold key and its merge order */
+typedef struct { contact_t c; int key, order; } newpt_t;
+#define NEWPT_MAX (4 * PGX_MAX_CAPSULES + PGX_MAX_CAPSULES * PGX_AO_OBSTACLES)
 
 /* contact detection; returns the number of contacts (grouped, each group sorted by id) */
 static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W, const kin_t* k, double* obj,
                   contact_t* out) {
     const double tau = p->contact_distance;
-    static cands_t s0, s1;   /* single-threaded checker */
+    static PGXO_TLS cands_t s0, s1;   /* per thread (cpu_baseline runs shards in threads) */
     s0.n = 0; s1.n = 0;
+    /* Bullet's persistent manifolds for the cube / obstacle pairs (the default budget), and with the
+     * study flag for the table / plane pairs as well */
+    const int pers = W->contacts == PGX_CONTACTS_FULL && !(p->flags & PGX_FLAG_FRESH_MANIFOLD);
+    const int pers_table = pers && (p->flags & PGX_FLAG_PERSISTENT_MANIFOLD);
+    static PGXO_TLS newpt_t np[NEWPT_MAX];
+    int nnp = 0;
     double Rc[9];
     if (W->has_object) {
         quat_to_mat(obj + 3, Rc);
@@ -815,7 +838,7 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
             double zt = ground_z(W, P);
             double d = P[2] - zt;
             if (d < tau) {
-                contact_t c = {0, v, -1, {0, 0, 1}, {P[0], P[1], P[2]}, {P[0], P[1], zt}, d, NULL, 0.0};
+                contact_t c = {0, v, -1, {0, 0, 1}, {P[0], P[1], P[2]}, {P[0], P[1], zt}, d, NULL, 0.0, 0};
                 cand_add(&s0, &c, zt == W->plane_z ? PAIR_PLANE : PAIR_TABLE);
             }
         }
@@ -836,14 +859,24 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
                 double zt = ground_z(W, P);
                 double d = P[2] - r - zt;
                 if (d < tau) {
-                    contact_t c = {1, 2 * ci + e, li, {0, 0, 1}, {P[0], P[1], P[2] - r}, {P[0], P[1], zt}, d, NULL, 0.0};
-                    cand_add(&s1, &c, 16 * ci + (zt == W->plane_z ? PAIR_PLANE : PAIR_TABLE));
+                    contact_t c = {1, 2 * ci + e, li, {0, 0, 1}, {P[0], P[1], P[2] - r}, {P[0], P[1], zt}, d, NULL,
+                                   0.0, 0};
+                    const int code = zt == W->plane_z ? PAIR_PLANE : PAIR_TABLE;
+                    if (pers_table) {
+                        np[nnp].c = c;
+                        np[nnp].key = KEY_TABLE + 64 * ci + 8 * code + 4 * e;
+                        np[nnp].order = 2 * ci + e;
+                        nnp++;
+                    } else {
+                        cand_add(&s1, &c, 16 * ci + code);
+                    }
                 }
             }
         }
         if (W->has_object && (m->cap_flags[ci] & PGX_CAP_VS_OBJECT)) {
             const double h = W->half;
             int ns = capsule_samples(m->cap_a[ci], m->cap_b[ci], r);
+            int best = -1;
             for (int s = 0; s < ns; s++) {
                 double t = ns > 1 ? (double)s / (double)(ns - 1) : 0.0, C[3], rel[3], cl[3];
                 for (int i = 0; i < 3; i++) { C[i] = A[i] + t * (B[i] - A[i]); rel[i] = C[i] - obj[i]; }
@@ -857,23 +890,30 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
                     depth = dist - r;
                 } else { /* sphere centre inside the box: push out through the nearest face */
                     int ax = 0;
-                    double best = h - fabs(cl[0]);
+                    double bst = h - fabs(cl[0]);
                     for (int i = 1; i < 3; i++)
-                        if (h - fabs(cl[i]) < best) { best = h - fabs(cl[i]); ax = i; }
+                        if (h - fabs(cl[i]) < bst) { bst = h - fabs(cl[i]); ax = i; }
                     double sg = cl[ax] < 0 ? -1.0 : 1.0;
                     nl[0] = nl[1] = nl[2] = 0.0;
                     nl[ax] = sg;
                     qb[ax] = sg * h;
-                    depth = -best - r;
+                    depth = -bst - r;
                 }
                 if (depth < tau) {
                     contact_t c;
                     c.grp = 2; c.id = 32 + ci * 16 + s; c.link = li; c.dist = depth;
-                    c.mp = NULL; c.imp = 0.0;
+                    c.mp = NULL; c.imp = 0.0; c.sub = 0;
                     m3_v(Rc, nl, c.n);
                     m3_v(Rc, qb, c.pb);
                     for (int i = 0; i < 3; i++) { c.pb[i] += obj[i]; c.pa[i] = C[i] - r * c.n[i]; }
-                    cand_add(&s1, &c, 16 * ci + PAIR_CUBE);
+                    if (pers) {   /* the pair's one new point: its deepest sample (the first on a tie) */
+                        if (best < 0 || depth < np[best].c.dist) {
+                            if (best < 0) { best = nnp++; np[best].key = 32 + 16 * ci; np[best].order = 1000 + ci; }
+                            np[best].c = c;
+                        }
+                    } else {
+                        cand_add(&s1, &c, 16 * ci + PAIR_CUBE);
+                    }
                 }
             }
         }
@@ -890,39 +930,71 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
                 const cdist_t cd = ao_capsule_obstacle(A, B, r, o, W->obst);
                 if (cd.d < tau) {
                     contact_t c = {1, 32 + 6 * ci + o, li, {-cd.n[0], -cd.n[1], -cd.n[2]},
-                                   {cd.pa[0], cd.pa[1], cd.pa[2]}, {cd.pb[0], cd.pb[1], cd.pb[2]}, cd.d, NULL, 0.0};
-                    cand_add(&s1, &c, 16 * ci + PAIR_OBSTACLE + o);
+                                   {cd.pa[0], cd.pa[1], cd.pa[2]}, {cd.pb[0], cd.pb[1], cd.pb[2]}, cd.d, NULL, 0.0, 0};
+                    if (pers) {
+                        np[nnp].c = c;
+                        np[nnp].key = 32 + 24 * ci + 4 * o;
+                        np[nnp].order = 2000 + 16 * o + ci;
+                        nnp++;
+                    } else {
+                        cand_add(&s1, &c, 16 * ci + PAIR_OBSTACLE + o);
+                    }
                 }
             }
+        }
+    }
+    if (pers) {
+        double* P = obj + OBJ_MAN;
+        const int cap = pers_table ? PGXO_POOL_MAX : (W->has_object ? PGX_MANIFOLD_POOL : PGX_MANIFOLD_POOL_AO);
+        const double thr = tau;   /* the breaking threshold (gContactBreakingThreshold 0.02) */
+        /* 1. addContactPoint in merge order (insertion sort by order) */
+        for (int i = 1; i < nnp; i++)
+            for (int j = i; j > 0 && np[j].order < np[j - 1].order; j--) { newpt_t t = np[j]; np[j] = np[j - 1]; np[j - 1] = t; }
+        for (int j = 0; j < nnp; j++) {
+            const contact_t* c = &np[j].c;
+            const int fl = cap_frame_link(m, key_capsule(np[j].key, W->has_object));
+            double pt[MAN_PT], d[3];
+            for (int i = 0; i < 3; i++) d[i] = c->pa[i] - k->o[fl][i];
+            for (int i = 0; i < 3; i++)
+                pt[MP_LA + i] = k->R[fl][i] * d[0] + k->R[fl][3 + i] * d[1] + k->R[fl][6 + i] * d[2];
+            if (np[j].key < KEY_TABLE && W->has_object) {
+                double e[3] = {c->pb[0] - obj[0], c->pb[1] - obj[1], c->pb[2] - obj[2]};
+                for (int i = 0; i < 3; i++) pt[MP_LB + i] = Rc[i] * e[0] + Rc[3 + i] * e[1] + Rc[6 + i] * e[2];
+            } else {
+                memcpy(pt + MP_LB, c->pb, 3 * sizeof(double));
+            }
+            memcpy(pt + MP_N, c->n, 3 * sizeof(double));
+            pt[MP_D] = c->dist;
+            pt[MP_KID] = 0.0;
+            pt[MP_IMP] = 0.0;
+            man_add(P, cap, np[j].key, pt, thr * thr);
+        }
+        /* 2. refreshContactPoints: move the points with their bodies, drop the broken ones */
+        const int cnt = (int)P[0];
+        double pa[PGXO_POOL_MAX][3], pb[PGXO_POOL_MAX][3];
+        for (int i = 0; i < cnt; i++) man_world(m, k, obj, W->has_object, pool_pt(P, i), pa[i], pb[i]);
+        pool_refresh(P, pa, pb, thr);
+        /* 3. the manifold points are the group's candidates after the fresh table ones, in pool order,
+         * each its own pair (a manifold holds <= 4 already) */
+        for (int i = 0; i < (int)P[0]; i++) {
+            double* c = pool_pt(P, i);
+            const int kid = (int)c[MP_KID], key = kid & ~3, ci = key_capsule(key, W->has_object);
+            contact_t ct;
+            ct.grp = (key < KEY_TABLE && W->has_object) ? 2 : 1;
+            ct.id = key >= KEY_TABLE ? 2 * ci + ((key >> 2) & 1) : kid;
+            ct.sub = key >= KEY_TABLE ? (kid & 3) : 0;
+            ct.link = m->cap_link[ci];
+            man_world(m, k, obj, W->has_object, c, ct.pa, ct.pb);
+            memcpy(ct.n, c + MP_N, sizeof ct.n);
+            ct.dist = c[MP_D];
+            ct.mp = c;
+            ct.imp = c[MP_IMP];
+            cand_add(&s1, &ct, 100000 + i);
         }
     }
     int np1;
     const int n0 = select_points(&s0, PGX_OBJECT_POINTS, out, NULL);
     const int budget = robot_budget >= 0 ? robot_budget : W->robot_points;
-    if (p->flags & PGX_FLAG_PERSISTENT_MANIFOLD) {   /* the robot group from the persistent manifolds */
-        persistent_manifolds(m, p, k, obj, &s1);
-        cands_t* sm = &s1;   /* reuse: the manifold points as the group's candidates */
-        sm->n = 0;
-        double* man = obj + OBJ_MAN;
-        for (int mi = 0; mi < PGXO_MAN; mi++) {
-            double* M = man + MAN_SZ * mi;
-            if (M[0] == 0.0) continue;
-            const int key = (int)M[0] - 1, ci = key >> 5, code = key & 31, li = m->cap_link[ci];
-            for (int sl = 0; sl < (int)M[1]; sl++) {
-                double* P = M + 2 + MAN_PT * sl;
-                contact_t c;
-                c.grp = code == 4 ? 2 : 1;
-                c.id = 4 * key + sl;
-                c.link = li;
-                man_world(k, obj, li, code, P, c.pa, c.pb);
-                memcpy(c.n, P + 6, sizeof c.n);
-                c.dist = P[9];
-                c.mp = P;
-                c.imp = P[10];
-                cand_add(sm, &c, mi);   /* each manifold its own pair (<= 4 points already) */
-            }
-        }
-    }
     const int n1 = select_points(&s1, budget, out + n0, &np1);
     pgxo_pair_hist[np1 < PGXO_ROBOT_HIST - 1 ? np1 : PGXO_ROBOT_HIST - 1]++;
     sort_by_id(out, n0);
@@ -1185,7 +1257,7 @@ static void substep_impl(const pgx_model* m, const pgx_sim_params* p, const doub
         q[d] += dt * vn[d];
     }
     for (int c = 0; c < ncon; c++)   /* persistent manifold: the applied impulse back to its point */
-        if (con[c].mp) con[c].mp[10] = cr[3 * c].lam;
+        if (con[c].mp) con[c].mp[MP_IMP] = cr[3 * c].lam;
     if (W) { /* contact cache: this step's features and normal impulses, per group */
         double* cache = obj + OBJ_CACHE;
         for (int s = 0; s < N_CACHE; s++) { cache[2 * s] = -1.0; cache[2 * s + 1] = 0.0; }
@@ -1546,7 +1618,9 @@ static void reset_one(const pgx_config* c, int64_t e, const double* inject_goal,
     if (obj) {
         for (int s = 0; s < N_CACHE; s++) { obj[OBJ_CACHE + 2 * s] = -1.0; obj[OBJ_CACHE + 2 * s + 1] = 0.0; }
         memcpy(obj + OBJ_QC, q, 7 * sizeof(double));   /* resetJointState refreshes the link cache */
-        memset(obj + OBJ_MAN, 0, PGXO_MAN * MAN_SZ * sizeof(double));   /* (resetBasePosition... clears them) */
+        /* a reset teleports the bodies: Bullet's broadphase drops the pairs that stop overlapping, and
+         * the next refresh the points of any other (they separate far beyond the 0.02 threshold) */
+        memset(obj + OBJ_MAN, 0, (1 + PGXO_POOL_MAX * MAN_PT) * sizeof(double));
     }
     *elapsed = 0;
     *episode += 1;
@@ -1907,7 +1981,7 @@ static void ao_reset_one(const pgx_config* c, int64_t e, const double* inject_go
         }
     for (int s = 0; s < N_CACHE; s++) { obj[OBJ_CACHE + 2 * s] = -1.0; obj[OBJ_CACHE + 2 * s + 1] = 0.0; }
     memcpy(obj + OBJ_QC, q, 7 * sizeof(double));
-    memset(obj + OBJ_MAN, 0, PGXO_MAN * MAN_SZ * sizeof(double));
+    memset(obj + OBJ_MAN, 0, (1 + PGXO_POOL_MAX * MAN_PT) * sizeof(double));
     *elapsed = 0;
     *episode += 1;
 }

@@ -56,17 +56,20 @@ void pgxo_substep(const pgx_model* m, const pgx_sim_params* p, const double base
 void pgxo_world_substep(const pgx_config* cfg, double* q, double* qd, double* obj,
                         const pgxo_motor* motors, pgxo_stats* st);
 #define PGXO_ROBOT_MAX 16   /* robot contact slots of the oracle's cache (its largest budget) */
-#define PGXO_MAN 16          /* persistent manifolds per env (PGX_FLAG_PERSISTENT_MANIFOLD) */
-#define PGXO_OBJ_N (13 + 2 * (PGX_OBJECT_POINTS + PGXO_ROBOT_MAX) + 4 * PGX_AO_OBSTACLES + 7 + PGXO_MAN * (2 + 4 * 11))
+#define PGXO_POOL_MAX 48     /* manifold pool points per env: PGX_MANIFOLD_POOL(_AO) in the default
+                                mode, all of it with the study flag PGX_FLAG_PERSISTENT_MANIFOLD */
+#define PGXO_OBJ_N (13 + 2 * (PGX_OBJECT_POINTS + PGXO_ROBOT_MAX) + 4 * PGX_AO_OBSTACLES + 7 + \
+                    1 + PGXO_POOL_MAX * PGX_MANIFOLD_POINT)
 /* the robot group's row budget (default / -1: the configuration's, pgx_config.contacts) and
  * the histogram of robot points Bullet's per-pair rule keeps before the budget, per substep */
 #define PGXO_ROBOT_HIST 33
 void pgxo_set_robot_budget(int budget);
-/* one persistent manifold [2 + 4 x 11]: (key + 1, count, points (local A, local B, normal on B,
- * distance, impulse)); add a point (returns its slot) / refresh it with the bodies at rest
- * (PGX_FLAG_PERSISTENT_MANIFOLD's btPersistentManifold restatement; tests) */
-int pgxo_manifold_add(double* M, const double* point, double thr);
-void pgxo_manifold_refresh_static(double* M, double thr);
+/* a manifold pool [1 + cap x PGX_MANIFOLD_POINT] (pgx.h): add a point (kid, local A, local B, normal
+ * on B, distance, impulse; kid and impulse ignored) to manifold `key` -- returns its slot, -1 when
+ * the pool is full -- / refresh every manifold with the bodies at rest (the btPersistentManifold
+ * restatement; tests) */
+int pgxo_manifold_add(double* pool, int cap, int key, const double* point, double thr);
+void pgxo_manifold_refresh_static(double* pool, double thr);
 void pgxo_pair_hist_read(int64_t* out, int clear);
 /* the last contact detection's points (group 0 object-scene / 1 robot-table / 2 robot-object,
  * feature id, robot link or -1, separation); returns their number */

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("PGX_LIB") or os.path.join(os.path.dirname(os.path.abs
 
 EXPORTS = [
     "pgx_version", "pgx_last_error", "pgx_obs_dim", "pgx_action_dim", "pgx_dev_model_bytes", "pgx_create", "pgx_destroy",
-    "pgx_get_state", "pgx_reset", "pgx_step", "pgx_sample_actions", "pgx_compute_reward",
+    "pgx_get_state", "pgx_reset", "pgx_step", "pgx_step_kernel", "pgx_sample_actions", "pgx_compute_reward",
     "pgx_state_bytes", "pgx_save_state", "pgx_restore_state", "pgx_snapshot", "pgx_restore", "pgx_release",
     "pgx_set_rng_streams", "pgx_get_rng_streams",
     "pgx_replay_create", "pgx_replay_destroy", "pgx_replay_add", "pgx_replay_size", "pgx_replay_sample",
@@ -53,6 +53,8 @@ def load(path: str = None):
     lib.pgx_get_state.argtypes = [C.c_void_p, C.POINTER(PgxStateView)]
     lib.pgx_reset.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(PgxStepOut), C.c_void_p]
     lib.pgx_step.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(PgxStepOut), C.c_void_p]
+    lib.pgx_step_kernel.argtypes = [C.c_void_p]
+    lib.pgx_step_kernel.restype = C.c_char_p
     lib.pgx_sample_actions.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
     lib.pgx_compute_reward.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_double, C.c_void_p,
                                        C.c_void_p]

@@ -23,6 +23,9 @@ ROBOT_POINTS_ARM = 8          # PGX_ROBOT_POINTS_ARM: Reach / ReachAO (16 lanes)
 ROBOT_POINTS_ONE_LANE = 4     # PGX_ROBOT_POINTS_ONE_LANE: the one-lane layout
 CONTACT_SLOTS = OBJECT_POINTS + ROBOT_POINTS
 CONTACTS_FULL = 2             # PGX_CONTACTS_FULL: pgx_config.contacts for the full manifold budget
+MANIFOLD_POOL = 16            # PGX_MANIFOLD_POOL: persistent manifold points per env (Push / PickAndPlace)
+MANIFOLD_POOL_AO = 8          # PGX_MANIFOLD_POOL_AO: ReachAO
+MANIFOLD_POINT = 12           # PGX_MANIFOLD_POINT: kid, local A[3], local B[3], normal[3], distance, impulse
 CAP_VS_TABLE, CAP_VS_OBJECT = 1, 2
 
 TASK_REACH, TASK_PUSH, TASK_PICK_AND_PLACE, TASK_REACH_AO = 0, 1, 2, 3
@@ -36,7 +39,8 @@ FLAG_IK_COM = 2
 FLAG_NO_RESIDUAL_EXIT = 4
 FLAG_LINKSTATE_CURRENT = 8   # getLinkState at the pose after the last substep (rejected hypothesis)
 FLAG_DYN_RECURSIVE = 16      # oracle: M, b by CRBA + Newton-Euler (the kernel's formulation), for the op count
-FLAG_PERSISTENT_MANIFOLD = 32  # oracle: Bullet's persistent contact manifolds for the robot pairs (study mode)
+FLAG_PERSISTENT_MANIFOLD = 32  # oracle study: the table / plane pairs through persistent manifolds too
+FLAG_FRESH_MANIFOLD = 64       # oracle study: round 4's per-substep rule for the cube / obstacle pairs
 
 HER_FUTURE, HER_FINAL, HER_EPISODE = 0, 1, 2
 
@@ -111,6 +115,7 @@ class PgxStateView(C.Structure):
         ("q", C.c_void_p), ("qd", C.c_void_p), ("qc", C.c_void_p), ("goal", C.c_void_p), ("object", C.c_void_p),
         ("contacts", C.c_void_p), ("obstacles", C.c_void_p), ("elapsed", C.c_void_p), ("episode", C.c_void_p),
         ("errors", C.c_void_p), ("robot_points", C.c_int32),
+        ("env_order", C.c_void_p), ("manifolds", C.c_void_p), ("manifold_pool", C.c_int32),
     ]
 
 

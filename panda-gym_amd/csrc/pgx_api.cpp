@@ -74,8 +74,13 @@ struct pgx_env {
     size_t blob_bytes;
     /* device snapshots by id (pgx_snapshot): slot i holds state id i, nullptr = free */
     std::vector<void*> snaps;
-    /* [N][4] numpy PCG64 streams of the reset draws (pgx_set_rng_streams), nullptr: Philox */
+    /* [N][4] numpy PCG64 streams of the reset draws (pgx_set_rng_streams) and, after them, the
+     * device mode word (PgxDevEnv.pcg_on): allocated by pgx_create, freed by pgx_destroy, so a
+     * graph captured in either mode never reads freed memory */
     uint64_t* pcg = nullptr;
+    bool pcg_set = false;   /* host mirror of the mode word */
+    /* the step kernel the last pgx_step launched (pgx_step_kernel) */
+    const char* step_kernel = nullptr;
 };
 
 extern "C" {
@@ -353,6 +358,7 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
 #endif
     PgxDevEnv& e = h->de;
     e.pcg = nullptr;
+    e.pcg_on = nullptr;
     e.perm_buf = nullptr;
     e.perm = nullptr;
     e.sort_mode = 0;   /* PGX_SORT_ENVS: 1 always, 0 never (A/B and test hook); unset: auto */
@@ -456,7 +462,15 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     h->ds.errors = (uint32_t*)(b + off_err);
     if (e.full_manifold) e.perm_buf = (int32_t*)(b + off_perm);   /* heavy-first env order (not state) */
     h->dm_dev = (PgxDevModel*)b;
-    rc = hip_check(hipMemset(h->blob, 0, total), "hipMemset(state)");
+    /* the PCG64 reset streams and their mode word: not part of the saved state (restoreState leaves
+     * np_random alone), so outside the blob */
+    const size_t pcg_bytes = align(32 * N);
+    rc = hip_check(hipMalloc((void**)&h->pcg, pcg_bytes + 256), "hipMalloc(rng streams)");
+    if (rc) { h->pcg = nullptr; (void)hipFree(h->blob); delete h; return rc; }
+    e.pcg = h->pcg;
+    e.pcg_on = (const int32_t*)((char*)h->pcg + pcg_bytes);
+    rc = hip_check(hipMemset(h->pcg, 0, pcg_bytes + 256), "hipMemset(rng streams)");
+    if (!rc) rc = hip_check(hipMemset(h->blob, 0, total), "hipMemset(state)");
     if (!rc) rc = hip_check(hipMemcpy(h->dm_dev, &h->dm, sizeof(PgxDevModel), hipMemcpyHostToDevice), "model copy");
     if (!rc) {
         PgxDevOut none;
@@ -467,7 +481,7 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
         if (!rc) rc = hip_check(hipMemset(h->ds.episode, 0, N * 4), "hipMemset(episode)");
         if (!rc) rc = hip_check(hipDeviceSynchronize(), "create sync");
     }
-    if (rc) { (void)hipFree(h->blob); delete h; return rc; }
+    if (rc) { (void)hipFree(h->pcg); (void)hipFree(h->blob); delete h; return rc; }
     *out = h;
     return PGX_OK;
 }
@@ -497,6 +511,7 @@ int pgx_get_state(pgx_handle h, pgx_state_view* out) {
     out->robot_points = !h->de.contacts ? 0
                       : !h->de.full_manifold ? PGX_ROBOT_POINTS_ONE_LANE
                       : h->de.has_object ? PGX_ROBOT_POINTS : PGX_ROBOT_POINTS_ARM;
+    out->env_order = h->de.perm_buf;
     return PGX_OK;
 }
 
@@ -530,8 +545,12 @@ int pgx_reset(pgx_handle h, const uint8_t* env_mask, const double* inject_goal, 
 
 int pgx_step(pgx_handle h, const float* action, pgx_step_out* out, void* stream) {
     if (!h || !action) return fail(PGX_E_INVALID, "null argument");
-    return hip_check((hipError_t)pgx_launch_step(h->dm_dev, h->de, h->ds, action, to_dev_out(out), stream), "step launch");
+    return hip_check((hipError_t)pgx_launch_step(h->dm_dev, h->de, h->ds, action, to_dev_out(out), stream,
+                                                 &h->step_kernel),
+                     "step launch");
 }
+
+const char* pgx_step_kernel(pgx_handle h) { return h ? h->step_kernel : nullptr; }
 
 int pgx_sample_actions(pgx_handle h, float* action, uint64_t step, void* stream) {
     if (!h || !action) return fail(PGX_E_INVALID, "null argument");
@@ -611,38 +630,29 @@ int pgx_release(pgx_handle h, int32_t state_id) {
     return rc;
 }
 
-/* Reset draws from numpy PCG64 streams (gymnasium's env.np_random, core.py:302, continued by
- * every later reset() -- the SB3 VecEnv auto-reset included): a copy of the caller's [N][4]
- * records on `stream`; NULL returns to the Philox counter.  ReachAO's rejection sampler draws
- * integers and a shuffle besides uniforms (reach_ao.py:1101-1161): not restated, refused. */
+/* Reset draws from numpy PCG64 streams instead of the Philox counter: a copy of the caller's
+ * [N][4] records on `stream`, then the device mode word set on the same stream; NULL clears the
+ * word (back to Philox) and keeps the buffer, which lives as long as the handle -- a HIP graph
+ * captured in either mode keeps valid pointers and draws in the mode of replay time.  ReachAO's
+ * rejection sampler draws integers and a shuffle besides uniforms (reach_ao.py:1101-1161): not
+ * restated, refused. */
 int pgx_set_rng_streams(pgx_handle h, const uint64_t* states, void* stream) {
     if (!h) return fail(PGX_E_INVALID, "null handle");
     if (h->de.ao && states) return fail(PGX_E_UNSUPPORTED, "PCG64 reset streams: ReachAO's reset draws are not restated");
     int rc = hip_check(hipSetDevice(h->device), "hipSetDevice");
     if (rc) return rc;
-    const size_t bytes = 32 * (size_t)h->de.n_envs;
-    if (!states) {
-        if (h->pcg) {
-            /* queued resets may still read the streams */
-            rc = hip_check(hipDeviceSynchronize(), "rng streams sync");
-            if (!rc) rc = hip_check(hipFree(h->pcg), "hipFree(rng streams)");
-            h->pcg = nullptr;
-        }
-        h->de.pcg = nullptr;
-        return rc;
-    }
-    if (!h->pcg) {
-        rc = hip_check(hipMalloc((void**)&h->pcg, bytes), "hipMalloc(rng streams)");
-        if (rc) { h->pcg = nullptr; return rc; }
-    }
-    rc = hip_check(hipMemcpyAsync(h->pcg, states, bytes, hipMemcpyDefault, (hipStream_t)stream), "rng streams copy");
-    if (!rc) h->de.pcg = h->pcg;
+    int32_t* on = const_cast<int32_t*>(h->de.pcg_on);
+    if (states)
+        rc = hip_check(hipMemcpyAsync(h->pcg, states, 32 * (size_t)h->de.n_envs, hipMemcpyDefault, (hipStream_t)stream),
+                       "rng streams copy");
+    if (!rc) rc = hip_check(hipMemsetD32Async((hipDeviceptr_t)on, states ? 1 : 0, 1, (hipStream_t)stream), "rng mode word");
+    if (!rc) h->pcg_set = states != nullptr;
     return rc;
 }
 
 int pgx_get_rng_streams(pgx_handle h, uint64_t* states, void* stream) {
     if (!h || !states) return fail(PGX_E_INVALID, "null argument");
-    if (!h->pcg) return fail(PGX_E_INVALID, "no PCG64 reset streams set (pgx_set_rng_streams)");
+    if (!h->pcg_set) return fail(PGX_E_INVALID, "no PCG64 reset streams set (pgx_set_rng_streams)");
     return hip_check(hipMemcpyAsync(states, h->pcg, 32 * (size_t)h->de.n_envs, hipMemcpyDefault, (hipStream_t)stream),
                      "rng streams copy");
 }

@@ -71,7 +71,10 @@ struct PgxDevEnv {
     int32_t wave_mode;             /* A/B hook (PGX_WAVES_PER_SIMD): 0 auto (two resident waves per SIMD
                                       beyond 1024 waves), 1 the one-wave build, 2 the two-wave build */
     uint64_t* pcg;                 /* [N][4] numpy PCG64 streams of the reset draws (pgx_set_rng_streams),
-                                      nullptr: the Philox counter */
+                                      allocated with the handle and freed with it */
+    const int32_t* pcg_on;         /* device word: 1 = resets draw from pcg, 0 = the Philox counter.  In
+                                      device memory and switched on the caller's stream, so a step loop
+                                      captured in a HIP graph draws in the mode of replay time */
     /* heavy-first env order of the per-pair manifold kernels (pgx_launch_step): perm_buf device
      * buffer (permutation [N] i32, keys [N] u8 padded to 4 B, per-block bin counts [N/256 + 1][13]); sort_mode (PGX_SORT_ENVS) 0 auto (more waves than fit at once), 1 always, -1 never;
      * perm: the order a launch uses (nullptr: identity), set by the launcher */
@@ -110,10 +113,11 @@ struct PgxDevOut {
 
 /* launchers (pgx_kernels.hip); return hipError_t as int */
 /* the arm-only (Reach) step kernels: their own translation unit (pgx_kernels.hip, PGX_TU) */
+/* name (may be NULL): set to the launched step kernel's name, as rocprof spells it */
 int pgx_launch_step_arm(const PgxDevModel* m_device, const PgxDevEnv& e, const PgxDevState& s, const float* action,
-                        const PgxDevOut& o, void* stream);
+                        const PgxDevOut& o, void* stream, const char** name);
 int pgx_launch_step(const PgxDevModel* m_device, const PgxDevEnv& e, const PgxDevState& s, const float* action,
-                    const PgxDevOut& o, void* stream);
+                    const PgxDevOut& o, void* stream, const char** name);
 int pgx_launch_reset(const PgxDevModel* m_device, const PgxDevEnv& e, const PgxDevState& s, const uint8_t* mask,
                      const double* inject_goal, const double* inject_object, const PgxDevOut& o, void* stream);
 int pgx_launch_sample_actions(const PgxDevEnv& e, float* action, uint64_t step, void* stream);

@@ -114,6 +114,29 @@ __device__ __forceinline__ void prof_mark(int k) {
 #define PGX_PROF_SWEEPS_DECL ((void)0)
 #endif
 
+/* Debug builds only (make dbg, tools/gpu_nan_probe.py): PGX_NAN_TRAP prints the first non-finite
+ * value per lane at each phase of the one-lane step (IK targets, unconstrained dynamics, the
+ * solve, the integration, the observation) with the model constants read at that point;
+ * PGX_LDS_POISON fills the step's LDS with NaN at kernel start, so any read of LDS the kernel did
+ * not write first turns into a non-finite result in every build. */
+#ifdef PGX_NAN_TRAP
+__device__ int pgx_nan_prints;
+#define PGX_TRAP(tag, sub, arr, n, mm)                                                                          \
+    do {                                                                                                   \
+        bool bad_ = false;                                                                                 \
+        for (int t_ = 0; t_ < (n); t_++) bad_ = bad_ || !isfinite((arr)[t_]);                            \
+        if (bad_ && atomicAdd(&pgx_nan_prints, 1) < 96)                                                    \
+            printf("PGX_NAN tag %d sub %d block %d lane %d v %g %g %g %g %g %g %g | dt %g kp %g kd %g "     \
+                   "maxv %g res %g erp %g fr %g it %d\n",                                                 \
+                   (tag), (sub), (int)blockIdx.x, (int)threadIdx.x, (arr)[0], (n) > 1 ? (arr)[1] : 0.0f,   \
+                   (n) > 2 ? (arr)[2] : 0.0f, (n) > 3 ? (arr)[3] : 0.0f, (n) > 4 ? (arr)[4] : 0.0f,        \
+                   (n) > 5 ? (arr)[5] : 0.0f, (n) > 6 ? (arr)[6] : 0.0f, (mm).dt, (mm).kp, (mm).kd,         \
+                   (mm).max_vel, (mm).residual_abs, (mm).contact_erp, (mm).friction, (mm).num_iterations); \
+    } while (0)
+#else
+#define PGX_TRAP(tag, sub, arr, n, mm) ((void)0)
+#endif
+
 struct V3 {
     float x, y, z;
 };
@@ -1862,6 +1885,14 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
     const V3 vcu = D.vcu, wcu = D.wcu;
 #define MINV(a, b) ((a) >= (b) ? Mi[a][b] : Mi[b][a])
     PGX_PROF_MARK(2);
+#ifdef PGX_NAN_TRAP
+    {
+        float mid[NJ];
+        for (int j = 0; j < NJ; j++) mid[j] = Mi[j][j];
+        PGX_TRAP(1, 0, vu, NJ, m);
+        PGX_TRAP(2, 0, mid, NJ, m);
+    }
+#endif
     float dv[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; j++) dv[j] = 0.0f;
@@ -2141,6 +2172,8 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
      * costs a scalar load and its s_waitcnt on every sweep */
     float res_thr = m.residual_abs;
     asm("" : "+s"(res_thr));
+    PGX_TRAP(3, n1, dv, NJ, m);
+    PGX_TRAP(8, n1, rhs, NJ, m);
     PGX_PROF_MARK(3);
     PGX_PROF_COUNT(9, 1);
     PGX_PROF_SWEEPS_DECL;
@@ -2249,6 +2282,7 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
     }
 #undef MINV
     PGX_PROF_SWEEPS_DONE();
+    PGX_TRAP(4, n1, dv, NJ, m);
     PGX_PROF_MARK(4);
     PGX_PROF_COUNT(11, any_contact ? 1 : 0);
 #pragma unroll
@@ -2257,6 +2291,8 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
         qd[j] = vn;
         q[j] += m.dt * vn;
     }
+    PGX_TRAP(5, n1, q, NJ, m);
+    PGX_TRAP(6, n1, qd, NJ, m);
     if (CONT) { /* contact cache: this step's features and normal impulses */
         ContactLds& L = *Lp;
 #pragma unroll
@@ -3410,7 +3446,7 @@ __device__ __forceinline__ void reset_env(MRef m, const PgxDevEnv& e, int i, uin
     uint64_t env = e.env_id_offset + (uint64_t)i;
     /* the draw source: the env's numpy PCG64 stream (pgx_set_rng_streams) advanced in draw order,
      * or the Philox counter (env, episode, draw index) */
-    const bool pcg = e.pcg != nullptr;
+    const bool pcg = e.pcg_on != nullptr && *e.pcg_on != 0;
     Pcg64 g{0, 0, 0, 0};
     if (pcg) {
         const uint64_t* r = e.pcg + 4 * (size_t)i;
@@ -3839,6 +3875,13 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     if constexpr (CONT) {
         __shared__ LT lds_buf;   /* one-lane: ~126 KB, one wave per CU; wide: ~9 KB */
         L = &lds_buf;
+#ifdef PGX_LDS_POISON
+        {
+            float* w = reinterpret_cast<float*>(L);
+            for (size_t t = threadIdx.x; t < sizeof(LT) / 4; t += blockDim.x) w[t] = __builtin_nanf("");
+            __syncthreads();
+        }
+#endif
         /* every row slot starts finite: the sweeps run unused slots predicated off, and an
          * inactive slot later only holds an earlier substep's (finite) row */
 #pragma unroll
@@ -3889,6 +3932,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
         tgt.z = fmaxf(0.0f, tgt.z);
         const float torn[4] = {1.0f, 0.0f, 0.0f, 0.0f};
         ik<WIDE != 0>(mp, q, tgt, torn, tq);
+        if constexpr (!WIDE) PGX_TRAP(0, 0, tq, NJ, m);
     } else {
 #pragma unroll
         for (int j = 0; j < NJ; j++) {
@@ -3971,6 +4015,12 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     for (int c = 0; c < 3; c++) goal[c] = s.goal[c * N + ii];
     V3 pos, vel;
     ee_state_cached(*fresh(mp), qprev, q, qd, pos, vel);
+#ifdef PGX_NAN_TRAP
+    if constexpr (!WIDE) {
+        const float pv[6] = {pos.x, pos.y, pos.z, vel.x, vel.y, vel.z};
+        PGX_TRAP(7, 0, pv, 6, m);
+    }
+#endif
     const int od = e.obs_dim;
     const V3 ag = OBJ ? ob.p : pos;
     double d = distance_f32_f64(ag, goal);
@@ -4281,15 +4331,25 @@ __global__ __launch_bounds__(SORT_BLOCK) void env_sort_scatter_kernel(int N, con
 #ifndef PGX_TU
 #define PGX_TU 0
 #endif
-#define PGX_STEP(C, O, K, A, W) hipLaunchKernelGGL((step_kernel<C, O, K, A, W>), grid, block, 0, st, m, e, s, action, o)
-#define PGX_STEP2(C, O, K, A, W)                                                                            \
-    do {                                                                                                    \
-        if (two) hipLaunchKernelGGL((step_kernel_o2<C, O, K, A, W>), grid, block, 0, st, m, e, s, action, o); \
-        else hipLaunchKernelGGL((step_kernel<C, O, K, A, W>), grid, block, 0, st, m, e, s, action, o);        \
+/* every launch names its kernel (rocprof's spelling) in *name: the label bench.py reports */
+#define PGX_KNAME(K, C, O, T, A, W) #K "<" #C ", " #O ", " #T ", " #A ", " #W ">"
+#define PGX_STEP(C, O, K, A, W)                                                                   \
+    do {                                                                                          \
+        hipLaunchKernelGGL((step_kernel<C, O, K, A, W>), grid, block, 0, st, m, e, s, action, o); \
+        if (name) *name = PGX_KNAME(step_kernel, C, O, K, A, W);                                  \
+    } while (0)
+#define PGX_STEP2(C, O, K, A, W)                                                                      \
+    do {                                                                                              \
+        if (two) {                                                                                    \
+            hipLaunchKernelGGL((step_kernel_o2<C, O, K, A, W>), grid, block, 0, st, m, e, s, action, o); \
+            if (name) *name = PGX_KNAME(step_kernel_o2, C, O, K, A, W);                                \
+        } else {                                                                                      \
+            PGX_STEP(C, O, K, A, W);                                                                  \
+        }                                                                                             \
     } while (0)
 #if PGX_TU != 2
 int pgx_launch_step_arm(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState& s, const float* action,
-                        const PgxDevOut& o, void* stream) {
+                        const PgxDevOut& o, void* stream, const char** name) {
     hipStream_t st = (hipStream_t)stream;
     const int wide = e.lanes_per_env == GW;
     const int per_block = wide ? EPW : 64;
@@ -4316,8 +4376,8 @@ int pgx_launch_step_arm(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevSt
 #endif
 #if PGX_TU != 1
 int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState& s, const float* action,
-                    const PgxDevOut& o, void* stream) {
-    if (!e.ao && !e.has_object) return pgx_launch_step_arm(m, e, s, action, o, stream);
+                    const PgxDevOut& o, void* stream, const char** name) {
+    if (!e.ao && !e.has_object) return pgx_launch_step_arm(m, e, s, action, o, stream, name);
     hipStream_t st = (hipStream_t)stream;
     const int wide = e.lanes_per_env == GW;
     const int per_block = wide ? EPW : 64;
@@ -4397,3 +4457,4 @@ int pgx_launch_compute_reward(const float* ag, const float* dg, int64_t n, int32
 #endif  /* PGX_TU != 1 */
 #undef PGX_STEP
 #undef PGX_STEP2
+#undef PGX_KNAME

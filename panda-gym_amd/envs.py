@@ -181,10 +181,13 @@ class PandaVecEnv:
 
     ``reset_rng``: where the reset draws (goal, object) come from.  ``"philox"`` (default): a
     device counter stream; a seeded ``reset`` injects the reference's numpy draws for that reset
-    only.  ``"pcg64"``: every env keeps numpy's PCG64 stream on the device (env i seeded with
-    seed + i, as SB3 seeds a VecEnv) and every reset -- the auto-reset included -- continues it,
-    as the reference's env.np_random does: the goal sequence of a whole seeded run is the
-    reference's, bit for bit.  Not for ReachAO (its rejection sampler is not restated)."""
+    only.  ``"pcg64"``: every env keeps a numpy PCG64 stream on the device, and a seeded reset
+    (env i with seed + i, as SB3 seeds a VecEnv) reseeds it and draws the reference's goal / object
+    on the device, bit for bit -- RobotTaskEnv.reset reseeds ``task.np_random`` on every reset
+    (core.py:302).  A reset without a seed, the auto-reset included, gets fresh OS entropy in the
+    reference, so there is no reference value to match: here it continues the env's stream (a
+    reproducible stand-in with the reference's distribution).  Not for ReachAO (its rejection
+    sampler is not restated on the device)."""
 
     def __init__(self, env_id: str = "PandaReach-v3", num_envs: int = 4096, device: Any = "cuda:0", seed: int = 0,
                  env_id_offset: int = 0, max_episode_steps: Optional[int] = None, auto_reset: bool = True,
@@ -200,6 +203,11 @@ class PandaVecEnv:
         self.lib = load(lib_path)
         self.env_id = env_id
         base_spec = spec(env_id)
+        if reset_rng not in ("philox", "pcg64"):
+            raise ValueError(f"reset_rng must be 'philox' or 'pcg64', got {reset_rng!r}")
+        if reset_rng == "pcg64" and base_spec.task == abi.TASK_REACH_AO:   # refused before pgx_create
+            raise PgxError("reset_rng='pcg64' is not available for ReachAO (its rejection sampler is not restated "
+                           "on the device; seeded resets are injected from the host)")
         if max_episode_steps is not None:
             base_spec = replace(base_spec, max_episode_steps=max_episode_steps)
         self.spec = base_spec
@@ -267,11 +275,13 @@ class PandaVecEnv:
         self._pending: Optional[torch.Tensor] = None
         self._pending_seed: Optional[int] = None
         self._step_index = 0
-        if reset_rng not in ("philox", "pcg64"):
-            raise ValueError(f"reset_rng must be 'philox' or 'pcg64', got {reset_rng!r}")
         self.reset_rng = reset_rng
         if reset_rng == "pcg64":
-            self._set_rng_streams(pcg64_records([seed + i for i in range(n)]))
+            try:
+                self._set_rng_streams(pcg64_records([seed + i for i in range(n)]))
+            except Exception:
+                self.close()
+                raise
 
     # ---------------------------------------------------------------- core
     def _check(self, rc: int, what: str) -> None:
@@ -312,6 +322,8 @@ class PandaVecEnv:
             "elapsed": _view(v.elapsed, (n,), torch.int32, self.device),
             "episode": _view(v.episode, (n,), torch.int32, self.device),
             "errors": _view(v.errors, (1,), torch.int32, self.device),
+            # not state: the env order of the last sorted step launch (heavy-first)
+            **({"env_order": _view(v.env_order, (n,), torch.int32, self.device)} if v.env_order else {}),
         }
 
     def robot_contact_budget(self) -> int:
@@ -354,11 +366,19 @@ class PandaVecEnv:
         return out.cpu().numpy().view(np.uint64)
 
     def reset_tensors(self, seed: Optional[int] = None, mask: Optional[torch.Tensor] = None,
-                      goals: Optional[np.ndarray] = None,
-                      objects: Optional[np.ndarray] = None) -> Dict[str, torch.Tensor]:
+                      goals: Optional[np.ndarray] = None, objects: Optional[np.ndarray] = None,
+                      episode_phase: Optional[str] = None) -> Dict[str, torch.Tensor]:
         """Reset (masked) envs on device; ``seed`` reproduces the reference's PCG64 goal (and
         object) draws for env i with seed+i (SB3 VecEnv seeding): injected into the kernel, or
-        with ``reset_rng="pcg64"`` the envs' device streams are reseeded and drawn from."""
+        with ``reset_rng="pcg64"`` the envs' device streams are reseeded and drawn from.
+
+        ``episode_phase="staggered"`` (benchmarks only): global env g starts its TimeLimit counter
+        at g mod max_episode_steps instead of 0, so its first episode is shorter and from then on
+        every step auto-resets about N / max_episode_steps envs -- the steady state of a long
+        VecEnv rollout (auto-reset and TimeLimit: core.py:352-368, __init__.py:30-35) in any window
+        of steps, instead of all envs resetting on the same step."""
+        if episode_phase not in (None, "staggered"):
+            raise ValueError(f"episode_phase must be None or 'staggered', got {episode_phase!r}")
         inj, inj_obj = None, None
         if goals is None and objects is None and seed is not None and self.reset_rng == "pcg64":
             rec = pcg64_records([seed + i for i in range(self.num_envs)])
@@ -385,7 +405,18 @@ class PandaVecEnv:
                                  None if inj_obj is None else C.c_void_p(inj_obj.data_ptr()), C.byref(self._out),
                                  self._stream()), "pgx_reset")
         self._keep = (m, inj, inj_obj)  # keep the buffers alive until the stream consumes them
+        if episode_phase == "staggered":   # stream-ordered after the reset (torch's current stream)
+            T = int(self.spec.max_episode_steps)
+            g = torch.arange(self.num_envs, device=self.device, dtype=torch.int64) + int(self._cfg.env_id_offset)
+            el = self.state()["elapsed"]
+            phase = (g % T).to(torch.int32)
+            el.copy_(phase if m is None else torch.where(m.bool(), phase, el))
         return self._obs_dict()
+
+    def step_kernel(self) -> Optional[str]:
+        """Name of the step kernel the last step launched (pgx_step_kernel; rocprof's spelling)."""
+        name = self.lib.pgx_step_kernel(self._h)
+        return None if name is None else name.decode()
 
     def step_tensors(self, actions: torch.Tensor):
         """Device-resident step: actions [N,A] f32 on device -> (obs dict, reward, terminated, truncated, success).
@@ -722,8 +753,10 @@ class PandaEnv:
 
     def __init__(self, env_id: str = "PandaReach-v3", device: Any = "cuda:0", max_episode_steps: Optional[int] = None,
                  seed: int = 0, reset_rng: str = "philox"):
-        """``reset_rng="pcg64"``: reset(seed) seeds the env's device PCG64 stream and every later
-        reset() continues it, as gymnasium's np_random does (PandaVecEnv)."""
+        """``reset_rng="pcg64"``: reset(seed) reseeds the env's device PCG64 stream and draws the
+        reference's goal / object for that seed (core.py:302); a later reset() without a seed
+        continues the stream -- a reproducible stand-in for the fresh OS entropy the reference
+        draws there, not a reference value (PandaVecEnv)."""
         self._vec = PandaVecEnv(env_id, num_envs=1, device=device, seed=seed, auto_reset=False,
                                 max_episode_steps=max_episode_steps, reset_rng=reset_rng)
         self.spec = self._vec.spec

@@ -536,3 +536,33 @@ def test_default_handles_keep_the_per_pair_manifold_budget(pg, env_id, points):
         v = pg.PandaVecEnv(env_id, num_envs=64, device="cuda:0", contacts=False)
         assert v.robot_contact_budget() == 0
         v.close()
+
+
+@pytest.mark.parametrize("env_id,n", [("PandaPush-v3", 8), ("PandaPickAndPlace-v3", 8)])
+def test_free_fall_known_answer_on_the_device(pg, oracle, env_id, n, lanes):
+    """test/pybullet_test.py:56-64 on the device: a cube released at rest, clear of every body,
+    has linear velocity [0, 0, -0.392] (atol 1e-3, the reference's) one env step later -- the
+    floating-base path (gravity, base damping, semi-implicit update) -- and equals the fp64
+    oracle's step to fp32 rounding.  (The reference's box has half extent 0.5; free fall does not
+    depend on the size or mass.)"""
+    venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=3, lanes_per_env=lanes)
+    venv.reset_tensors()
+    st = venv.state()
+    xs = torch.linspace(-0.2, 0.1, n, device="cuda:0")
+    st["object"][0].copy_(xs)
+    st["object"][1].zero_()
+    st["object"][2].fill_(1.0)                    # 1 m above the table, 0.5 m above the arm's reach
+    st["object"][3:6].zero_()
+    st["object"][6].fill_(1.0)
+    st["object"][7:13].zero_()
+    torch.cuda.synchronize()
+    ref = oracle.OracleVecEnv(venv._cfg, n)
+    _state_to_oracle(venv, ref)
+    venv.step_tensors(torch.zeros((n, venv.action_dim), device="cuda:0"))
+    out = ref.step(np.zeros((n, venv.action_dim), np.float32))
+    k = 6 + (0 if venv.spec.block_gripper else 1) + 6   # obs: ee pos, ee vel, [width], pos, euler, linvel
+    lin = venv.obs.cpu().numpy()[:, k:k + 3]
+    assert np.allclose(lin, [0.0, 0.0, -0.392], atol=1e-3), lin
+    assert np.abs(lin - out["obs"][:, k:k + 3]).max() <= 1e-5
+    assert np.all(venv.obs.cpu().numpy()[:, k + 3:k + 6] == 0.0)
+    venv.close()

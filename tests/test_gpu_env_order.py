@@ -27,6 +27,7 @@ v = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=5)
 v.reset_tensors(seed=5)
 h = hashlib.sha256()
 heavy = 0
+moved = 0
 for t in range(steps):
     v.step_tensors(v.sample_actions(t))
     st = v.state()
@@ -37,7 +38,11 @@ for t in range(steps):
     c = st["contacts"].cpu().numpy()
     keys = (c[8:8 + 2 * 12:2] >= 0).sum(0)
     heavy = max(heavy, int(keys.max()))
-print(h.hexdigest(), heavy)
+    if os.environ.get("PGX_SORT_ENVS") == "1":   # the order the launch used: a permutation, not always the identity
+        perm = st["env_order"].cpu().numpy()
+        assert np.array_equal(np.sort(perm), np.arange(n)), perm
+        moved += int((perm != np.arange(n)).any())
+print(h.hexdigest(), heavy, moved)
 '''
 
 
@@ -46,13 +51,14 @@ def _run(env_id, n, steps, mode):
     out = subprocess.run([sys.executable, "-c", CHILD, env_id, str(n), str(steps)], capture_output=True, text=True,
                          cwd=ROOT, env=env, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
-    digest, heavy = out.stdout.split()[-2:]
-    return digest, int(heavy)
+    digest, heavy, moved = out.stdout.split()[-3:]
+    return digest, int(heavy), int(moved)
 
 
 @pytest.mark.parametrize("env_id,n", [("PandaPush-v3", 67), ("PandaPickAndPlace-v3", 256), ("PandaReachAO-v3", 130)])
 def test_heavy_first_order_leaves_every_env_bit_identical(env_id, n):
-    d_on, heavy = _run(env_id, n, 40, "1")
-    d_off, _ = _run(env_id, n, 40, "0")
-    assert heavy >= 1   # some env held robot points: the order was not the identity
+    d_on, heavy, moved = _run(env_id, n, 40, "1")
+    d_off, _, _ = _run(env_id, n, 40, "0")
+    assert heavy >= 1   # some env held robot points
+    assert moved >= 1   # and some launch read its envs in an order other than the identity
     assert d_on == d_off

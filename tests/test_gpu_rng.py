@@ -1,8 +1,12 @@
 """GPU: the device reset in its numpy-PCG64 mode (``reset_rng="pcg64"``, pgx_set_rng_streams)
-against numpy itself -- gymnasium's env.np_random (core.py:302), continued by every reset of an
-SB3 VecEnv (the auto-reset included) and drawn in the task's order (reach.py:75-78,
-push.py:75-87, pick_and_place.py:71-85).  Bit-exact: the fp64 goal in the device state, the
-object position (f32 of the fp64 draw) and the stream records after every reset."""
+against numpy itself.  What is the reference's: a reset with seed s draws from
+gymnasium's seeding.np_random(s) = Generator(PCG64(SeedSequence(s))), because RobotTaskEnv.reset
+reseeds task.np_random on every reset (core.py:302), in the task's order (reach.py:75-78,
+push.py:75-87, pick_and_place.py:71-85) -- bit-exact here: the fp64 goal in the device state, the
+object position (f32 of the fp64 draw) and the stream record.  What is not: a reset without a seed
+(the auto-reset included) gets fresh OS entropy in the reference, so it has no reference value; the
+device continues the env's stream instead, and the tests below pin that continuation against
+numpy as this build's own reproducible contract, not as reference parity."""
 import numpy as np
 import pytest
 
@@ -42,9 +46,11 @@ def _check_envs(pg, venv, gens, expect):
 @pytest.mark.parametrize("env_id,lanes,contacts", [
     ("PandaReach-v3", 16, True), ("PandaReach-v3", 1, True), ("PandaReach-v3", 0, False),
     ("PandaPush-v3", 16, True), ("PandaPickAndPlace-v3", 16, True), ("PandaPickAndPlace-v3", 1, True)])
-def test_seeded_run_draws_the_reference_stream_across_auto_resets(pg, env_id, lanes, contacts):
-    """reset(seed) then three 2-step episodes: after each auto-reset every env's goal (and object)
-    is the next task draw of its own numpy Generator(PCG64(SeedSequence(seed + i)))."""
+def test_seeded_reset_is_the_reference_draw_then_auto_resets_continue_the_stream(pg, env_id, lanes, contacts):
+    """reset(seed): every env's goal (and object) is the reference's draw for seed + i, bit for bit.
+    Then three 2-step episodes: each auto-reset (OS entropy in the reference, no reference value)
+    takes the next task draw of the env's own Generator(PCG64(SeedSequence(seed + i))) -- the
+    device stream's continuation contract."""
     n, seed = 67, 4242
     venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=seed, max_episode_steps=2,
                           lanes_per_env=lanes, contacts=contacts, reset_rng="pcg64")
@@ -62,7 +68,8 @@ def test_seeded_run_draws_the_reference_stream_across_auto_resets(pg, env_id, la
 
 
 def test_sb3_reset_seed_then_auto_reset(pg):
-    """SB3 protocol: seed(s) + reset() reseeds env i with s + i; step_wait's auto-reset continues."""
+    """SB3 protocol: seed(s) + reset() reseeds env i with s + i (the reference's draw); step_wait's
+    auto-reset continues the stream (the build's contract: the reference draws OS entropy there)."""
     n, seed = 5, 77
     venv = pg.PandaVecEnv("PandaPush-v3", num_envs=n, device="cuda:0", seed=0, max_episode_steps=1,
                           reset_rng="pcg64")
@@ -108,9 +115,10 @@ def test_injected_and_masked_resets_keep_the_other_streams(pg):
     venv.close()
 
 
-def test_single_env_reset_continues_np_random(pg):
-    """RobotTaskEnv.reset(seed) then reset(), reset(): the goals are three consecutive draws of one
-    Generator(PCG64(SeedSequence(seed))) -- what gymnasium's np_random gives the reference."""
+def test_single_env_seeded_reset_then_unseeded_resets_continue_the_stream(pg):
+    """RobotTaskEnv.reset(seed): the reference's draw.  Then reset(), reset(): the next two draws of
+    the same Generator(PCG64(SeedSequence(seed))) -- the device stream's continuation (the
+    reference reseeds from OS entropy there, core.py:302, so it has no value to compare)."""
     env = pg.make("PandaPickAndPlace-v3", reset_rng="pcg64")
     gen = _gens(12345, 1)[0]
     for k in range(3):
@@ -139,3 +147,27 @@ def test_back_to_philox_and_reach_ao_refused(pg):
     ref.close()
     with pytest.raises(pg.PgxError, match="ReachAO"):
         pg.PandaVecEnv("PandaReachAO-v3", num_envs=4, device="cuda:0", reset_rng="pcg64")
+
+
+def test_captured_graph_draws_in_the_mode_of_replay_time(pg):
+    """The RNG mode is a device word switched on the stream and the stream buffer lives with the
+    handle: a step loop captured in Philox mode, replayed after pgx_set_rng_streams, auto-resets
+    from the PCG64 streams (and never reads freed memory after a switch back)."""
+    n, seed = 16, 99
+    venv = pg.PandaVecEnv("PandaReach-v3", num_envs=n, device="cuda:0", seed=seed, max_episode_steps=1)
+    acts = torch.zeros((1, n, venv.action_dim), device="cuda:0")
+    g = venv.capture_steps(1, acts)          # every step auto-resets (TimeLimit 1)
+    rec = pg.pcg64_records([500 + i for i in range(n)])
+    venv._set_rng_streams(rec)
+    g.replay()
+    torch.cuda.synchronize()
+    gens = _gens(500, n)
+    expect = np.stack([pg.task_draws(venv.spec, gg)[0] for gg in gens])
+    assert np.array_equal(venv.state()["goal"].cpu().numpy().T, expect)
+    assert venv.lib.pgx_set_rng_streams(venv._h, None, venv._stream()) == 0
+    g.replay()                               # back to Philox: the buffer is still the handle's
+    torch.cuda.synchronize()
+    assert not np.array_equal(venv.state()["goal"].cpu().numpy().T,
+                              np.stack([pg.task_draws(venv.spec, gg)[0] for gg in gens]))
+    del g
+    venv.close()

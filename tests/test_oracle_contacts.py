@@ -199,12 +199,16 @@ def test_two_links_on_table_keep_all_points(oracle):
 
 
 def test_link_on_cube_keeps_all_points_per_pair_cap(oracle):
+    """The fresh per-pair rule (round 4's, now the study flag PGX_FLAG_FRESH_MANIFOLD): every capsule
+    on the cube brings its 4 deepest samples at once; Bullet's persistent manifold (the default)
+    starts each pair from its one new point."""
     cfg = _cfg(task=abi.TASK_PUSH)
     cfg.contacts = abi.CONTACTS_FULL
     env = oracle.OracleVecEnv(cfg, 1)
     env.reset()   # cfg seed 0
     ee = env.step(np.zeros((1, 3)))["obs"][0, :3]   # the cube at the closed fingertips, in the air
     q = env.q[0].copy()
+    cfg.params.contents.flags = abi.FLAG_FRESH_MANIFOLD
     pts, n_pair = _detect(oracle, cfg, q, _obj(tuple(ee)))
     ids, links, d = _robot(pts)
     assert np.all(ids >= 32)                                    # capsule spheres vs the cube
@@ -212,63 +216,94 @@ def test_link_on_cube_keeps_all_points_per_pair_cap(oracle):
     per_pair = np.bincount(caps)
     assert per_pair.max() == 4 and (per_pair > 0).sum() >= 2    # >= 2 capsules, each capped at 4
     assert n_pair == len(ids) > 4                               # the budget (12) cuts nothing
+    cfg.params.contents.flags = 0                               # Bullet's manifolds, from empty ones
+    ptsp, _ = _detect(oracle, cfg, q, _obj(tuple(ee)))
+    idsp = _robot(ptsp)[0]
+    assert len(idsp) == (per_pair > 0).sum() and np.all((idsp - 32) % 16 == 0)   # one per pair, slot 0
     cfg.contacts = 1
     pts4, _ = _detect(oracle, cfg, q, _obj(tuple(ee)))
     assert len(_robot(pts4)[0]) == 4
 
 
-# ---------------------------------------------------------------- persistent manifold (study mode)
-# PGX_FLAG_PERSISTENT_MANIFOLD restates Bullet's btPersistentManifold for the robot pairs (oracle
-# only; DESIGN.md section 2 records how far it moves Push / PickAndPlace from the default rule).
+# ---------------------------------------------------------------- persistent manifold
+# Bullet's btPersistentManifold for the robot's cube / obstacle pairs (the default with
+# PGX_CONTACTS_FULL): a pool of points per env, pgx.h PGX_MANIFOLD_POOL.
 def _pt(a, dist, normal=(0.0, 0.0, 1.0), imp=0.0):
     a, n = np.asarray(a, float), np.asarray(normal, float)
-    return np.concatenate([a, a - n * dist, n, [dist, imp]])
+    return np.concatenate([[0.0], a, a - n * dist, n, [dist, imp]])
 
 
-def _man(oracle):
-    M = np.zeros(2 + 4 * oracle.MAN_PT)
-    M[0] = 1.0
-    return M
+def _pool(oracle, cap=16):
+    return np.zeros(1 + cap * oracle.MAN_PT)
+
+
+def _P(oracle, P, i):
+    return P[1 + i * oracle.MAN_PT:1 + (i + 1) * oracle.MAN_PT]
 
 
 def test_manifold_merges_appends_and_replaces_by_area(oracle):
-    M = _man(oracle)
-    assert oracle.manifold_add(M, _pt((0, 0, 0), -0.003)) == 0 and M[1] == 1
-    M[2 + 10] = 5.0                                            # the solver wrote an impulse back
+    P = _pool(oracle)
+    key = 32
+    assert oracle.manifold_add(P, key, _pt((0, 0, 0), -0.003)) == 0 and P[0] == 1
+    _P(oracle, P, 0)[oracle.MP_IMP] = 5.0                       # the solver wrote an impulse back
     # within the breaking threshold (0.02) of the cached point in A's frame: replaces it, impulse kept
-    assert oracle.manifold_add(M, _pt((0.01, 0, 0), -0.002)) == 0 and M[1] == 1
-    assert M[2 + 10] == 5.0 and M[2] == 0.01
+    assert oracle.manifold_add(P, key, _pt((0.01, 0, 0), -0.002)) == 0 and P[0] == 1
+    assert _P(oracle, P, 0)[oracle.MP_IMP] == 5.0 and _P(oracle, P, 0)[1] == 0.01
     for a in ((0.05, 0, 0), (0, 0.05, 0), (0.05, 0.05, 0)):   # farther apart: appended
-        oracle.manifold_add(M, _pt(a, -0.001))
-    assert M[1] == 4
-    P = M[2:].reshape(4, -1)
+        oracle.manifold_add(P, key, _pt(a, -0.001))
+    assert P[0] == 4
+    assert [int(_P(oracle, P, i)[0]) for i in range(4)] == [32, 33, 34, 35]   # kid = key + slot
+    pts = np.stack([_P(oracle, P, i).copy() for i in range(4)])
     # a fifth point: sortCachedPoints -- never the deepest (slot 0), else the largest remaining area
     new = _pt((0.1, 0.1, 0), -0.0005)
     res = []
     for i, (ia, ib, ic) in enumerate(((1, 3, 2), (0, 3, 2), (0, 3, 1), (0, 2, 1))):
-        x = np.cross(new[:3] - P[ia, :3], P[ib, :3] - P[ic, :3])
+        x = np.cross(new[1:4] - pts[ia, 1:4], pts[ib, 1:4] - pts[ic, 1:4])
         res.append(0.0 if i == 0 else float(x @ x))
     want = int(np.argmax(res))
-    assert want != 0 and oracle.manifold_add(M, new) == want and M[1] == 4
-    assert np.array_equal(M[2:].reshape(4, -1)[want], new)
+    assert want != 0 and oracle.manifold_add(P, key, new) == want and P[0] == 4
+    got = _P(oracle, P, want)
+    assert got[0] == 32 + want and np.array_equal(got[1:11], new[1:11]) and got[oracle.MP_IMP] == 0.0
+    # another pair's manifold shares the pool; a full pool drops a point that needs a new entry
+    Q = _pool(oracle, cap=2)
+    assert oracle.manifold_add(Q, 48, _pt((0, 0, 0), -0.001), cap=2) == 0
+    assert oracle.manifold_add(Q, 64, _pt((0, 0, 0), -0.001), cap=2) == 0
+    assert oracle.manifold_add(Q, 48, _pt((0.05, 0, 0), -0.001), cap=2) == -1 and Q[0] == 2
 
 
 def test_manifold_refresh_breaks_points(oracle):
-    M = _man(oracle)
+    P = _pool(oracle)
     for a in ((0, 0, 0), (0.05, 0, 0), (0, 0.05, 0)):
-        oracle.manifold_add(M, _pt(a, -0.001))
-    P = M[2:].reshape(4, -1)
-    P[1, 3:6] = P[1, 0:3] - np.array([0, 0, 0.03])              # B point 0.03 below A: separated past 0.02
-    P[2, 3:6] = P[2, 0:3] + np.array([0.03, 0, 0.001])          # slid 0.03 sideways
-    oracle.manifold_refresh_static(M)
-    assert M[1] == 1 and np.allclose(M[2:5], 0.0) and abs(M[2 + 9] - (-0.001)) < 1e-15
+        oracle.manifold_add(P, 32, _pt(a, -0.001))
+    _P(oracle, P, 1)[4:7] = _P(oracle, P, 1)[1:4] - np.array([0, 0, 0.03])    # B 0.03 below A: separated past 0.02
+    _P(oracle, P, 2)[4:7] = _P(oracle, P, 2)[1:4] + np.array([0.03, 0, 0.001])  # slid 0.03 sideways
+    oracle.manifold_refresh_static(P)
+    assert P[0] == 1 and np.allclose(_P(oracle, P, 0)[1:4], 0.0)
+    assert abs(_P(oracle, P, 0)[oracle.MP_D] - (-0.001)) < 1e-15
+
+
+def test_manifold_removal_renumbers_slots_as_bullet(oracle):
+    """removeContactPoint in reverse slot order, the last slot's point filling the hole: dropping
+    slots 1 and 3 of four leaves the old slot 0 at 0 and the old slot 2 at 1; the pool keeps the
+    survivors' order and another manifold's points are untouched."""
+    P = _pool(oracle)
+    for a in ((0, 0, 0), (0.05, 0, 0), (0, 0.05, 0), (0.05, 0.05, 0)):
+        oracle.manifold_add(P, 32, _pt(a, -0.001))
+    oracle.manifold_add(P, 48, _pt((0.3, 0, 0), -0.001))
+    for i in (1, 3):
+        _P(oracle, P, i)[4:7] = _P(oracle, P, i)[1:4] - np.array([0, 0, 0.05])
+    oracle.manifold_refresh_static(P)
+    assert P[0] == 3
+    kids = [int(_P(oracle, P, i)[0]) for i in range(3)]
+    las = [tuple(_P(oracle, P, i)[1:4]) for i in range(3)]
+    assert kids == [32, 33, 48] and las == [(0, 0, 0), (0, 0.05, 0), (0.3, 0, 0)]
 
 
 def test_persistent_manifold_builds_over_substeps(oracle):
     """The cube at the closed fingertips (test_link_on_cube_keeps_all_points_per_pair_cap): the
-    default rule gives each colliding capsule its 4 deepest samples at once; Bullet's manifold
-    starts from the pair's one closest point and gains at most one point per pair per substep,
-    never more than 4."""
+    fresh rule (PGX_FLAG_FRESH_MANIFOLD) gives each colliding capsule its 4 deepest samples at once;
+    Bullet's manifold (the default) starts from the pair's one closest point and gains at most one
+    point per pair per substep, never more than 4."""
     from oracle import oracle as orc
 
     cfg = _cfg(task=abi.TASK_PUSH)
@@ -277,17 +312,57 @@ def test_persistent_manifold_builds_over_substeps(oracle):
     env.reset()
     ee = env.step(np.zeros((1, 3)))["obs"][0, :3]
     q0 = env.q[0].copy()
-    cfgp = _cfg(task=abi.TASK_PUSH)
-    cfgp.contacts = abi.CONTACTS_FULL
-    cfgp.params.contents.flags = abi.FLAG_PERSISTENT_MANIFOLD
     q, qd, obj, mot = q0.copy(), np.zeros(7), _obj(tuple(ee)), _motors(oracle, q0)
     counts = []
     for t in range(12):
-        q, qd, obj, _ = oracle.world_substep(cfgp, q, qd, obj, mot)
-        cube = {key: len(pts) for key, pts in orc.manifolds(obj) if key & 31 == 4}
+        q, qd, obj, _ = oracle.world_substep(cfg, q, qd, obj, mot)
+        cube = {key: len(pts) for key, pts in orc.manifolds(obj)}
+        assert all(32 <= key < 32 + 16 * 16 and (key - 32) % 16 == 0 for key in cube)
         counts.append(cube)
     assert counts[0] and all(v == 1 for v in counts[0].values())      # one closest point per pair first
     for a, b in zip(counts, counts[1:]):
         for key, v in b.items():
             assert v <= a.get(key, 0) + 1 and v <= 4
     assert max(max(c.values(), default=0) for c in counts) >= 2       # and it builds up
+    # the fresh rule from the same start holds up to 4 per pair at once
+    cff = _cfg(task=abi.TASK_PUSH)
+    cff.contacts = abi.CONTACTS_FULL
+    cff.params.contents.flags = abi.FLAG_FRESH_MANIFOLD
+    q1, qd1, obj1, _ = oracle.world_substep(cff, q0.copy(), np.zeros(7), _obj(tuple(ee)), mot)
+    assert int(obj1[orc.OBJ_MAN]) == 0                                   # (no pool in that mode)
+    g, ids, _, _ = orc.last_contacts()
+    per_cap = {}
+    for gg, i in zip(g, ids):
+        if gg == 2:
+            per_cap[(i - 32) // 16] = per_cap.get((i - 32) // 16, 0) + 1
+    assert max(per_cap.values()) > 1
+
+
+def test_table_manifolds_equal_the_fresh_table_rule(oracle):
+    """The fresh table / plane rule stands for Bullet's manifolds of the end spheres (each re-reports
+    its one point every substep, which merges into itself with its impulse): Reach with the tool bar
+    on the table, 60 substeps, the default (fresh table pairs) against the study flag
+    PGX_FLAG_PERSISTENT_MANIFOLD (every robot pair through manifolds) -- the same trajectory to
+    rounding."""
+    from oracle import oracle as orc
+
+    outs = []
+    for flags in (0, abi.FLAG_PERSISTENT_MANIFOLD):
+        cfg = _cfg(task=abi.TASK_REACH)
+        cfg.contacts = abi.CONTACTS_FULL
+        cfg.params.contents.flags = flags
+        q = np.array(abi.NEUTRAL_Q[:7])
+        q[1], q[3] = 0.6, -1.55           # EE low over the table
+        target = q.copy()
+        target[1] += 0.35                 # drive it down into the table
+        qd, obj = np.zeros(7), _obj((5.0, 5.0, 5.0))
+        mot = _motors(oracle, target)
+        pts = 0
+        for _ in range(60):
+            q, qd, obj, st = oracle.world_substep(cfg, q, qd, obj, mot)
+            pts = max(pts, st.n_contacts)
+        outs.append((q.copy(), qd.copy(), pts, int(obj[orc.OBJ_MAN])))
+    (q0, qd0, n0, pool0), (q1, qd1, n1, pool1) = outs
+    assert n0 >= 1 and n0 == n1          # the bar touches the table in both
+    assert pool0 == 0 and pool1 >= 1     # only the study mode keeps manifolds for the table
+    assert np.abs(q0 - q1).max() < 1e-9 and np.abs(qd0 - qd1).max() < 1e-7

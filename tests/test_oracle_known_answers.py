@@ -156,3 +156,36 @@ def test_gravity_bias_matches_potential_gradient(oracle, custom_model):
     grad = np.array([(V(q + e) - V(q - e)) / 2e-6 for e in np.eye(7) * 1e-6])
     b = oracle.bias(custom_model, p, q, np.zeros(7), True, base=(-0.6, 0, 0))
     assert np.allclose(b, grad, atol=1e-5)
+
+
+def test_free_fall_base_velocity_known_answer(oracle):
+    """test/pybullet_test.py:56-64: a 1 kg box (half extents 0.5) created at rest, one env step
+    (20 substeps of 1/500 s) later, has base velocity [0, 0, -0.392] at atol 1e-3 -- the
+    floating-base path the cube takes (gravity, the base's damping m v (k + k|v|), the
+    semi-implicit update).  The oracle's scene has a table and a plane, so the box starts 10 m
+    up, far from both and from the robot; the reference's PyBullet() has neither."""
+    from oracle import oracle as orc
+
+    model = abi.make_model(load_model("panda_custom0"), ee_link=11)
+    params = abi.default_sim_params()
+    cfg = abi.make_config(abi.EnvSpec(task=abi.TASK_PUSH), 1, model, params)
+    cfg.object_half, cfg.object_mass = 0.5, 1.0
+    cfg.object_inertia = 1.0 * (2 * 0.5) ** 2 / 6.0   # box formula, 1 m edge
+    obj = np.zeros(orc.OBJ_N)
+    obj[0:3], obj[3:7] = (0.0, 0.0, 10.0), (0.0, 0.0, 0.0, 1.0)
+    obj[orc.OBJ_CACHE:orc.OBJ_AO:2] = -1.0
+    q, qd = np.array(abi.NEUTRAL_Q[:7]), np.zeros(7)
+    mot = oracle.make_motors(7, {d: (q[d], 0.0, 0.1, 1.0, abi.JOINT_FORCES[d] / 500.0) for d in range(7)})
+    for _ in range(20):
+        q, qd, obj, st = oracle.world_substep(cfg, q, qd, obj, mot)
+        assert st.n_contacts == 0
+    assert np.allclose(obj[7:10], [0.0, 0.0, -0.392], atol=ATOL), obj[7:10]
+    assert np.array_equal(obj[10:13], np.zeros(3))
+    # without the base's damping the same step gives g * 0.04 = -0.3924 exactly: the answer pins
+    # gravity and the update, and the damping keeps it within the tolerance (-0.39209)
+    assert -0.3924 < obj[9] < -0.3920
+    # the velocity the damping leaves, in closed form: v <- v + dt (g - (k + k|v|) v) twenty times
+    v = 0.0
+    for _ in range(20):
+        v = v + (1.0 / 500.0) * (-9.81 - (0.04 + 0.04 * abs(v)) * v)
+    assert abs(obj[9] - v) < 1e-12

@@ -1,0 +1,43 @@
+#!/bin/bash
+# Round 5 GPU script.  Steps (each under its own time limit, chained so the first crash ends it):
+#   PROBE="abl/a.so ..."  tools/gpu_nan_probe.py on debug libraries (make -C panda-gym_amd/csrc dbg)
+#   tests (unless NO_TESTS=1): pytest -m gpu (PGX_PYTEST_ARGS appended), then smoke()
+#   AB="abl/a.so abl/b.so" AB_CASES=...: tools/ab_libs.py timing of library builds
+#   BENCH=1: bench.py with the driver's arguments (--steps 20 --warmup 5) and the defaults, then
+#            rocprofv3 --kernel-trace --stats of the driver-argument run
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${1:-r5}
+TEST_RC=0
+if [ -n "$PROBE" ]; then
+  timeout -k 10 900 python -u tools/gpu_nan_probe.py $PROBE > gpurun_out/probe_$TAG.log 2>&1
+  rc=$?
+  tail -60 gpurun_out/probe_$TAG.log
+  if [ $rc -ne 0 ]; then exit $rc; fi
+fi
+if [ -z "$NO_TESTS" ]; then
+  # assertion failures (pytest rc 1) do not stop the timing steps below; anything else (a crash,
+  # an abort, a time limit) ends the script here
+  timeout -k 10 900 python -u -m pytest tests -v -m gpu --timeout 240 --timeout-method thread ${PGX_PYTEST_ARGS} > gpurun_out/pytest_gpu_$TAG.log 2>&1
+  TEST_RC=$?
+  grep -E "FAILED|ERROR" gpurun_out/pytest_gpu_$TAG.log | head -40
+  tail -3 gpurun_out/pytest_gpu_$TAG.log
+  if [ $TEST_RC -ne 0 ] && [ $TEST_RC -ne 1 ]; then exit $TEST_RC; fi
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { tail -20 gpurun_out/smoke_$TAG.log; exit 1; }
+  cat gpurun_out/smoke_$TAG.log
+fi
+if [ -n "$AB" ]; then
+  timeout -k 10 1100 python -u tools/ab_libs.py $AB > gpurun_out/ab_$TAG.log 2> gpurun_out/ab_$TAG.err || { tail -20 gpurun_out/ab_$TAG.err; exit 1; }
+  cat gpurun_out/ab_$TAG.log
+fi
+if [ -n "$BENCH" ]; then
+  timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_drv_$TAG.json 2> gpurun_out/bench_drv_$TAG.err || { tail -20 gpurun_out/bench_drv_$TAG.err; exit 1; }
+  cat gpurun_out/bench_drv_$TAG.json
+  timeout -k 10 400 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -20 gpurun_out/bench_$TAG.err; exit 1; }
+  cat gpurun_out/bench_$TAG.json
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1 || { tail -20 gpurun_out/prof_$TAG.log; exit 1; }
+  find gpurun_out/prof_$TAG -name "*stats*"
+fi
+exit $TEST_RC
