@@ -53,8 +53,9 @@ def load(path: str = None):
     lib.pgx_get_state.argtypes = [C.c_void_p, C.POINTER(PgxStateView)]
     lib.pgx_reset.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(PgxStepOut), C.c_void_p]
     lib.pgx_step.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(PgxStepOut), C.c_void_p]
-    lib.pgx_step_kernel.argtypes = [C.c_void_p]
-    lib.pgx_step_kernel.restype = C.c_char_p
+    if hasattr(lib, "pgx_step_kernel"):   # (A/B runs load older builds with EXPORTS filtered)
+        lib.pgx_step_kernel.argtypes = [C.c_void_p]
+        lib.pgx_step_kernel.restype = C.c_char_p
     lib.pgx_sample_actions.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
     lib.pgx_compute_reward.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_double, C.c_void_p,
                                        C.c_void_p]

@@ -79,6 +79,7 @@ struct pgx_env {
      * graph captured in either mode never reads freed memory */
     uint64_t* pcg = nullptr;
     bool pcg_set = false;   /* host mirror of the mode word */
+    int man_pool = 0;       /* persistent manifold pool capacity (0: none) */
     /* the step kernel the last pgx_step launched (pgx_step_kernel) */
     const char* step_kernel = nullptr;
 };
@@ -440,10 +441,17 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     if (rc) { delete h; return rc; }
     const size_t N = (size_t)cfg->n_envs;
     auto align = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    /* Bullet's persistent manifolds of the robot's cube / obstacle pairs (the per-pair budget's
+     * kernels): the pool, count + points (pgx.h PGX_MANIFOLD_POOL) */
+    const int man_pool = (e.full_manifold && (e.has_object || e.ao)) ? (e.has_object ? PGX_MANIFOLD_POOL
+                                                                                     : PGX_MANIFOLD_POOL_AO) : 0;
+    const size_t man_rows = man_pool ? 1 + (size_t)man_pool * PGX_MANIFOLD_POINT : 0;
+    h->man_pool = man_pool;
     size_t off_goal = align(sizeof(PgxDevModel)), off_q = align(off_goal + 3 * N * 8), off_qd = align(off_q + PGX_NJ * N * 4),
            off_qc = align(off_qd + PGX_NJ * N * 4), off_obj = align(off_qc + PGX_NJ * N * 4), off_ct = align(off_obj + 13 * N * 4),
            off_ao = align(off_ct + 2 * PGX_CONTACT_SLOTS * N * 4),
-           off_el = align(off_ao + (e.ao ? 4 * PGX_AO_OBSTACLES * N * 4 : 0)), off_ep = align(off_el + N * 4),
+           off_man = align(off_ao + (e.ao ? 4 * PGX_AO_OBSTACLES * N * 4 : 0)),
+           off_el = align(off_man + man_rows * N * 4), off_ep = align(off_el + N * 4),
            off_err = align(off_ep + N * 4), off_perm = align(off_err + 4),
            total = align(off_perm + (e.full_manifold ? N * 4 + (N + 3) / 4 * 4 + (N / 256 + 1) * 13 * 4 : 0));
     rc = hip_check(hipMalloc(&h->blob, total), "hipMalloc(state)");
@@ -457,6 +465,7 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     h->ds.object = (float*)(b + off_obj);
     h->ds.contacts = (float*)(b + off_ct);
     h->ds.obstacles = e.ao ? (float*)(b + off_ao) : nullptr;
+    h->ds.man = man_pool ? (float*)(b + off_man) : nullptr;
     h->ds.elapsed = (int32_t*)(b + off_el);
     h->ds.episode = (uint32_t*)(b + off_ep);
     h->ds.errors = (uint32_t*)(b + off_err);
@@ -512,6 +521,8 @@ int pgx_get_state(pgx_handle h, pgx_state_view* out) {
                       : !h->de.full_manifold ? PGX_ROBOT_POINTS_ONE_LANE
                       : h->de.has_object ? PGX_ROBOT_POINTS : PGX_ROBOT_POINTS_ARM;
     out->env_order = h->de.perm_buf;
+    out->manifolds = h->ds.man;
+    out->manifold_pool = h->man_pool;
     return PGX_OK;
 }
 

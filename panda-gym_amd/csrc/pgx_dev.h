@@ -92,6 +92,7 @@ struct PgxDevState {
     float* object;     /* [13][N] pos3 quat4 (x,y,z,w) linvel3 angvel3 */
     float* contacts;   /* [2*PGX_CONTACT_SLOTS][N] warm-start cache (feature id, normal impulse) */
     float* obstacles;  /* [4*PGX_AO_OBSTACLES][N] ReachAO centres (o, xyz) then active flags */
+    float* man;        /* [1 + pool * PGX_MANIFOLD_POINT][N] persistent manifold pool (pgx.h), or nullptr */
     int32_t* elapsed;  /* [N] */
     uint32_t* episode; /* [N] */
     uint32_t* errors;  /* [1] sticky PGX_ERR_* bits (pgx_state_view.errors) */

@@ -719,6 +719,13 @@ __device__ __forceinline__ V3 ao_table_h(const PgxDevEnv& e) { return v3(e.table
  * stride, so each quad is one conflict-free ds_read_b128 (MI355X_MICROARCH.md, LDS). */
 constexpr int CG = PGX_OBJECT_POINTS;   /* object-scene budget; robot points whose rows live in VGPRs */
 constexpr int MANIFOLD = 4;             /* btPersistentManifold MANIFOLD_CACHE_SIZE: points per pair */
+/* ReachAO's obstacle pairs through Bullet's persistent manifolds (PGX_AO_FRESH: round 4's fresh
+ * per-substep candidates instead -- an A/B build only, the oracle's PGX_FLAG_FRESH_MANIFOLD) */
+#ifdef PGX_AO_FRESH
+constexpr bool AO_PERS = false;
+#else
+constexpr bool AO_PERS = true;
+#endif
 
 /* robot points kept per env: the one-lane layout holds its rows in LDS for 64 envs (4); the
  * wide layout 4 in VGPRs, and with FULL (PGX_FLAG_FULL_MANIFOLD) the rest, up to
@@ -740,9 +747,11 @@ static_assert(PGX_NCAP <= 16, "PgxDevModel.cap_mu holds 16 capsules");
  * plane 2c + end, cube 32 + 16c + sample, obstacle 32 + 6c + obstacle (AO).  In the default build
  * the table is a compile-time constant, so the chain folds to the capsules that differ from the
  * cube's pair (m.friction). */
-template <int AO>
+template <int AO, int FULL = 0>
 __device__ __forceinline__ float point_mu(MRef m, float id) {
-    const float cf = id < kTableIdLimit ? id * 0.5f : (id - kTableIdLimit) * (AO ? (1.0f / 6.0f) : 0.0625f);
+    /* (FULL: ReachAO's manifold points 32 + 24 c + 4 o + slot; the cube's 32 + 16 c + slot) */
+    const float cf = id < kTableIdLimit ? id * 0.5f
+                   : (id - kTableIdLimit) * (AO ? (FULL ? (1.0f / 24.0f) : (1.0f / 6.0f)) : 0.0625f);
     const int cap = (int)(cf + 1e-3f);   /* (ids are exact small integers; the margin covers 1/6's rounding) */
     float mu = m.friction;
     sfor<0, PGX_NCAP>([&](auto kc) __attribute__((always_inline)) {
@@ -760,15 +769,27 @@ struct ContactLdsT {
     static constexpr int P0 = OBJ ? CG : 0;
     static constexpr int NQR = 3 * (P0 + CG), NQX = 3 * (P0 + RB);
     static constexpr int XR = (W == 64 || RB <= CG) ? 1 : NQX - NQR;   /* extra rows */
+    /* Bullet's persistent manifolds of the robot's cube / obstacle pairs (FULL, the wide layout): the
+     * pool's capacity in points (pgx.h PGX_MANIFOLD_POOL / _AO; Reach has no such pair) */
+    static constexpr int MP = (W == 64 || !FULL) ? 1 : (OBJ ? PGX_MANIFOLD_POOL : PGX_MANIFOLD_POOL_AO);
+    /* the object-scene arrays exist in the object tasks' layouts only (ReachAO's two-wave kernel
+     * fits its LDS budget without them) */
+    static constexpr int G0 = (W == 64 || OBJ) ? CG : 1;
     /* group 0: object vertices vs table / plane (normal +z) */
-    float4 g0q[CG][4][W];         /* [0] = contact point - object COM; [1 + dir] = (jinv, den, rhs, lambda) */
-    float g0d[CG][W], g0id[CG][W];
+    float4 g0q[G0][4][W];         /* [0] = contact point - object COM; [1 + dir] = (jinv, den, rhs, lambda) */
+    float g0d[G0][W], g0id[G0][W];
     /* group 1: robot vs table / plane / object / obstacles */
     float g1p[RB][3][W];          /* point on the robot */
     float g1n[RB][3][W];          /* normal, from the other body to the robot */
     float g1rb[RB][3][W];         /* object contacts: point on the object - object COM */
     float g1d[RB][W], g1id[RB][W];
     int g1j[RB][W];               /* arm joint carrying the robot link */
+    int g1w[RB][W];               /* a manifold point's pool index (its warm start and write-back), -1 else */
+    /* the manifold pool per env (pgx.h PGX_MANIFOLD_POOL): count, then per point kid (key + slot),
+     * local A (the carrying joint's frame), local B (cube frame / world), normal on B (world),
+     * distance (the last refresh's), applied normal impulse */
+    int mcnt[W];
+    float mkid[MP][W], mla[MP][3][W], mlb[MP][3][W], mn[MP][3][W], md[MP][W], mimp[MP][W];
     /* one-lane layout, per direction: (J0..3) (J4..6, jinv) (R0..3) (R4..6, den) (cl, rhs) (ca, lambda)
      * with J the robot Jacobian row, R = M^-1 J^T, (cl, ca) the object part (0 against the table) */
     float4 g1q[W == 64 ? CG : 1][3][6][W == 64 ? W : 1];
@@ -789,10 +810,10 @@ struct ContactLdsT {
     float xrhs[XR][W], xlam[XR][W], xlam0[XR][W], xfk[XR][W], xjinv[XR][W];
     /* wide layout, the register points' normal rows: jinv (the cache's impulse lambda' jinv)
      * and lambda' at the solve's start (a redo), kept here through the sweeps */
-    float pjn[W == 64 ? 1 : 2 * CG][W], pl0[W == 64 ? 1 : 2 * CG][W];
+    float pjn[W == 64 ? 1 : P0 + CG][W], pl0[W == 64 ? 1 : P0 + CG][W];
     /* wide layout, object tasks: the limit rows' rhs' and lambda' of the all-rows solve (in
      * registers beside the 24 contact rows they set the kernel's register peak) */
-    float lrhs[W == 64 ? 1 : PGX_N_ROWS - PGX_NJ][W], llam[W == 64 ? 1 : PGX_N_ROWS - PGX_NJ][W];
+    float lrhs[(W == 64 || !OBJ) ? 1 : PGX_N_ROWS - PGX_NJ][W], llam[(W == 64 || !OBJ) ? 1 : PGX_N_ROWS - PGX_NJ][W];
     /* wide layout: state that lives across the substep loop but is read once per substep or after
      * it, parked here instead of in registers (the motor targets; the substeps' start poses,
      * double-buffered: getLinkState's cached pose is the last completed substep's start) */
@@ -867,6 +888,7 @@ __device__ __forceinline__ void g1_copy(LT& L, int ln, int to, int from) {
     L.g1d[to][ln] = L.g1d[from][ln];
     L.g1id[to][ln] = L.g1id[from][ln];
     L.g1j[to][ln] = L.g1j[from][ln];
+    L.g1w[to][ln] = L.g1w[from][ln];
     for (int k = 0; k < 3; k++) {
         L.g1p[to][k][ln] = L.g1p[from][k][ln];
         L.g1n[to][k][ln] = L.g1n[from][k][ln];
@@ -874,14 +896,14 @@ __device__ __forceinline__ void g1_copy(LT& L, int ln, int to, int from) {
     }
 }
 template <class LT>
-__device__ __forceinline__ void g1_insert(LT& L, int ln, float d, float id, int j, V3 p, V3 n, V3 rb) {
+__device__ __forceinline__ void g1_insert(LT& L, int ln, float d, float id, int j, V3 p, V3 n, V3 rb, int w = -1) {
     constexpr int RB = LT::RB;   /* the robot group's budget: its RB deepest */
     int c = L.cnt[1][ln], pos;
     if (c < RB) { pos = c; L.cnt[1][ln] = c + 1; }
     else if (d < L.g1d[RB - 1][ln]) pos = RB - 1;
     else return;
     while (pos > 0 && d < L.g1d[pos - 1][ln]) { g1_copy(L, ln, pos, pos - 1); pos--; }
-    L.g1d[pos][ln] = d; L.g1id[pos][ln] = id; L.g1j[pos][ln] = j;
+    L.g1d[pos][ln] = d; L.g1id[pos][ln] = id; L.g1j[pos][ln] = j; L.g1w[pos][ln] = w;
     L.g1p[pos][0][ln] = p.x; L.g1p[pos][1][ln] = p.y; L.g1p[pos][2][ln] = p.z;
     L.g1n[pos][0][ln] = n.x; L.g1n[pos][1][ln] = n.y; L.g1n[pos][2][ln] = n.z;
     L.g1rb[pos][0][ln] = rb.x; L.g1rb[pos][1][ln] = rb.y; L.g1rb[pos][2][ln] = rb.z;
@@ -893,11 +915,11 @@ __device__ __forceinline__ void sort_g1_by_depth(LT& L, int ln) {
     for (int i = 1; i < c1; i++)
         for (int j = i; j > 0 && L.g1d[j][ln] < L.g1d[j - 1][ln]; j--) {
             float d = L.g1d[j][ln], id = L.g1id[j][ln];
-            int jj = L.g1j[j][ln];
+            int jj = L.g1j[j][ln], ww = L.g1w[j][ln];
             float p[3], n[3], rb[3];
             for (int k = 0; k < 3; k++) { p[k] = L.g1p[j][k][ln]; n[k] = L.g1n[j][k][ln]; rb[k] = L.g1rb[j][k][ln]; }
             g1_copy(L, ln, j, j - 1);
-            L.g1d[j - 1][ln] = d; L.g1id[j - 1][ln] = id; L.g1j[j - 1][ln] = jj;
+            L.g1d[j - 1][ln] = d; L.g1id[j - 1][ln] = id; L.g1j[j - 1][ln] = jj; L.g1w[j - 1][ln] = ww;
             for (int k = 0; k < 3; k++) { L.g1p[j - 1][k][ln] = p[k]; L.g1n[j - 1][k][ln] = n[k]; L.g1rb[j - 1][k][ln] = rb[k]; }
         }
 }
@@ -915,11 +937,11 @@ __device__ __forceinline__ void sort_groups(LT& L, int ln) {
     for (int i = 1; i < c1; i++)
         for (int j = i; j > 0 && L.g1id[j][ln] < L.g1id[j - 1][ln]; j--) {
             float d = L.g1d[j][ln], id = L.g1id[j][ln];
-            int jj = L.g1j[j][ln];
+            int jj = L.g1j[j][ln], ww = L.g1w[j][ln];
             float p[3], n[3], rb[3];
             for (int k = 0; k < 3; k++) { p[k] = L.g1p[j][k][ln]; n[k] = L.g1n[j][k][ln]; rb[k] = L.g1rb[j][k][ln]; }
             g1_copy(L, ln, j, j - 1);
-            L.g1d[j - 1][ln] = d; L.g1id[j - 1][ln] = id; L.g1j[j - 1][ln] = jj;
+            L.g1d[j - 1][ln] = d; L.g1id[j - 1][ln] = id; L.g1j[j - 1][ln] = jj; L.g1w[j - 1][ln] = ww;
             for (int k = 0; k < 3; k++) { L.g1p[j - 1][k][ln] = p[k]; L.g1n[j - 1][k][ln] = n[k]; L.g1rb[j - 1][k][ln] = rb[k]; }
         }
 }
@@ -1096,6 +1118,236 @@ __device__ __forceinline__ void object_candidates_g(const PgxDevEnv& e, float ta
     }
 }
 
+/* ---- Bullet's persistent manifolds in the wide layout (FULL kernels, the robot's pairs with the cube
+ * or the obstacles): the oracle's man_add / pool_refresh (oracle/pgx_oracle.c)
+ * with the same rules and order, in fp32.  The per-env steps (a merge, the insertion into the row
+ * list) run on every lane of the env's row with the same values (LDS reads, identical writes); the
+ * refresh runs lane-parallel, lane p of the row refreshing pool point p. */
+template <int AO>
+__device__ __forceinline__ int man_capsule(int key) { return AO ? (key - 32) / 24 : (key - 32) / 16; }
+
+/* addContactPoint of the new point (la, lb, n, d) to manifold `key` of env es's pool: getCacheEntry
+ * (the cached point nearest in A's frame, strictly within thr^2, first in slot order) -> its fields
+ * replaced, impulse kept; else appended below 4 points (dropped when the pool is full); else
+ * sortCachedPoints' slot overwritten, impulse 0 */
+template <class LT>
+__device__ __forceinline__ void man_add_g(LT& L, int es, int key, V3 la, V3 lb, V3 n, float d, float thr2) {
+    constexpr int MP = LT::MP;
+    const int cnt = L.mcnt[es];
+    int i0 = 0, i1 = 0, i2 = 0, i3 = 0, nk = 0;
+    for (int i = 0; i < cnt; i++) {   /* the manifold's points by slot */
+        const int kid = (int)L.mkid[i][es];
+        if ((kid & ~3) == key) {
+            const int sl = kid & 3;
+            i0 = sl == 0 ? i : i0; i1 = sl == 1 ? i : i1; i2 = sl == 2 ? i : i2; i3 = sl == 3 ? i : i3;
+            nk++;
+        }
+    }
+    const int idx[4] = {i0, i1, i2, i3};
+    V3 cla[4];
+    float cd[4];
+    int near = -1;
+    float sh = thr2;
+#pragma unroll
+    for (int sl = 0; sl < 4; sl++) {
+        cla[sl] = lds3(L.mla[idx[sl]], es);
+        cd[sl] = L.md[idx[sl]][es];
+        const V3 e = cla[sl] - la;
+        const float dd = dot(e, e);
+        if (sl < nk && dd < sh) { sh = dd; near = sl; }
+    }
+    int at;
+    if (near >= 0) {
+        at = idx[0];
+        at = near == 1 ? idx[1] : at; at = near == 2 ? idx[2] : at; at = near == 3 ? idx[3] : at;
+    } else if (nk < 4) {
+        if (cnt >= MP) return;   /* the pool is full: dropped (as the oracle) */
+        at = cnt;
+        L.mkid[at][es] = (float)(key + nk);
+        L.mimp[at][es] = 0.0f;
+        L.mcnt[es] = cnt + 1;
+    } else {   /* sortCachedPoints: keep the deepest, else the largest area */
+        int maxi = -1;
+        float maxpen = d;
+#pragma unroll
+        for (int sl = 0; sl < 4; sl++)
+            if (cd[sl] < maxpen) { maxi = sl; maxpen = cd[sl]; }
+        float res[4];
+        res[0] = maxi == 0 ? 0.0f : dot(cross(la - cla[1], cla[3] - cla[2]), cross(la - cla[1], cla[3] - cla[2]));
+        res[1] = maxi == 1 ? 0.0f : dot(cross(la - cla[0], cla[3] - cla[2]), cross(la - cla[0], cla[3] - cla[2]));
+        res[2] = maxi == 2 ? 0.0f : dot(cross(la - cla[0], cla[3] - cla[1]), cross(la - cla[0], cla[3] - cla[1]));
+        res[3] = maxi == 3 ? 0.0f : dot(cross(la - cla[0], cla[2] - cla[1]), cross(la - cla[0], cla[2] - cla[1]));
+        int best = 0;
+        float bv = res[0];
+#pragma unroll
+        for (int sl = 1; sl < 4; sl++)
+            if (res[sl] > bv) { bv = res[sl]; best = sl; }
+        at = idx[0];
+        at = best == 1 ? idx[1] : at; at = best == 2 ? idx[2] : at; at = best == 3 ? idx[3] : at;
+        L.mimp[at][es] = 0.0f;
+    }
+    L.mla[at][0][es] = la.x; L.mla[at][1][es] = la.y; L.mla[at][2][es] = la.z;
+    L.mlb[at][0][es] = lb.x; L.mlb[at][1][es] = lb.y; L.mlb[at][2][es] = lb.z;
+    L.mn[at][0][es] = n.x; L.mn[at][1][es] = n.y; L.mn[at][2][es] = n.z;
+    L.md[at][es] = d;
+}
+
+/* the joint frame j (lane j of the row holds R_j, o_j in Rl, ol) in any lane: a row bpermute */
+__device__ __forceinline__ void joint_frame(const M3& Rl, V3 ol, int j, M3& R, V3& o) {
+    const int src = (int)(threadIdx.x & ~(unsigned)(GW - 1)) + (j < 0 ? 0 : j);
+#pragma unroll
+    for (int t = 0; t < 9; t++) R.m[t] = __shfl(Rl.m[t], src);
+    o = v3(__shfl(ol.x, src), __shfl(ol.y, src), __shfl(ol.z, src));
+}
+
+/* refreshContactPoints of env es's pool (lane c refreshes point c), the removals renumbered as
+ * Bullet's removeContactPoint does (reverse slot order, the last slot's point fills the hole) with
+ * the survivors' pool order kept, then every point inserted into the robot row list (g1_insert:
+ * after the table candidates, in pool order) as its own row: id = kid, pool index in g1w.
+ * OBJ: B is the cube (Rc, op), else a static obstacle (local B = world). */
+template <int OBJ, int AO, class LT>
+__device__ __forceinline__ void man_refresh_insert_g(LT& L, int es, int c, const M3& Rl, V3 ol, const M3& Rc, V3 op,
+                                                     float thr) {
+    const int cnt = L.mcnt[es];
+    const bool mine = c < cnt;
+    const int p = mine ? c : 0;
+    const int kid = (int)L.mkid[p][es], key = kid & ~3;
+    const int cap = man_capsule<AO>(key < 32 ? 32 : key);
+    const int j = kCapJ[cap < 0 ? 0 : (cap >= PGX_NCAP ? PGX_NCAP - 1 : cap)];
+    M3 R;
+    V3 o;
+    joint_frame(Rl, ol, j, R, o);
+    const V3 la = lds3(L.mla[p], es), lb = lds3(L.mlb[p], es), n = lds3(L.mn[p], es);
+    const V3 pa = o + mul(R, la);
+    const V3 pb = OBJ ? op + mul(Rc, lb) : lb;
+    const float d = dot(pa - pb, n);
+    const V3 e = pb - (pa - d * n);
+    const bool drop = mine && (d > thr || dot(e, e) > thr * thr);
+    const unsigned dm = row_ballot(drop);
+    const unsigned km = row_ballot(mine && !drop);
+    const int row0 = (int)(threadIdx.x & ~(unsigned)(GW - 1));
+    const int newp = mine && !drop ? __builtin_popcount(km & ((1u << c) - 1u)) : -1;
+    int kidn = kid;   /* this point's kid after the removals */
+    if (__any(dm != 0u)) {   /* (rare) removals: this point's slot after Bullet's renumbering, compaction */
+        int slot = kid & 3, dmask = 0, nk = 0;
+        for (int t = 0; t < GW; t++) {
+            const int kt = __shfl(kid, row0 + t);
+            const bool inm = ((km | dm) >> t) & 1u;
+            if (inm && (kt & ~3) == key) {
+                nk++;
+                if ((dm >> t) & 1u) dmask |= 1 << (kt & 3);
+            }
+        }
+        int cur0 = 0, cur1 = 1, cur2 = 2, cur3 = 3, nn = nk;
+#pragma unroll
+        for (int s2 = 3; s2 >= 0; s2--) {
+            const int cs = s2 == 0 ? cur0 : (s2 == 1 ? cur1 : (s2 == 2 ? cur2 : cur3));
+            if (s2 < nn && ((dmask >> cs) & 1)) {
+                const int last = nn - 1 == 0 ? cur0 : (nn - 1 == 1 ? cur1 : (nn - 1 == 2 ? cur2 : cur3));
+                if (s2 == 0) cur0 = last; else if (s2 == 1) cur1 = last; else if (s2 == 2) cur2 = last; else cur3 = last;
+                nn--;
+            }
+        }
+        int ns = slot;
+        ns = (0 < nn && cur0 == slot) ? 0 : ns;
+        ns = (1 < nn && cur1 == slot) ? 1 : ns;
+        ns = (2 < nn && cur2 == slot) ? 2 : ns;
+        ns = (3 < nn && cur3 == slot) ? 3 : ns;
+        kidn = key + ns;
+        /* read every field, then write it at the compacted index with the new kid */
+        const float imp = L.mimp[p][es];
+        if (newp >= 0) {
+            L.mkid[newp][es] = (float)kidn;
+            L.mla[newp][0][es] = la.x; L.mla[newp][1][es] = la.y; L.mla[newp][2][es] = la.z;
+            L.mlb[newp][0][es] = lb.x; L.mlb[newp][1][es] = lb.y; L.mlb[newp][2][es] = lb.z;
+            L.mn[newp][0][es] = n.x; L.mn[newp][1][es] = n.y; L.mn[newp][2][es] = n.z;
+            L.md[newp][es] = d;
+            L.mimp[newp][es] = imp;
+        }
+        L.mcnt[es] = __builtin_popcount(km);
+    } else if (mine) {
+        L.md[p][es] = d;
+    }
+    /* the manifold points as rows, in pool order (after the table candidates already in the list) */
+    const V3 rb = pb - op;
+    const int nkeep = __builtin_popcount(km);
+    for (int t = 0; t < GW; t++) {
+        if (!__any(t < nkeep)) break;
+        /* the lane holding new pool index t: the t-th set bit of km */
+        unsigned mm = km;
+        for (int u = 0; u < t; u++) mm &= mm - 1u;
+        const int src = row0 + (mm ? __builtin_ctz(mm) : 0);
+        const float dt = __shfl(d, src);
+        const int kidt = __shfl(kidn, src);
+        const V3 pt = v3(__shfl(pa.x, src), __shfl(pa.y, src), __shfl(pa.z, src));
+        const V3 nt = v3(__shfl(n.x, src), __shfl(n.y, src), __shfl(n.z, src));
+        const V3 rt = v3(__shfl(rb.x, src), __shfl(rb.y, src), __shfl(rb.z, src));
+        const int jt = __shfl(j, src);
+        if (t < nkeep) g1_insert(L, es, dt, (float)kidt, jt, pt, nt, OBJ ? rt : v3(0.0f, 0.0f, 0.0f), t);
+    }
+}
+
+/* Bullet's persistent manifold of capsule cn (wave-uniform) and the cube (FULL kernels): lane s of
+ * the env's row evaluates sample s as object_candidates_g does (the same arithmetic), the pair's new
+ * point is its deepest candidate (ties: the lowest sample -- GJK's closest pair of the convex
+ * capsule and the box, restated), and addContactPoint merges it into the env's pool (man_add_g):
+ * point on the capsule pa = C - r n in the frame of the capsule's joint, the box's closest point
+ * in the cube frame, the normal from the cube, the depth. */
+template <class LT>
+__device__ __forceinline__ void object_new_point_g(const PgxDevEnv& e, float tau, LT& L, int es, const ObjState& ob,
+                                                   const M3& Rc, int cn, int c, bool env_near, const M3& Rl, V3 ol) {
+    const V3 A = lds3(L.capA[cn], es), B = lds3(L.capB[cn], es);
+    const float r = kCapR[cn];
+    const int jc = kCapJ[cn], ns = kCapNs[cn];
+    const float h = e.obj_half;
+    const V3 ab = B - A;
+    const float inv_n = ns > 1 ? 1.0f / (float)(ns - 1) : 0.0f;
+    const V3 C = A + ((float)c * inv_n) * ab;
+    const V3 cl = mul_t(Rc, C - ob.p);
+    V3 qb = v3(fminf(fmaxf(cl.x, -h), h), fminf(fmaxf(cl.y, -h), h), fminf(fmaxf(cl.z, -h), h));
+    const V3 diff = cl - qb;
+    const float d2 = dot(diff, diff);
+    V3 nl;
+    float depth;
+    if (d2 > 1e-24f) {
+        const float dist = fast_sqrt(d2);
+        nl = fast_rcp(dist) * diff;
+        depth = dist - r;
+    } else { /* centre inside the box: out through the nearest face */
+        const float bx = h - fabsf(cl.x), by = h - fabsf(cl.y), bz = h - fabsf(cl.z);
+        int ax = 0;
+        float best = bx;
+        if (by < best) { best = by; ax = 1; }
+        if (bz < best) { best = bz; ax = 2; }
+        const float sx = cl.x < 0.0f ? -1.0f : 1.0f, sy = cl.y < 0.0f ? -1.0f : 1.0f, sz = cl.z < 0.0f ? -1.0f : 1.0f;
+        nl = v3(ax == 0 ? sx : 0.0f, ax == 1 ? sy : 0.0f, ax == 2 ? sz : 0.0f);
+        if (ax == 0) qb.x = sx * h;
+        if (ax == 1) qb.y = sy * h;
+        if (ax == 2) qb.z = sz * h;
+        depth = -best - r;
+    }
+    const bool cand = env_near && c < ns && depth < tau;
+    const float dd = cand ? depth : 3.0e38f;
+    int rank = 0;
+    sfor<0, 16>([&](auto uc) __attribute__((always_inline)) {
+        constexpr int U = decltype(uc)::value;
+        const float du = bcast16<U>(dd);
+        rank += (du < dd || (du == dd && U < c)) ? 1 : 0;
+    });
+    const unsigned bm = row_ballot(cand && rank == 0);
+    M3 Rj;
+    V3 oj;
+    joint_frame(Rl, ol, jc, Rj, oj);   /* (every lane: a row bpermute) */
+    const int src = (int)(threadIdx.x & ~(unsigned)(GW - 1)) + (bm ? __builtin_ctz(bm) : 0);
+    const V3 n = mul(Rc, nl);
+    const V3 pa = C - r * n;
+    const V3 pk = v3(__shfl(pa.x, src), __shfl(pa.y, src), __shfl(pa.z, src));
+    const V3 nk = v3(__shfl(n.x, src), __shfl(n.y, src), __shfl(n.z, src));
+    const V3 qk = v3(__shfl(qb.x, src), __shfl(qb.y, src), __shfl(qb.z, src));
+    const float dk = __shfl(depth, src);
+    if (bm) man_add_g(L, es, 32 + 16 * cn, mul_t(Rj, pk - oj), qk, nk, dk, tau * tau);
+}
+
 /* ReachAO: the obstacles are static colliders (create_obstacle_sphere / _cuboid,
  * reach_ao.py:819-860: mass 0, not ghosts), so stepSimulation resolves robot contacts with
  * them like the table's (oracle detect(), "ReachAO" branch): capsule c (wave-uniform) against
@@ -1248,14 +1500,14 @@ __device__ __forceinline__ void robot_table_contacts_g(const PgxDevEnv& e, float
     const int jc = cl.j;
     if (k0) {
         const int sl = base;
-        L.g1d[sl][es] = d0; L.g1id[sl][es] = (float)(2 * c); L.g1j[sl][es] = jc;
+        L.g1d[sl][es] = d0; L.g1id[sl][es] = (float)(2 * c); L.g1j[sl][es] = jc; L.g1w[sl][es] = -1;
         L.g1p[sl][0][es] = A.x; L.g1p[sl][1][es] = A.y; L.g1p[sl][2][es] = A.z - r;
         L.g1n[sl][0][es] = 0.0f; L.g1n[sl][1][es] = 0.0f; L.g1n[sl][2][es] = 1.0f;
         L.g1rb[sl][0][es] = 0.0f; L.g1rb[sl][1][es] = 0.0f; L.g1rb[sl][2][es] = 0.0f;
     }
     if (k1) {
         const int sl = base + (k0 ? 1 : 0);
-        L.g1d[sl][es] = d1; L.g1id[sl][es] = (float)(2 * c + 1); L.g1j[sl][es] = jc;
+        L.g1d[sl][es] = d1; L.g1id[sl][es] = (float)(2 * c + 1); L.g1j[sl][es] = jc; L.g1w[sl][es] = -1;
         L.g1p[sl][0][es] = B.x; L.g1p[sl][1][es] = B.y; L.g1p[sl][2][es] = B.z - r;
         L.g1n[sl][0][es] = 0.0f; L.g1n[sl][1][es] = 0.0f; L.g1n[sl][2][es] = 1.0f;
         L.g1rb[sl][0][es] = 0.0f; L.g1rb[sl][1][es] = 0.0f; L.g1rb[sl][2][es] = 0.0f;
@@ -1651,6 +1903,7 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                     const float lb = fminf(box_sd(A, tc, thi), box_sd(B, tc, thi)) - 0.5f * norm(B - A) - kAoMargin - r;
                     if (lb <= 0.0f) hit = capsule_box_hit(A, B, r, tc, th);
                 }
+                unsigned cmask = 0;   /* FULL: this lane's candidate obstacles */
                 V3 Cs[AO_N];   /* the obstacle centres, one LDS batch */
 #pragma unroll
                 for (int o = 0; o < AO_N; o++) Cs[o] = lds3(Lp->aoC[o], es);
@@ -1669,6 +1922,10 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                     }
                     hit = hit || (chk && d <= 0.0f);
                     const bool cand = cap_on && d < tau;
+                    if constexpr (FULL && AO_PERS) {   /* the manifolds take the new points after the collision check */
+                        cmask |= cand ? (1u << o) : 0u;
+                        continue;
+                    }
                     const uint64_t bm = __ballot(cand);
                     if (bm == 0) continue;
                     if (!sorted) { sort_g1_by_depth(*Lp, es); sorted = true; }
@@ -1689,6 +1946,54 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                 if (sorted) sort_groups(*Lp, es);
                 D.coll = row_any(hit);
                 if (D.coll) return;   /* the step stops here: nothing of this substep runs */
+                if constexpr (FULL && AO_PERS) {
+                    /* Bullet's persistent manifolds of the obstacle pairs: each candidate pair's new
+                     * point (the same closest-pair arithmetic as above, recomputed for the few
+                     * candidates) merged obstacle-major, capsule by capsule, then the refresh and the
+                     * rows (oracle detect(), the persistent branch) */
+                    if (__any(cmask != 0u)) {
+                        for (int o = 0; o < AO_N; o++) {
+                            const bool have = (cmask >> o) & 1u;
+                            const uint64_t bo = __ballot(have);
+                            if (bo == 0) continue;
+                            const V3 C = lds3(Lp->aoC[o], es);
+                            V3 P = seg_closest(A, B, C);
+                            const V3 v = C - P;
+                            const float len = norm(v);
+                            V3 n = len > 0.0f ? fast_rcp(len) * v : v3(0.0f, 0.0f, 1.0f);
+                            float d = 3.0e38f;
+                            if (have) {
+                                if (o < 3) d = len - r - kAoSize;
+                                else d = capsule_box_pair<true>(A, B, r, C, hcube, &P, &n);
+                            }
+                            const V3 pa = P + r * n;        /* on the capsule, towards the obstacle */
+                            const V3 pb = pa + d * n;       /* on the obstacle (static: local = world) */
+                            unsigned wo = __builtin_amdgcn_readfirstlane(
+                                (unsigned)((bo | (bo >> 16) | (bo >> 32) | (bo >> 48)) & 0xFFFFu));
+                            while (wo) {
+                                const int k = __builtin_ctz(wo);   /* wave-uniform: capsule k's joint frame */
+                                wo &= wo - 1u;
+                                const int src = row0 + k;
+                                M3 Rj;
+                                V3 oj;
+                                joint_frame(Rl, ol, kCapJ[k], Rj, oj);
+                                if (__shfl((int)have, src) == 0) continue;
+                                const V3 pak = v3(__shfl(pa.x, src), __shfl(pa.y, src), __shfl(pa.z, src));
+                                const V3 lak = mul_t(Rj, pak - oj);
+                                const V3 pbk = v3(__shfl(pb.x, src), __shfl(pb.y, src), __shfl(pb.z, src));
+                                const V3 nk = v3(__shfl(n.x, src), __shfl(n.y, src), __shfl(n.z, src));
+                                const float dk = __shfl(d, src);
+                                man_add_g(*Lp, es, 32 + 24 * k + 4 * o, lak, pbk, (-1.0f) * nk, dk, tau * tau);
+                            }
+                        }
+                    }
+                    if (__any(Lp->mcnt[es] > 0)) {
+                        sort_g1_by_depth(*Lp, es);
+                        man_refresh_insert_g<0, 1>(*Lp, es, c, Rl, ol, M3{{1, 0, 0, 0, 1, 0, 0, 0, 1}}, v3(0.0f, 0.0f, 0.0f),
+                                                   tau);
+                        sort_groups(*Lp, es);
+                    }
+                }
             }
         } else {
             PGX_PROF_MARK(20);
@@ -1715,7 +2020,24 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
             robot_table_contacts_g(e, m.contact_dist, *Lp, es, c);
             const uint64_t bn = __ballot(near);
             unsigned wm = (unsigned)((bn | (bn >> 16) | (bn >> 32) | (bn >> 48)) & 0xFFFFu);
-            if (wm) {
+            if constexpr (FULL) {
+                /* Bullet's persistent manifolds of the cube pairs: the near capsules' new points merged
+                 * into the pool in capsule order, the pool refreshed, its points the rows after the
+                 * table candidates (oracle detect(), the persistent branch) */
+                const unsigned rm = row_ballot(near);
+                wm = __builtin_amdgcn_readfirstlane(wm);
+                while (wm) {
+                    const int cn = __builtin_ctz(wm);
+                    wm &= wm - 1u;
+                    object_new_point_g(e, m.contact_dist, *Lp, es, ob, Rc, cn, c, ((rm >> cn) & 1u) != 0, Rl, ol);
+                }
+                if (__any(Lp->mcnt[es] > 0)) {
+                    sort_g1_by_depth(*Lp, es);
+                    man_refresh_insert_g<1, 0>(*Lp, es, c, Rl, ol, Rc, ob.p, m.contact_dist);
+                    sort_groups(*Lp, es);
+                }
+                PGX_PROF_MARK(21);
+            } else if (wm) {
                 const unsigned rm = row_ballot(near);
                 sort_g1_by_depth(*Lp, es);
                 wm = __builtin_amdgcn_readfirstlane(wm);
@@ -2345,6 +2667,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
      * PickAndPlace 16384: 2.93 -> 2.59 ms (profiles/r03/ab_lds_limit_rows.log). */
     constexpr bool LDS_LIM = OBJ;
     constexpr bool NO_PART = OBJ && PART == 2;
+    constexpr bool PERS = CONT && FULL && (OBJ || (AO && AO_PERS));   /* Bullet's persistent manifolds (the pool) */
     Dyn D;
     substep_dyn_g<OBJ, CONT, AO, FULL>(m, e, q, qd, ob, Lp, es, D, c, K, check);
     if constexpr (AO) {
@@ -2444,15 +2767,21 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         /* the points' records read up front, one batch behind one wait (read inside each point's
          * branch they cost a wait per point) */
         V3 gP[CG], gN[CG], gRb[CG];
-        int gJ[CG];
+        int gJ[CG], gW[CG];
         float gId[CG], gD[CG];
         auto read_point = [&](int k) __attribute__((always_inline)) {
             gP[k] = v3(L.g1p[k][0][es], L.g1p[k][1][es], L.g1p[k][2][es]);
             gN[k] = v3(L.g1n[k][0][es], L.g1n[k][1][es], L.g1n[k][2][es]);
             gRb[k] = OBJ ? v3(L.g1rb[k][0][es], L.g1rb[k][1][es], L.g1rb[k][2][es]) : v3(0.0f, 0.0f, 0.0f);
             gJ[k] = L.g1j[k][es];
+            gW[k] = PERS ? L.g1w[k][es] : -1;
             gId[k] = L.g1id[k][es];
             gD[k] = L.g1d[k][es];
+        };
+        /* a manifold point's warm start is its own applied impulse (btManifoldPoint::m_appliedImpulse
+         * x the warm-starting factor), a fresh table point's its feature's cached one */
+        auto warm_pt = [&](int w, float id) __attribute__((always_inline)) {
+            return (PERS && w >= 0) ? m.warmstart * L.mimp[w < 0 ? 0 : w][es] : warm_of(cid1, cim1, id);
         };
         /* (ReachAO: points are rare and the o2 kernel's registers scarce: read per point) */
         if (!AO && __any(n1 > 0)) {
@@ -2475,9 +2804,9 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 const V3 rb = gRb[k];
                 const int jl = gJ[k];
                 const float id = gId[k];
-                pmu[p] = point_mu<AO>(m, id);
+                pmu[p] = point_mu<AO, FULL>(m, id);
                 const bool vs_obj = OBJ && id >= kTableIdLimit;
-                const float warm = warm_of(cid1, cim1, id);
+                const float warm = warm_pt(gW[k], id);
                 V3 t1, t2;
                 plane_space(n, t1, t2);
                 const V3 Jv = (arm && c <= jl) ? cross(zc, P - oc) : v3(0, 0, 0);
@@ -2546,7 +2875,9 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 const int jl = L.g1j[k][es];
                 const float id = L.g1id[k][es];
                 const bool vs_obj = OBJ && id >= kTableIdLimit;
-                const float warm = warm_lookup<RB>(L, es, CACHE1, id, m.warmstart);
+                const int wk = PERS ? L.g1w[k][es] : -1;
+                const float warm = (PERS && wk >= 0) ? m.warmstart * L.mimp[wk < 0 ? 0 : wk][es]
+                                                     : warm_lookup<RB>(L, es, CACHE1, id, m.warmstart);
                 V3 t1, t2;
                 plane_space(n, t1, t2);
                 const V3 Jv = (arm && c <= jl) ? cross(zc, P - oc) : v3(0, 0, 0);
@@ -2588,7 +2919,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                     /* every lane of the env writes the same (row-uniform) values */
                     L.xrhs[xq][es] = (a ? rhs : 0.0f) * da;
                     L.xlam[xq][es] = L.xlam0[xq][es] = rok_n && dir == 0 ? lam * da : 0.0f;
-                    L.xfk[xq][es] = dir == 0 ? (rok ? 3.0e38f : 0.0f) : (rok ? point_mu<AO>(m, id) * jinv_n * da : 0.0f);
+                    L.xfk[xq][es] = dir == 0 ? (rok ? 3.0e38f : 0.0f) : (rok ? point_mu<AO, FULL>(m, id) * jinv_n * da : 0.0f);
                     L.xjinv[xq][es] = ja;
                 }
             }
@@ -3311,6 +3642,14 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 L.cache[CACHE1 + 2 * s + 1][es] = s < n1 ? L.xlam[xq][es] * L.xjinv[xq][es] : 0.0f;
             }
         }
+        if constexpr (PERS) {   /* the solved normal impulse back to its manifold point (writeBackContacts) */
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            for (int s = 0; s < RB; s++) {
+                if (!__any(s < n1)) break;
+                const int w = s < n1 ? L.g1w[s][es] : -1;
+                if (w >= 0) L.mimp[w][es] = L.cache[CACHE1 + 2 * s + 1][es];
+            }
+        }
     }
     if (OBJ) {
         const V3 dvl = v3(bcast16<7>(gv), bcast16<8>(gv), bcast16<9>(gv));
@@ -3913,6 +4252,25 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
 #pragma unroll
         for (int k = 0; k < CACHE_K; k++) L->cache[k][ln] = s.contacts[k * N + ii];
     }
+    /* Bullet's persistent manifolds (the wide FULL kernels of the object tasks and ReachAO): the
+     * pool, point p loaded by lane p of the env's row */
+    constexpr bool PERS = WIDE == 2 && CONT && (OBJ || (AO && AO_PERS));
+    if constexpr (PERS) {
+        const int mc = (int)s.man[ii];
+        L->mcnt[ln] = mc;
+        if (c < mc) {
+            const float* b = s.man + (size_t)(1 + PGX_MANIFOLD_POINT * c) * N + ii;
+            L->mkid[c][ln] = b[0];
+#pragma unroll
+            for (int t = 0; t < 3; t++) {
+                L->mla[c][t][ln] = b[(size_t)(1 + t) * N];
+                L->mlb[c][t][ln] = b[(size_t)(4 + t) * N];
+                L->mn[c][t][ln] = b[(size_t)(7 + t) * N];
+            }
+            L->md[c][ln] = b[(size_t)10 * N];
+            L->mimp[c][ln] = b[(size_t)11 * N];
+        }
+    }
     if constexpr (AO) ao_load(s, N, ii, *L, ln);
 
     /* Panda.set_action: clip to Box(-1,1) in float32 */
@@ -4087,6 +4445,26 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
 #pragma unroll
             for (int k = 0; k < CACHE_K; k++) L->cache[k][ln] = (k & 1) ? 0.0f : -1.0f;
         }
+        /* the reset teleports the bodies: Bullet's broadphase drops the pairs that no longer
+         * overlap and the next refresh any other point (oracle pgxo_vec_step / reset) */
+        if constexpr (PERS) L->mcnt[ln] = 0;
+    }
+    if constexpr (PERS) {   /* the pool back, point p by lane p */
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        const int mc = L->mcnt[ln];
+        if (lead) s.man[i] = (float)mc;
+        if (c < mc) {
+            float* b = s.man + (size_t)(1 + PGX_MANIFOLD_POINT * c) * N + i;
+            b[0] = L->mkid[c][ln];
+#pragma unroll
+            for (int t = 0; t < 3; t++) {
+                b[(size_t)(1 + t) * N] = L->mla[c][t][ln];
+                b[(size_t)(4 + t) * N] = L->mlb[c][t][ln];
+                b[(size_t)(7 + t) * N] = L->mn[c][t][ln];
+            }
+            b[(size_t)10 * N] = L->md[c][ln];
+            b[(size_t)11 * N] = L->mimp[c][ln];
+        }
     }
     const V3 ag2 = OBJ ? ob.p : pos;
     if (!lead) return;
@@ -4205,6 +4583,7 @@ __global__ __launch_bounds__(64) void reset_kernel(const PgxDevModel* __restrict
     if constexpr (AO) ao_store(s, N, i, *L, ln);
 #pragma unroll
     for (int k = 0; k < CACHE_N; k++) s.contacts[k * N + i] = (k & 1) ? 0.0f : -1.0f;
+    if (s.man) s.man[i] = 0.0f;   /* the persistent manifold pool: empty after a reset */
     s.elapsed[i] = 0;
     s.episode[i] = episode;
 }

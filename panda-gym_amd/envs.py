@@ -322,6 +322,10 @@ class PandaVecEnv:
             "elapsed": _view(v.elapsed, (n,), torch.int32, self.device),
             "episode": _view(v.episode, (n,), torch.int32, self.device),
             "errors": _view(v.errors, (1,), torch.int32, self.device),
+            # Bullet's persistent manifolds (pgx.h PGX_MANIFOLD_POOL): count, then per point kid, local A,
+            # local B, normal, distance, impulse
+            **({"manifolds": _view(v.manifolds, (1 + v.manifold_pool * abi.MANIFOLD_POINT, n), torch.float32,
+                                   self.device)} if v.manifolds else {}),
             # not state: the env order of the last sorted step launch (heavy-first)
             **({"env_order": _view(v.env_order, (n,), torch.int32, self.device)} if v.env_order else {}),
         }

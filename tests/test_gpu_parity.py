@@ -40,6 +40,9 @@ def _state_to_oracle(venv, ref):
     orc.set_contact_cache(ref.obj, st["contacts"].double().cpu().numpy().T)
     if "obstacles" in st:
         ref.obj[:, orc.OBJ_AO:orc.OBJ_AO + 24] = st["obstacles"].double().cpu().numpy().T
+    # Bullet's persistent manifolds (the per-pair budget's object / ReachAO kernels)
+    orc.set_manifolds(ref.obj, st["manifolds"].double().cpu().numpy().T if "manifolds" in st
+                      else np.zeros((ref.obj.shape[0], 1)))
 
 
 def _check_step(out_gpu, out_ref, goal):

@@ -21,6 +21,10 @@ import json, os, sys
 import numpy as np
 import torch
 sys.path.insert(0, os.getcwd())
+import ctypes
+from panda_gym_amd import _native
+_l = ctypes.CDLL(sys.argv[1])   # an older build may lack newer exports: check the ones it has
+_native.EXPORTS = [x for x in _native.EXPORTS if hasattr(_l, x)]
 import panda_gym_amd as pg
 lib, env_id, lanes, steps, drive = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5] == "1"
 n = 64
@@ -56,9 +60,12 @@ CASES = [("PandaReach-v3", 1, 3, True), ("PandaReach-v3", 1, 20, False), ("Panda
 
 
 def main():
+    cases = CASES
+    if os.environ.get("PROBE_CASES"):   # e.g. PROBE_CASES=0,0,0: case indices, repeats allowed
+        cases = [CASES[int(k)] for k in os.environ["PROBE_CASES"].split(",")]
     for lib in sys.argv[1:]:
         path = os.path.abspath(lib)
-        for env_id, lanes, steps, drive in CASES:
+        for env_id, lanes, steps, drive in cases:
             out = subprocess.run([sys.executable, "-c", CHILD, path, env_id, str(lanes), str(steps), "1" if drive else "0"],
                                  capture_output=True, text=True, cwd=ROOT, timeout=240)
             lines = [ln for ln in out.stdout.splitlines() if ln.strip()]

@@ -17,10 +17,16 @@ if [ -n "$PROBE" ]; then
   tail -60 gpurun_out/probe_$TAG.log
   if [ $rc -ne 0 ]; then exit $rc; fi
 fi
+if [ -n "$REPRO" ]; then   # the round-4 sort's graph fault, restated (tools/repro_sort_graph.hip)
+  timeout -k 10 120 tools/repro_sort_graph 96 > gpurun_out/repro_sort_$TAG.log 2>&1
+  rc=$?
+  cat gpurun_out/repro_sort_$TAG.log
+  if [ $rc -ne 0 ]; then exit $rc; fi
+fi
 if [ -z "$NO_TESTS" ]; then
   # assertion failures (pytest rc 1) do not stop the timing steps below; anything else (a crash,
   # an abort, a time limit) ends the script here
-  timeout -k 10 900 python -u -m pytest tests -v -m gpu --timeout 240 --timeout-method thread ${PGX_PYTEST_ARGS} > gpurun_out/pytest_gpu_$TAG.log 2>&1
+  timeout -k 10 900 python -u -m pytest ${PGX_TESTS:-tests} -v -m gpu --timeout 240 --timeout-method thread ${PGX_PYTEST_ARGS} > gpurun_out/pytest_gpu_$TAG.log 2>&1
   TEST_RC=$?
   grep -E "FAILED|ERROR" gpurun_out/pytest_gpu_$TAG.log | head -40
   tail -3 gpurun_out/pytest_gpu_$TAG.log

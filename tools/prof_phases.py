@@ -22,7 +22,11 @@ def run(env_id, n, contacts, launches=100, warm=26):
     buf = (C.c_ulonglong * 24)()
     kw = json.loads(os.environ.get("PH_KW", "{}"))   # e.g. PH_KW='{"full_manifold": true}'
     venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=0, contacts=contacts, **kw)
-    venv.reset_tensors()
+    if os.environ.get("PH_STAGGER"):   # the bench's steady state: staggered episode phases, one episode in
+        venv.reset_tensors(episode_phase="staggered")
+        warm = max(warm, venv.spec.max_episode_steps + 5)
+    else:
+        venv.reset_tensors()
     for t in range(warm):
         venv.step_tensors(venv.sample_actions(t))
     torch.cuda.synchronize()
