@@ -244,6 +244,11 @@ typedef struct pgx_config {
     int32_t terminate_on_success; /* RobotTaskEnv(terminate_on_success): 1 for ReachAO */
     int32_t pad3;
     double collision_reward;      /* -100: added to the sparse reward on collision */
+    double ao_ee_neutral[3];      /* ReachAO: the EE (panda_ee COM) at the neutral pose, fp64 -- the
+                                     reset sampler's obstacle centre (reach_ao.py:635-644, the
+                                     get_ee_position it reads after Panda.reset) and its goal
+                                     fallback, a model constant computed once on the host; all zero:
+                                     the kernel's own fp32 FK of that pose */
 } pgx_config;
 
 typedef struct pgx_env* pgx_handle;
@@ -357,17 +362,19 @@ int pgx_release(pgx_handle h, int32_t state_id);
  * seeded reset drawn on the device, no host injection).  RobotTaskEnv.reset reseeds the task's
  * generator on EVERY reset, task.np_random = seeding.np_random(seed) (core.py:302): a reset with
  * seed s draws from PCG64(SeedSequence(s)), which is what a record set from s reproduces bit for bit
- * (goal / object in the task's order, reach.py:75-78, push.py:75-87, pick_and_place.py:71-85).  A
- * reset without a seed -- the step's auto-reset included -- gets a fresh OS-entropy generator in the
- * reference, so no reference value exists for it: here it continues stream i, a reproducible
- * stand-in with the same distribution, not the reference's draws.  states: [N][4] uint64 per env
- * {state_lo, state_hi, inc_lo, inc_hi} of numpy's PCG64 (bit_generator.state["state"]), host or
- * device memory, copied on `stream`; NULL returns to Philox.  The mode is a device word switched on
- * `stream` and the stream buffer lives as long as the handle, so a step loop captured in a HIP graph
- * draws in the mode of replay time.  An injected reset leaves its env's stream untouched.  Streams
- * are not part of the saved state (restoreState keeps np_random as it is).  ReachAO:
- * PGX_E_UNSUPPORTED.  pgx_get_rng_streams copies the current records out ([N][4], host or device
- * memory). */
+ * (goal / object in the task's order, reach.py:75-78, push.py:75-87, pick_and_place.py:71-85;
+ * ReachAO's rejection sampler, reach_ao.py:965-1082, with Generator.uniform / random / integers /
+ * shuffle as numpy draws them).  A reset without a seed -- the step's auto-reset included -- gets a
+ * fresh OS-entropy generator in the reference, so no reference value exists for it: here it
+ * continues stream i, a reproducible stand-in with the same distribution, not the reference's
+ * draws.  states: [N][PGX_PCG64_WORDS] uint64 per env {state_lo, state_hi, inc_lo, inc_hi,
+ * has_uint32, uinteger} -- numpy's PCG64 bit_generator.state -- host or device memory, copied on
+ * `stream`; NULL returns to Philox.  The mode is a device word switched on `stream` and the stream
+ * buffer lives as long as the handle, so a step loop captured in a HIP graph draws in the mode of
+ * replay time.  An injected reset leaves its env's stream untouched.  Streams are not part of the
+ * saved state (restoreState keeps np_random as it is).  pgx_get_rng_streams copies the current
+ * records out (same layout, host or device memory). */
+#define PGX_PCG64_WORDS 6
 int pgx_set_rng_streams(pgx_handle h, const uint64_t* states, void* stream);
 int pgx_get_rng_streams(pgx_handle h, uint64_t* states, void* stream);
 

@@ -26,6 +26,7 @@ CONTACTS_FULL = 2             # PGX_CONTACTS_FULL: pgx_config.contacts for the f
 MANIFOLD_POOL = 16            # PGX_MANIFOLD_POOL: persistent manifold points per env (Push / PickAndPlace)
 MANIFOLD_POOL_AO = 8          # PGX_MANIFOLD_POOL_AO: ReachAO
 MANIFOLD_POINT = 12           # PGX_MANIFOLD_POINT: kid, local A[3], local B[3], normal[3], distance, impulse
+PCG64_WORDS = 6               # PGX_PCG64_WORDS: state_lo, state_hi, inc_lo, inc_hi, has_uint32, uinteger
 CAP_VS_TABLE, CAP_VS_OBJECT = 1, 2
 
 TASK_REACH, TASK_PUSH, TASK_PICK_AND_PLACE, TASK_REACH_AO = 0, 1, 2, 3
@@ -95,6 +96,7 @@ class PgxConfig(C.Structure):
         ("object_half", C.c_double), ("object_mass", C.c_double), ("object_inertia", C.c_double),
         ("table_center", C.c_double * 3), ("table_half", C.c_double * 3), ("plane_z", C.c_double),
         ("terminate_on_success", C.c_int32), ("pad3", C.c_int32), ("collision_reward", C.c_double),
+        ("ao_ee_neutral", C.c_double * 3),
     ]
 
 

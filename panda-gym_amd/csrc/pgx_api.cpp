@@ -74,7 +74,7 @@ struct pgx_env {
     size_t blob_bytes;
     /* device snapshots by id (pgx_snapshot): slot i holds state id i, nullptr = free */
     std::vector<void*> snaps;
-    /* [N][4] numpy PCG64 streams of the reset draws (pgx_set_rng_streams) and, after them, the
+    /* [N][PGX_PCG64_WORDS] numpy PCG64 streams of the reset draws (pgx_set_rng_streams) and, after them, the
      * device mode word (PgxDevEnv.pcg_on): allocated by pgx_create, freed by pgx_destroy, so a
      * graph captured in either mode never reads freed memory */
     uint64_t* pcg = nullptr;
@@ -403,6 +403,8 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     e.terminate_on_success = cfg->terminate_on_success ? 1 : 0;
     e.no_auto_reset = cfg->no_auto_reset ? 1 : 0;
     e.collision_reward = cfg->collision_reward;
+    for (int k = 0; k < 3; k++) e.ao_ee[k] = cfg->ao_ee_neutral[k];
+    e.ao_ee_set = (cfg->ao_ee_neutral[0] != 0.0 || cfg->ao_ee_neutral[1] != 0.0 || cfg->ao_ee_neutral[2] != 0.0) ? 1 : 0;
     /* Step layout (pgx_kernels.hip): 16 lanes per env (4096 x 16 lanes = 1024 waves = one per
      * SIMD; beyond, several per SIMD) or one lane per env.  Round 1 measured the one-lane layout
      * ahead at 16384 envs (profiles/r01/time_layouts_v11.json: 1.33 vs 2.27 ms Reach, 3.54 vs
@@ -473,7 +475,7 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     h->dm_dev = (PgxDevModel*)b;
     /* the PCG64 reset streams and their mode word: not part of the saved state (restoreState leaves
      * np_random alone), so outside the blob */
-    const size_t pcg_bytes = align(32 * N);
+    const size_t pcg_bytes = align(8 * PGX_PCG64_WORDS * N);
     rc = hip_check(hipMalloc((void**)&h->pcg, pcg_bytes + 256), "hipMalloc(rng streams)");
     if (rc) { h->pcg = nullptr; (void)hipFree(h->blob); delete h; return rc; }
     e.pcg = h->pcg;
@@ -649,14 +651,13 @@ int pgx_release(pgx_handle h, int32_t state_id) {
  * restated, refused. */
 int pgx_set_rng_streams(pgx_handle h, const uint64_t* states, void* stream) {
     if (!h) return fail(PGX_E_INVALID, "null handle");
-    if (h->de.ao && states) return fail(PGX_E_UNSUPPORTED, "PCG64 reset streams: ReachAO's reset draws are not restated");
     int rc = hip_check(hipSetDevice(h->device), "hipSetDevice");
     if (rc) return rc;
     int32_t* on = const_cast<int32_t*>(h->de.pcg_on);
     if (states)
-        rc = hip_check(hipMemcpyAsync(h->pcg, states, 32 * (size_t)h->de.n_envs, hipMemcpyDefault, (hipStream_t)stream),
+        rc = hip_check(hipMemcpyAsync(h->pcg, states, 8 * PGX_PCG64_WORDS * (size_t)h->de.n_envs, hipMemcpyDefault, (hipStream_t)stream),
                        "rng streams copy");
-    if (!rc) rc = hip_check(hipMemsetD32Async((hipDeviceptr_t)on, states ? 1 : 0, 1, (hipStream_t)stream), "rng mode word");
+    if (!rc) rc = hip_check((hipError_t)pgx_launch_set_word(on, states ? 1 : 0, stream), "rng mode word");
     if (!rc) h->pcg_set = states != nullptr;
     return rc;
 }
@@ -664,7 +665,7 @@ int pgx_set_rng_streams(pgx_handle h, const uint64_t* states, void* stream) {
 int pgx_get_rng_streams(pgx_handle h, uint64_t* states, void* stream) {
     if (!h || !states) return fail(PGX_E_INVALID, "null argument");
     if (!h->pcg_set) return fail(PGX_E_INVALID, "no PCG64 reset streams set (pgx_set_rng_streams)");
-    return hip_check(hipMemcpyAsync(states, h->pcg, 32 * (size_t)h->de.n_envs, hipMemcpyDefault, (hipStream_t)stream),
+    return hip_check(hipMemcpyAsync(states, h->pcg, 8 * PGX_PCG64_WORDS * (size_t)h->de.n_envs, hipMemcpyDefault, (hipStream_t)stream),
                      "rng streams copy");
 }
 

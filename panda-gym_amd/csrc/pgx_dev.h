@@ -63,6 +63,8 @@ struct PgxDevEnv {
     int32_t terminate_on_success;
     int32_t no_auto_reset;         /* pgx_config.no_auto_reset: finished envs keep their state */
     double collision_reward;
+    double ao_ee[3];               /* pgx_config.ao_ee_neutral: the reset sampler's EE centre, fp64 */
+    int32_t ao_ee_set;             /* 0: the kernel's fp32 FK of the neutral pose instead */
     int32_t lanes_per_env;         /* step layout: 1 (env per lane) or 16 (env per DPP row) */
     int32_t pgs_mode;              /* test hook (PGX_PGS_MODE): 0 auto, 2 never speculate on the limit
                                       rows, 3 always redo the speculative solve with them */
@@ -70,7 +72,7 @@ struct PgxDevEnv {
     int32_t full_manifold;         /* contacts == PGX_CONTACTS_FULL: robot budget PGX_ROBOT_POINTS(_ARM) */
     int32_t wave_mode;             /* A/B hook (PGX_WAVES_PER_SIMD): 0 auto (two resident waves per SIMD
                                       beyond 1024 waves), 1 the one-wave build, 2 the two-wave build */
-    uint64_t* pcg;                 /* [N][4] numpy PCG64 streams of the reset draws (pgx_set_rng_streams),
+    uint64_t* pcg;                 /* [N][PGX_PCG64_WORDS] numpy PCG64 streams of the reset draws (pgx_set_rng_streams),
                                       allocated with the handle and freed with it */
     const int32_t* pcg_on;         /* device word: 1 = resets draw from pcg, 0 = the Philox counter.  In
                                       device memory and switched on the caller's stream, so a step loop
@@ -122,5 +124,6 @@ int pgx_launch_step(const PgxDevModel* m_device, const PgxDevEnv& e, const PgxDe
 int pgx_launch_reset(const PgxDevModel* m_device, const PgxDevEnv& e, const PgxDevState& s, const uint8_t* mask,
                      const double* inject_goal, const double* inject_object, const PgxDevOut& o, void* stream);
 int pgx_launch_sample_actions(const PgxDevEnv& e, float* action, uint64_t step, void* stream);
+int pgx_launch_set_word(int32_t* p, int32_t v, void* stream);
 int pgx_launch_compute_reward(const float* ag, const float* dg, int64_t n, int32_t reward_type, double thr,
                               float* out, void* stream);

@@ -1131,29 +1131,31 @@ __device__ __forceinline__ int man_capsule(int key) { return AO ? (key - 32) / 2
  * replaced, impulse kept; else appended below 4 points (dropped when the pool is full); else
  * sortCachedPoints' slot overwritten, impulse 0 */
 template <class LT>
-__device__ __forceinline__ void man_add_g(LT& L, int es, int key, V3 la, V3 lb, V3 n, float d, float thr2) {
+__device__ __forceinline__ void man_add_g(LT& L, int es, int c, int key, V3 la, V3 lb, V3 n, float d, float thr2) {
     constexpr int MP = LT::MP;
     const int cnt = L.mcnt[es];
-    int i0 = 0, i1 = 0, i2 = 0, i3 = 0, nk = 0;
-    for (int i = 0; i < cnt; i++) {   /* the manifold's points by slot */
-        const int kid = (int)L.mkid[i][es];
-        if ((kid & ~3) == key) {
-            const int sl = kid & 3;
-            i0 = sl == 0 ? i : i0; i1 = sl == 1 ? i : i1; i2 = sl == 2 ? i : i2; i3 = sl == 3 ? i : i3;
-            nk++;
-        }
+    /* lane p of the row looks at pool point p: the manifold's points by slot from the row's ballots */
+    const int p = c < cnt ? c : 0;
+    const int kidp = (int)L.mkid[p][es];
+    const bool match = c < cnt && (kidp & ~3) == key;
+    const V3 lap = lds3(L.mla[p], es);
+    const float dp = L.md[p][es];
+    const V3 e = lap - la;
+    const float ddp = dot(e, e);
+    const int row0 = (int)(threadIdx.x & ~(unsigned)(GW - 1));
+    int idx[4], nk = 0;
+#pragma unroll
+    for (int sl = 0; sl < 4; sl++) {
+        const unsigned m = row_ballot(match && (kidp & 3) == sl);
+        idx[sl] = m ? __builtin_ctz(m) : 0;
+        nk += m ? 1 : 0;
     }
-    const int idx[4] = {i0, i1, i2, i3};
-    V3 cla[4];
-    float cd[4];
+    /* getCacheEntry: the nearest in slot order, strictly within thr^2 */
     int near = -1;
     float sh = thr2;
 #pragma unroll
     for (int sl = 0; sl < 4; sl++) {
-        cla[sl] = lds3(L.mla[idx[sl]], es);
-        cd[sl] = L.md[idx[sl]][es];
-        const V3 e = cla[sl] - la;
-        const float dd = dot(e, e);
+        const float dd = __shfl(ddp, row0 + idx[sl]);
         if (sl < nk && dd < sh) { sh = dd; near = sl; }
     }
     int at;
@@ -1167,6 +1169,14 @@ __device__ __forceinline__ void man_add_g(LT& L, int es, int key, V3 la, V3 lb, 
         L.mimp[at][es] = 0.0f;
         L.mcnt[es] = cnt + 1;
     } else {   /* sortCachedPoints: keep the deepest, else the largest area */
+        V3 cla[4];
+        float cd[4];
+#pragma unroll
+        for (int sl = 0; sl < 4; sl++) {
+            const int src = row0 + idx[sl];
+            cla[sl] = v3(__shfl(lap.x, src), __shfl(lap.y, src), __shfl(lap.z, src));
+            cd[sl] = __shfl(dp, src);
+        }
         int maxi = -1;
         float maxpen = d;
 #pragma unroll
@@ -1268,9 +1278,34 @@ __device__ __forceinline__ void man_refresh_insert_g(LT& L, int es, int c, const
     } else if (mine) {
         L.md[p][es] = d;
     }
-    /* the manifold points as rows, in pool order (after the table candidates already in the list) */
+    /* the manifold points as rows.  With room for every point (the common case) each kept lane
+     * writes its row straight to its id-ordered slot after the table candidates (their ids are
+     * below 32, every manifold id above): its rank among the env's kept ids by row broadcasts.
+     * Otherwise the budget's deepest by (depth, discovery), as g1_insert keeps them: the table
+     * candidates first, then the points in pool order, then id order (oracle select_points). */
     const V3 rb = pb - op;
     const int nkeep = __builtin_popcount(km);
+    const int nt = L.cnt[1][es];
+    const float kf = (float)kidn;
+    int rank = 0;
+    sfor<0, 16>([&](auto uc) __attribute__((always_inline)) {
+        constexpr int U = decltype(uc)::value;
+        const float ku = bcast16<U>(kf);
+        rank += (((km >> U) & 1u) && ku < kf) ? 1 : 0;
+    });
+    if (nt + nkeep <= LT::RB) {
+        if (newp >= 0) {
+            const int sl = nt + rank;
+            L.g1d[sl][es] = d; L.g1id[sl][es] = kf; L.g1j[sl][es] = j; L.g1w[sl][es] = newp;
+            L.g1p[sl][0][es] = pa.x; L.g1p[sl][1][es] = pa.y; L.g1p[sl][2][es] = pa.z;
+            L.g1n[sl][0][es] = n.x; L.g1n[sl][1][es] = n.y; L.g1n[sl][2][es] = n.z;
+            const V3 r0 = OBJ ? rb : v3(0.0f, 0.0f, 0.0f);
+            L.g1rb[sl][0][es] = r0.x; L.g1rb[sl][1][es] = r0.y; L.g1rb[sl][2][es] = r0.z;
+        }
+        L.cnt[1][es] = nt + nkeep;
+        return;
+    }
+    sort_g1_by_depth(L, es);
     for (int t = 0; t < GW; t++) {
         if (!__any(t < nkeep)) break;
         /* the lane holding new pool index t: the t-th set bit of km */
@@ -1280,11 +1315,12 @@ __device__ __forceinline__ void man_refresh_insert_g(LT& L, int es, int c, const
         const float dt = __shfl(d, src);
         const int kidt = __shfl(kidn, src);
         const V3 pt = v3(__shfl(pa.x, src), __shfl(pa.y, src), __shfl(pa.z, src));
-        const V3 nt = v3(__shfl(n.x, src), __shfl(n.y, src), __shfl(n.z, src));
+        const V3 nt2 = v3(__shfl(n.x, src), __shfl(n.y, src), __shfl(n.z, src));
         const V3 rt = v3(__shfl(rb.x, src), __shfl(rb.y, src), __shfl(rb.z, src));
         const int jt = __shfl(j, src);
-        if (t < nkeep) g1_insert(L, es, dt, (float)kidt, jt, pt, nt, OBJ ? rt : v3(0.0f, 0.0f, 0.0f), t);
+        if (t < nkeep) g1_insert(L, es, dt, (float)kidt, jt, pt, nt2, OBJ ? rt : v3(0.0f, 0.0f, 0.0f), t);
     }
+    sort_groups(L, es);
 }
 
 /* Bullet's persistent manifold of capsule cn (wave-uniform) and the cube (FULL kernels): lane s of
@@ -1345,7 +1381,7 @@ __device__ __forceinline__ void object_new_point_g(const PgxDevEnv& e, float tau
     const V3 nk = v3(__shfl(n.x, src), __shfl(n.y, src), __shfl(n.z, src));
     const V3 qk = v3(__shfl(qb.x, src), __shfl(qb.y, src), __shfl(qb.z, src));
     const float dk = __shfl(depth, src);
-    if (bm) man_add_g(L, es, 32 + 16 * cn, mul_t(Rj, pk - oj), qk, nk, dk, tau * tau);
+    if (bm) man_add_g(L, es, c, 32 + 16 * cn, mul_t(Rj, pk - oj), qk, nk, dk, tau * tau);
 }
 
 /* ReachAO: the obstacles are static colliders (create_obstacle_sphere / _cuboid,
@@ -1904,6 +1940,9 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                     if (lb <= 0.0f) hit = capsule_box_hit(A, B, r, tc, th);
                 }
                 unsigned cmask = 0;   /* FULL: this lane's candidate obstacles */
+                int o1 = -1;          /* FULL: the first of them, its point kept (the rest recomputed) */
+                V3 pa1 = v3(0.0f, 0.0f, 0.0f), pb1 = pa1, n1v = pa1;
+                float d1 = 0.0f;
                 V3 Cs[AO_N];   /* the obstacle centres, one LDS batch */
 #pragma unroll
                 for (int o = 0; o < AO_N; o++) Cs[o] = lds3(Lp->aoC[o], es);
@@ -1924,6 +1963,13 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                     const bool cand = cap_on && d < tau;
                     if constexpr (FULL && AO_PERS) {   /* the manifolds take the new points after the collision check */
                         cmask |= cand ? (1u << o) : 0u;
+                        if (cand && o1 < 0) {
+                            o1 = o;
+                            pa1 = P + r * n;
+                            pb1 = pa1 + d * n;
+                            n1v = n;
+                            d1 = d;
+                        }
                         continue;
                     }
                     const uint64_t bm = __ballot(cand);
@@ -1956,18 +2002,19 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                             const bool have = (cmask >> o) & 1u;
                             const uint64_t bo = __ballot(have);
                             if (bo == 0) continue;
-                            const V3 C = lds3(Lp->aoC[o], es);
-                            V3 P = seg_closest(A, B, C);
-                            const V3 v = C - P;
-                            const float len = norm(v);
-                            V3 n = len > 0.0f ? fast_rcp(len) * v : v3(0.0f, 0.0f, 1.0f);
-                            float d = 3.0e38f;
-                            if (have) {
+                            V3 pa = pa1, pb = pb1, n = n1v;   /* pa on the capsule, towards the obstacle; pb on it */
+                            float d = d1;
+                            if (have && o != o1) {   /* a second candidate of this capsule: the pair again */
+                                const V3 C = lds3(Lp->aoC[o], es);
+                                V3 P = seg_closest(A, B, C);
+                                const V3 v = C - P;
+                                const float len = norm(v);
+                                n = len > 0.0f ? fast_rcp(len) * v : v3(0.0f, 0.0f, 1.0f);
                                 if (o < 3) d = len - r - kAoSize;
                                 else d = capsule_box_pair<true>(A, B, r, C, hcube, &P, &n);
+                                pa = P + r * n;
+                                pb = pa + d * n;   /* (static obstacle: local = world) */
                             }
-                            const V3 pa = P + r * n;        /* on the capsule, towards the obstacle */
-                            const V3 pb = pa + d * n;       /* on the obstacle (static: local = world) */
                             unsigned wo = __builtin_amdgcn_readfirstlane(
                                 (unsigned)((bo | (bo >> 16) | (bo >> 32) | (bo >> 48)) & 0xFFFFu));
                             while (wo) {
@@ -1983,16 +2030,13 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                                 const V3 pbk = v3(__shfl(pb.x, src), __shfl(pb.y, src), __shfl(pb.z, src));
                                 const V3 nk = v3(__shfl(n.x, src), __shfl(n.y, src), __shfl(n.z, src));
                                 const float dk = __shfl(d, src);
-                                man_add_g(*Lp, es, 32 + 24 * k + 4 * o, lak, pbk, (-1.0f) * nk, dk, tau * tau);
+                                man_add_g(*Lp, es, c, 32 + 24 * k + 4 * o, lak, pbk, (-1.0f) * nk, dk, tau * tau);
                             }
                         }
                     }
-                    if (__any(Lp->mcnt[es] > 0)) {
-                        sort_g1_by_depth(*Lp, es);
+                    if (__any(Lp->mcnt[es] > 0))
                         man_refresh_insert_g<0, 1>(*Lp, es, c, Rl, ol, M3{{1, 0, 0, 0, 1, 0, 0, 0, 1}}, v3(0.0f, 0.0f, 0.0f),
                                                    tau);
-                        sort_groups(*Lp, es);
-                    }
                 }
             }
         } else {
@@ -2031,11 +2075,7 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                     wm &= wm - 1u;
                     object_new_point_g(e, m.contact_dist, *Lp, es, ob, Rc, cn, c, ((rm >> cn) & 1u) != 0, Rl, ol);
                 }
-                if (__any(Lp->mcnt[es] > 0)) {
-                    sort_g1_by_depth(*Lp, es);
-                    man_refresh_insert_g<1, 0>(*Lp, es, c, Rl, ol, Rc, ob.p, m.contact_dist);
-                    sort_groups(*Lp, es);
-                }
+                if (__any(Lp->mcnt[es] > 0)) man_refresh_insert_g<1, 0>(*Lp, es, c, Rl, ol, Rc, ob.p, m.contact_dist);
                 PGX_PROF_MARK(21);
             } else if (wm) {
                 const unsigned rm = row_ballot(near);
@@ -3642,12 +3682,14 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 L.cache[CACHE1 + 2 * s + 1][es] = s < n1 ? L.xlam[xq][es] * L.xjinv[xq][es] : 0.0f;
             }
         }
-        if constexpr (PERS) {   /* the solved normal impulse back to its manifold point (writeBackContacts) */
+        if constexpr (PERS) {   /* the solved normal impulse back to its manifold point (writeBackContacts):
+                                 * lane c takes slot c (each point feeds one slot, so no two lanes write
+                                 * the same word) */
+            static_assert(RB <= GW, "one lane per robot slot");
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            for (int s = 0; s < RB; s++) {
-                if (!__any(s < n1)) break;
-                const int w = s < n1 ? L.g1w[s][es] : -1;
-                if (w >= 0) L.mimp[w][es] = L.cache[CACHE1 + 2 * s + 1][es];
+            if (c < n1) {
+                const int w = L.g1w[c][es];
+                if (w >= 0) L.mimp[w][es] = L.cache[CACHE1 + 2 * c + 1][es];
             }
         }
     }
@@ -3706,11 +3748,22 @@ __device__ __forceinline__ double reset_uniform(const PgxDevEnv& e, uint64_t env
 /* numpy's PCG64 (XSL-RR 128/64, the generator gymnasium's seeding.np_random builds,
  * core.py:302): state <- state * M + inc (mod 2^128), then the output of the new state:
  * rotr64(hi ^ lo, hi >> 58).  next_double = (u >> 11) * 2^-53 as in the reset draws above.
- * Record per env (pgx_set_rng_streams): state_lo, state_hi, inc_lo, inc_hi. */
+ * next_uint32 (numpy pcg64_next32) hands out a 64-bit output's low half and keeps the high half
+ * for the next call (has_uint32 / uinteger); next_uint64 and next_double leave that half alone.
+ * numpy leaves a spent uinteger in its state; the record holds 0 there (pcg64_record does too).
+ * Record per env (pgx_set_rng_streams, PGX_PCG64_WORDS): state_lo, state_hi, inc_lo, inc_hi,
+ * has_uint32, uinteger -- numpy's bit_generator.state. */
 struct Pcg64 {
     uint64_t lo, hi, ilo, ihi;
+    uint32_t has, u32;
 };
-__device__ __forceinline__ double pcg64_next_double(Pcg64& g) {
+__device__ __forceinline__ Pcg64 pcg64_load(const uint64_t* r) {
+    return Pcg64{r[0], r[1], r[2], r[3], (uint32_t)r[4], (uint32_t)r[5]};
+}
+__device__ __forceinline__ void pcg64_store(const Pcg64& g, uint64_t* r) {
+    r[0] = g.lo; r[1] = g.hi; r[2] = g.ilo; r[3] = g.ihi; r[4] = g.has; r[5] = g.u32;
+}
+__device__ __forceinline__ uint64_t pcg64_next64(Pcg64& g) {
     constexpr uint64_t MLO = 0x4385DF649FCCF645ull, MHI = 0x2360ED051FC65DA4ull;
     const uint64_t plo = g.lo * MLO;
     uint64_t hi = __umul64hi(g.lo, MLO) + g.lo * MHI + g.hi * MLO;
@@ -3720,8 +3773,46 @@ __device__ __forceinline__ double pcg64_next_double(Pcg64& g) {
     g.hi = hi;
     const uint64_t x = hi ^ lo;
     const uint32_t rot = (uint32_t)(hi >> 58);
-    const uint64_t u = (x >> rot) | (x << ((64u - rot) & 63u));
-    return (double)(u >> 11) * (1.0 / 9007199254740992.0);
+    return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+__device__ __forceinline__ double pcg64_next_double(Pcg64& g) {
+    return (double)(pcg64_next64(g) >> 11) * (1.0 / 9007199254740992.0);
+}
+__device__ __forceinline__ uint32_t pcg64_next32(Pcg64& g) {
+    if (g.has) {   /* (the spent half is cleared: a record's uinteger is 0 unless has_uint32) */
+        const uint32_t v = g.u32;
+        g.has = 0;
+        g.u32 = 0;
+        return v;
+    }
+    const uint64_t n = pcg64_next64(g);
+    g.has = 1;
+    g.u32 = (uint32_t)(n >> 32);
+    return (uint32_t)n;
+}
+/* Generator.integers(off, off + rng + 1) for rng < 2^32 - 1 (int64 default: Lemire's bounded
+ * draw on next_uint32, numpy buffered_bounded_lemire_uint32) */
+__device__ __forceinline__ uint32_t pcg64_bounded(Pcg64& g, uint32_t rng) {
+    const uint32_t excl = rng + 1u;
+    uint64_t m = (uint64_t)pcg64_next32(g) * excl;
+    uint32_t left = (uint32_t)m;
+    if (left < excl) {
+        const uint32_t thr = (0xFFFFFFFFu - rng) % excl;
+        while (left < thr) {
+            m = (uint64_t)pcg64_next32(g) * excl;
+            left = (uint32_t)m;
+        }
+    }
+    return (uint32_t)(m >> 32);
+}
+/* random_interval(max) for max < 2^32 (Generator.shuffle of a list): masked rejection on next_uint32 */
+__device__ __forceinline__ uint32_t pcg64_interval(Pcg64& g, uint32_t max) {
+    if (max == 0) return 0;
+    uint32_t mask = max;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    uint32_t v;
+    while ((v = (pcg64_next32(g) & mask)) > max) {}
+    return v;
 }
 
 /* --------------------------------------------------------- env epilogue */
@@ -3786,11 +3877,8 @@ __device__ __forceinline__ void reset_env(MRef m, const PgxDevEnv& e, int i, uin
     /* the draw source: the env's numpy PCG64 stream (pgx_set_rng_streams) advanced in draw order,
      * or the Philox counter (env, episode, draw index) */
     const bool pcg = e.pcg_on != nullptr && *e.pcg_on != 0;
-    Pcg64 g{0, 0, 0, 0};
-    if (pcg) {
-        const uint64_t* r = e.pcg + 4 * (size_t)i;
-        g = Pcg64{r[0], r[1], r[2], r[3]};
-    }
+    Pcg64 g{0, 0, 0, 0, 0, 0};
+    if (pcg) g = pcg64_load(e.pcg + PGX_PCG64_WORDS * (size_t)i);
     auto draw = [&](int k) -> double { return pcg ? pcg64_next_double(g) : reset_uniform(e, env, episode, k); };
     double noise[3];
 #pragma unroll
@@ -3813,10 +3901,7 @@ __device__ __forceinline__ void reset_env(MRef m, const PgxDevEnv& e, int i, uin
         ob.qx = 0.0f; ob.qy = 0.0f; ob.qz = 0.0f; ob.qw = 1.0f;
     }
     /* an injected reset replaces the task's draws: its stream stays where it was */
-    if (pcg && lead && !inject && !inject_obj) {
-        uint64_t* r = e.pcg + 4 * (size_t)i;
-        r[0] = g.lo; r[1] = g.hi; r[2] = g.ilo; r[3] = g.ihi;
-    }
+    if (pcg && lead && !inject && !inject_obj) pcg64_store(g, e.pcg + PGX_PCG64_WORDS * (size_t)i);
     episode += 1;
 }
 
@@ -4068,12 +4153,17 @@ __device__ __noinline__ bool ao_robot_hit(LT& L, int ln, int lane, int kind, V3 
     }
 }
 
+/* the reset's draw source: the env's numpy PCG64 stream (g, pgx_set_rng_streams) or the Philox
+ * counter (env, episode, draw index) */
 struct AoDraw {
     uint64_t env;
     uint32_t episode;
     int k;
+    Pcg64* g;
 };
-__device__ __forceinline__ double ao_draw(const PgxDevEnv& e, AoDraw& d) { return reset_uniform(e, d.env, d.episode, d.k++); }
+__device__ __forceinline__ double ao_draw(const PgxDevEnv& e, AoDraw& d) {
+    return d.g ? pcg64_next_double(*d.g) : reset_uniform(e, d.env, d.episode, d.k++);
+}
 __device__ __forceinline__ double ao_uniform(const PgxDevEnv& e, AoDraw& d, double lo, double hi) {
     return uniform_draw(lo, hi, ao_draw(e, d));
 }
@@ -4091,17 +4181,26 @@ __device__ __noinline__ void ao_hollow_sphere(const PgxDevEnv& e, AoDraw& d, dou
 
 /* ReachAO.reset for reachao_rand (reach_ao.py:965-1082; oracle ao_reset_task): goal,
  * obstacles by rejection against robot / table / dummy sphere, 4-5 active.  Needs the
- * neutral-pose capsules in LDS; leaves the centres in L.aoC. */
+ * neutral-pose capsules in LDS; leaves the centres in L.aoC.  rec: the env's PCG64 record
+ * (pgx_set_rng_streams; nullptr: Philox), drawn as numpy's Generator draws (uniform / random:
+ * next_double; integers(4, 6): Lemire on next_uint32; shuffle of the 6 names: random_interval on
+ * next_uint32) and written back by the lead lane unless the reset is injected. */
 template <bool PAR, class LT>
 __device__ __noinline__ bool ao_reset(const PgxDevEnv& e, LT& L, int ln, int lane, uint64_t env, uint32_t episode, V3 ee,
-                                      const double* inject_goal, const double* inject_obst, double* goal) {
+                                      const double* inject_goal, const double* inject_obst, double* goal,
+                                      uint64_t* rec, bool lead) {
     bool failed = false;   /* set_coll_free_obs gave up: the reference raises StopIteration */
-    AoDraw d{env, episode, 0};
+    /* get_ee_position after Panda.reset: the host's fp64 value when given (pgx_config.ao_ee_neutral) */
+    const double ex = e.ao_ee_set ? e.ao_ee[0] : (double)ee.x, ey = e.ao_ee_set ? e.ao_ee[1] : (double)ee.y,
+                 ez = e.ao_ee_set ? e.ao_ee[2] : (double)ee.z;
+    Pcg64 g{0, 0, 0, 0, 0, 0};
+    if (rec) g = pcg64_load(rec);
+    AoDraw d{env, episode, 0, rec ? &g : nullptr};
     const V3 tc = ao_table_c(e), th = ao_table_h(e);
     double dummy[3] = {0.0, 0.0, 0.0};
     for (int i = 0;; i++) {
         ao_hollow_sphere(e, d, 0.5, 0.8, true, goal);
-        if (i > 9999) { goal[0] = ee.x; goal[1] = ee.y; goal[2] = ee.z; break; }
+        if (i > 9999) { goal[0] = ex; goal[1] = ey; goal[2] = ez; break; }
         dummy[0] = goal[0]; dummy[1] = goal[1]; dummy[2] = goal[2];
         const V3 g = v3((float)goal[0], (float)goal[1], (float)goal[2]);
         const bool coll = box_sd(g, tc, v3(th.x - kAoMargin, th.y - kAoMargin, th.z - kAoMargin)) - kAoMargin -
@@ -4118,7 +4217,7 @@ __device__ __noinline__ bool ao_reset(const PgxDevEnv& e, LT& L, int ln, int lan
             double sm[3];
             ao_hollow_sphere(e, d, 0.1, 0.5, false, sm);
             if (rnd > 0.5) { P[0] = sm[0] + goal[0]; P[1] = sm[1] + goal[1]; P[2] = sm[2] + goal[2]; }
-            else { P[0] = (double)ee.x + sm[0]; P[1] = (double)ee.y + sm[1]; P[2] = (double)ee.z + sm[2]; }
+            else { P[0] = ex + sm[0]; P[1] = ey + sm[1]; P[2] = ez + sm[2]; }
             const V3 Pf = v3((float)P[0], (float)P[1], (float)P[2]);
             float dtab, ddum;
             if (o < 3) {
@@ -4136,10 +4235,10 @@ __device__ __noinline__ bool ao_reset(const PgxDevEnv& e, LT& L, int ln, int lan
         failed = failed || !placed;
         L.aoC[o][0][ln] = (float)P[0]; L.aoC[o][1][ln] = (float)P[1]; L.aoC[o][2][ln] = (float)P[2];
     }
-    const int n_active = 4 + (int)(ao_draw(e, d) * 2.0);
+    const int n_active = 4 + (rec ? (int)pcg64_bounded(g, 1u) : (int)(ao_draw(e, d) * 2.0));
     int perm[AO_N] = {0, 1, 2, 3, 4, 5};
     for (int j = AO_N - 1; j > 0; j--) {   /* Fisher-Yates, unrolled so perm stays in VGPRs */
-        int r = (int)(ao_draw(e, d) * (double)(j + 1));
+        int r = rec ? (int)pcg64_interval(g, (uint32_t)j) : (int)(ao_draw(e, d) * (double)(j + 1));
         r = r > j ? j : r;
         int pj = 0, pr = 0;
 #pragma unroll
@@ -4156,6 +4255,7 @@ __device__ __noinline__ bool ao_reset(const PgxDevEnv& e, LT& L, int ln, int lan
     if (inject_obst)
         for (int o = 0; o < AO_N; o++)
             for (int k = 0; k < 3; k++) L.aoC[o][k][ln] = (float)inject_obst[3 * o + k];
+    if (rec && lead && !inject_goal && !inject_obst) pcg64_store(g, rec);
     return failed && !inject_obst;
 }
 
@@ -4304,7 +4404,12 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     if constexpr (WIDE) lane_consts(lk);
     const int n_substeps = e.n_substeps;
     bool collided = false;
-    float qprev[NJ];   /* the pose the last substep starts from: getLinkState's cached pose */
+    /* the pose the last substep starts from: getLinkState's cached pose (defined before the loop:
+     * with no substep it is the pose itself, and no path reads an uninitialised value -- the
+     * round-4 runtime-model SLP build's non-finite outputs) */
+    float qprev[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; j++) qprev[j] = q[j];
     /* PARK (wide layout with contacts, an LDS buffer): the motor targets and the substeps' start
      * poses wait in LDS (relaxed atomics: not promoted back into registers) -- ~14 registers
      * fewer across the substep loop, which the two-waves-per-SIMD kernels otherwise spill to
@@ -4428,7 +4533,9 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
             for (int j = 0; j < NJ; j++) { q[j] = mr.neutral_q[j]; qd[j] = 0.0f; qprev[j] = q[j]; }
             ee_state(mr, q, qd, pos, vel);
             ao_caps(mr, q, *L, ln);
-            if (ao_reset<WIDE != 0>(e, *L, ln, c, e.env_id_offset + (uint64_t)i, episode, pos, nullptr, nullptr, goal) &&
+            uint64_t* rec = (e.pcg_on != nullptr && *e.pcg_on != 0) ? e.pcg + PGX_PCG64_WORDS * (size_t)i : nullptr;
+            if (ao_reset<WIDE != 0>(e, *L, ln, c, e.env_id_offset + (uint64_t)i, episode, pos, nullptr, nullptr, goal, rec,
+                                    lead) &&
                 lead)
                 atomicOr(s.errors, PGX_ERR_AO_OBSTACLE);
             episode += 1;
@@ -4549,9 +4656,10 @@ __global__ __launch_bounds__(64) void reset_kernel(const PgxDevModel* __restrict
         for (int j = 0; j < NJ; j++) { q[j] = m.neutral_q[j]; qd[j] = 0.0f; }
         ee_state(m, q, qd, pos, vel);
         ao_caps(m, q, *L, ln);
+        uint64_t* rec = (e.pcg_on != nullptr && *e.pcg_on != 0) ? e.pcg + PGX_PCG64_WORDS * (size_t)i : nullptr;
         if (ao_reset<false>(e, *L, ln, 0, e.env_id_offset + (uint64_t)i, episode, pos,
                             inject_goal ? inject_goal + 3 * (size_t)i : nullptr,
-                            inject_obj ? inject_obj + 3 * AO_N * (size_t)i : nullptr, goal))
+                            inject_obj ? inject_obj + 3 * AO_N * (size_t)i : nullptr, goal, rec, true))
             atomicOr(s.errors, PGX_ERR_AO_OBSTACLE);
         episode += 1;
         ao_link_obs(*L, ln);
@@ -4831,6 +4939,14 @@ int pgx_launch_compute_reward(const float* ag, const float* dg, int64_t n, int32
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(compute_reward_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, ag, dg, n,
                        reward_type, (float)thr, out);
+    return (int)hipGetLastError();
+}
+/* one device word written on the stream (the PCG64 mode word): a kernel node, not a memset node,
+ * when a caller captures it -- a memset node of a graph destroyed after instantiation (torch's
+ * default capture) replays garbage from its second launch on, DESIGN.md section 4 */
+__global__ void set_word_kernel(int32_t* p, int32_t v) { *p = v; }
+int pgx_launch_set_word(int32_t* p, int32_t v, void* stream) {
+    hipLaunchKernelGGL(set_word_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, p, v);
     return (int)hipGetLastError();
 }
 #endif  /* PGX_TU != 1 */

@@ -21,7 +21,7 @@ import ctypes as C
 import math
 import os
 from dataclasses import replace
-from typing import Any, Dict, List, Optional, Sequence, Tuple
+from typing import Any, Dict, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
@@ -109,10 +109,11 @@ def seeded_goal(env_spec: abi.EnvSpec, seed: Optional[int]) -> Optional[np.ndarr
 _AO_GEOM: Dict[tuple, "reach_ao.RobotGeometry"] = {}
 
 
-def _ao_geometry(base_pos: tuple) -> "reach_ao.RobotGeometry":
-    if base_pos not in _AO_GEOM:
-        _AO_GEOM[base_pos] = reach_ao.RobotGeometry(load_model("panda_custom0"), base_pos)
-    return _AO_GEOM[base_pos]
+def _ao_geometry(base_pos: tuple, model_name: str = "panda_custom0") -> "reach_ao.RobotGeometry":
+    key = (base_pos, model_name)
+    if key not in _AO_GEOM:
+        _AO_GEOM[key] = reach_ao.RobotGeometry(load_model(model_name), base_pos)
+    return _AO_GEOM[key]
 
 
 def seeded_reset(env_spec: abi.EnvSpec, seed: Optional[int]) -> Optional[Tuple[np.ndarray, Optional[np.ndarray]]]:
@@ -145,23 +146,33 @@ def task_draws(env_spec: abi.EnvSpec, rng: np.random.Generator) -> Tuple[np.ndar
     return goal, obj
 
 
-def pcg64_records(seeds: Sequence[int]) -> np.ndarray:
-    """[N, 4] uint64 {state_lo, state_hi, inc_lo, inc_hi} of PCG64(SeedSequence(seed)) per seed:
-    gymnasium's seeding.np_random(seed) (core.py:302), the records pgx_set_rng_streams takes."""
-    out = np.empty((len(seeds), 4), dtype=np.uint64)
+def pcg64_record(gen: Union[np.random.Generator, np.random.PCG64]) -> np.ndarray:
+    """[abi.PCG64_WORDS] uint64 {state_lo, state_hi, inc_lo, inc_hi, has_uint32, uinteger}: numpy's
+    PCG64 bit_generator.state, the record pgx_set_rng_streams takes per env (pgx.h)."""
+    bg = gen.bit_generator if isinstance(gen, np.random.Generator) else gen
+    st = bg.state
     m = (1 << 64) - 1
+    s = st["state"]
+    has = int(st["has_uint32"])   # (a spent uinteger, which numpy keeps, is recorded as 0)
+    return np.array([s["state"] & m, s["state"] >> 64, s["inc"] & m, s["inc"] >> 64, has,
+                     int(st["uinteger"]) if has else 0], dtype=np.uint64)
+
+
+def pcg64_records(seeds: Sequence[int]) -> np.ndarray:
+    """[N, abi.PCG64_WORDS] records of PCG64(SeedSequence(seed)) per seed: gymnasium's
+    seeding.np_random(seed) (core.py:302)."""
+    out = np.empty((len(seeds), abi.PCG64_WORDS), dtype=np.uint64)
     for i, sd in enumerate(seeds):
-        st = np.random.PCG64(np.random.SeedSequence(int(sd))).state["state"]
-        out[i] = (st["state"] & m, st["state"] >> 64, st["inc"] & m, st["inc"] >> 64)
+        out[i] = pcg64_record(np.random.PCG64(np.random.SeedSequence(int(sd))))
     return out
 
 
 def pcg64_from_record(rec: np.ndarray) -> np.random.Generator:
-    """numpy Generator at a record's stream position (inverse of pcg64_records)."""
+    """numpy Generator at a record's stream position (inverse of pcg64_record)."""
     bg = np.random.PCG64()
     st = bg.state
     st["state"] = {"state": int(rec[0]) | (int(rec[1]) << 64), "inc": int(rec[2]) | (int(rec[3]) << 64)}
-    st["has_uint32"], st["uinteger"] = 0, 0
+    st["has_uint32"], st["uinteger"] = int(rec[4]), int(rec[5])
     bg.state = st
     return np.random.Generator(bg)
 
@@ -186,8 +197,10 @@ class PandaVecEnv:
     on the device, bit for bit -- RobotTaskEnv.reset reseeds ``task.np_random`` on every reset
     (core.py:302).  A reset without a seed, the auto-reset included, gets fresh OS entropy in the
     reference, so there is no reference value to match: here it continues the env's stream (a
-    reproducible stand-in with the reference's distribution).  Not for ReachAO (its rejection
-    sampler is not restated on the device)."""
+    reproducible stand-in with the reference's distribution).  ReachAO draws its rejection sampler
+    (reach_ao.py:965-1082) from the stream with numpy's uniform / random / integers / shuffle; its
+    accept / reject tests are the kernel's fp32 geometry, so a seed whose numpy-side test sits
+    within fp32 rounding of its threshold can take the other branch."""
 
     def __init__(self, env_id: str = "PandaReach-v3", num_envs: int = 4096, device: Any = "cuda:0", seed: int = 0,
                  env_id_offset: int = 0, max_episode_steps: Optional[int] = None, auto_reset: bool = True,
@@ -205,9 +218,6 @@ class PandaVecEnv:
         base_spec = spec(env_id)
         if reset_rng not in ("philox", "pcg64"):
             raise ValueError(f"reset_rng must be 'philox' or 'pcg64', got {reset_rng!r}")
-        if reset_rng == "pcg64" and base_spec.task == abi.TASK_REACH_AO:   # refused before pgx_create
-            raise PgxError("reset_rng='pcg64' is not available for ReachAO (its rejection sampler is not restated "
-                           "on the device; seeded resets are injected from the host)")
         if max_episode_steps is not None:
             base_spec = replace(base_spec, max_episode_steps=max_episode_steps)
         self.spec = base_spec
@@ -229,6 +239,10 @@ class PandaVecEnv:
         self._cfg = abi.make_config(self.spec, self.num_envs, self._model, self._params, seed=seed,
                                     env_id_offset=env_id_offset, contacts=contacts, lanes_per_env=lanes_per_env,
                                     full_manifold=full_manifold)
+        if self.spec.task == abi.TASK_REACH_AO:   # the reset sampler's EE centre, fp64 (pgx.h ao_ee_neutral)
+            ee = _ao_geometry(tuple(self.spec.base_pos), model_name).ee
+            for i in range(3):
+                self._cfg.ao_ee_neutral[i] = float(ee[i])
         # auto_reset=False: a finished env keeps its terminal state until reset (one gymnasium env)
         self._cfg.no_auto_reset = 0 if auto_reset else 1
         self.auto_reset = bool(auto_reset)
@@ -362,9 +376,9 @@ class PandaVecEnv:
         self._rng_keep = rec   # read by the queued copy
 
     def rng_streams(self) -> np.ndarray:
-        """[N, 4] uint64 PCG64 records of the envs' reset streams (``reset_rng="pcg64"``): where each
-        env's np_random stands (pcg64_from_record rebuilds the numpy Generator)."""
-        out = torch.empty((self.num_envs, 4), dtype=torch.int64, device=self.device)
+        """[N, abi.PCG64_WORDS] uint64 PCG64 records of the envs' reset streams (``reset_rng="pcg64"``):
+        where each env's np_random stands (pcg64_from_record rebuilds the numpy Generator)."""
+        out = torch.empty((self.num_envs, abi.PCG64_WORDS), dtype=torch.int64, device=self.device)
         self._check(self.lib.pgx_get_rng_streams(self._h, C.c_void_p(out.data_ptr()), self._stream()),
                     "pgx_get_rng_streams")
         return out.cpu().numpy().view(np.uint64)

@@ -20,8 +20,9 @@ and ReachAO.reset (reach_ao.py:965-1000) then draws, in this order:
 numpy's own Generator produces the draws here (uniform, random, integers, shuffle),
 so the stream is the reference's by construction; the geometry (signed distances
 of the capsule robot to spheres and rounded boxes) restates the kernel's
-(``pgx_kernels.hip``) in float64.  The device auto-reset draws the same sequence
-from the counter-based Philox stream instead.
+(``pgx_kernels.hip``) in float64.  The device reset draws the same sequence from the
+env's PCG64 record (``reset_rng="pcg64"``: numpy's draws, bit for bit) or from the
+counter-based Philox stream.
 """
 from __future__ import annotations
 
@@ -129,22 +130,30 @@ def _hollow_sphere(rng: np.random.Generator, rmin: float, rmax: float, upper_hal
     return np.array([r * np.sin(theta) * np.cos(phi), r * np.sin(theta) * np.sin(phi), r * np.cos(theta)])
 
 
-def reset_draws(rng: np.random.Generator, geom: RobotGeometry) -> Tuple[np.ndarray, np.ndarray]:
-    """(goal[3], obstacles[6, 3]) of one ReachAO.reset drawn from ``rng``."""
+def reset_draws(rng: np.random.Generator, geom: RobotGeometry, trace: Optional[list] = None,
+                margins: Optional[list] = None) -> Tuple[np.ndarray, np.ndarray]:
+    """(goal[3], obstacles[6, 3]) of one ReachAO.reset drawn from ``rng``.  ``trace`` collects the
+    draws in order (("double", k), ("integers", 1), ("shuffle", 6)); ``margins`` every accept /
+    reject test's distance minus its threshold (a test within rounding of 0 may decide otherwise
+    in another precision)."""
     th = TABLE_HALF
     goal = None
     dummy = None
     i = 0
+    rec = trace.append if trace is not None else (lambda _x: None)
+    mrg = margins.extend if margins is not None else (lambda _x: None)
     while True:
         goal = _hollow_sphere(rng, 0.5, 0.8, True)
+        rec(("double", 3))
         if i > 9999:
             goal = geom.ee.copy()
             break
         i += 1
         dummy = goal
-        coll = (float(rbox_sd(goal, TABLE_CENTER, th)) - DUMMY_R <= GOAL_MARGIN,
-                geom.distance(0, goal, DUMMY_R) <= GOAL_MARGIN)
-        if not any(coll):
+        d = (float(rbox_sd(goal, TABLE_CENTER, th)) - DUMMY_R - GOAL_MARGIN,
+             geom.distance(0, goal, DUMMY_R) - GOAL_MARGIN)
+        mrg(d)
+        if not any(x <= 0.0 for x in d):
             break
     obst = np.zeros((6, 3))
     hcube = np.array([AO_SIZE] * 3)
@@ -152,6 +161,7 @@ def reset_draws(rng: np.random.Generator, geom: RobotGeometry) -> Tuple[np.ndarr
         for _ in range(10000):
             rnd = rng.random()
             s = _hollow_sphere(rng, 0.1, 0.5, False)
+            rec(("double", 4))
             P = s + goal if rnd > 0.5 else geom.ee + s
             if kind == 0:
                 dtab = float(rbox_sd(P, TABLE_CENTER, th)) - AO_SIZE
@@ -160,15 +170,18 @@ def reset_draws(rng: np.random.Generator, geom: RobotGeometry) -> Tuple[np.ndarr
             else:
                 dtab = float(box_sd(P, TABLE_CENTER, th + AO_SIZE - 2 * MARGIN)) - 2 * MARGIN
                 ddum = float(rbox_sd(dummy, P, hcube)) - DUMMY_R
-            coll = (geom.distance(kind, P, AO_SIZE) <= OBST_MARGIN, dtab <= OBST_MARGIN, ddum <= OBST_MARGIN)
+            d = (geom.distance(kind, P, AO_SIZE) - OBST_MARGIN, dtab - OBST_MARGIN, ddum - OBST_MARGIN)
+            mrg(d)
             obst[o] = P
-            if not any(coll):
+            if not any(x <= 0.0 for x in d):
                 break
         else:   # set_coll_free_obs (reach_ao.py:1143-1145): the 10001st attempt raises
             raise StopIteration("Couldn't find collision free obstacle!")
     n_active = int(rng.integers(4, 6))
     keys = list(range(6))
     rng.shuffle(keys)
+    rec(("integers", 1))
+    rec(("shuffle", 6))
     for k in keys[:abs(n_active - 6)]:
         obst[k] = PARKED
     return goal, obst

@@ -166,15 +166,18 @@ def _inside_envelope(name, dev, f32, pcts=(99, 99.9), floor=1e-5):
 
 def _self_sensitivity(oracle, cfg, rec, trials=16, rel=1e-7, seed=0):
     """The oracle's own one-step response (max |ee|, |ag| change over ``trials``) to its input
-    state perturbed by ``rel`` relative -- the fp32 rounding scale of the device state."""
+    state perturbed by ``rel`` relative -- the fp32 rounding scale of the device state.  Half the
+    trials at rel, half at 3 rel: the device state carries the rounding of every operation of the
+    step before (a few fp32 ulps), not one."""
     c1 = type(cfg).from_buffer_copy(cfg)
     c1.n_envs = 1
     rng = np.random.default_rng(seed)
     d_ee = d_ag = 0.0
-    for _ in range(trials):
+    for t in range(trials):
         r = oracle.OracleVecEnv(c1, 1)
         q, qd, goal, obj, el, ep = (x.copy() for x in rec["state"])
-        pert = lambda x: x * (1.0 + rel * rng.standard_normal(x.shape))  # noqa: E731
+        rt = rel if t % 2 == 0 else 3.0 * rel
+        pert = lambda x: x * (1.0 + rt * rng.standard_normal(x.shape))  # noqa: E731
         r.q[:], r.qd[:], r.goal[:], r.obj[:] = pert(q), pert(qd), goal, obj
         r.obj[:, :13] = pert(obj[:, :13])
         # the persistent manifold points are state the device holds in fp32 too: their positions,
@@ -262,7 +265,7 @@ def test_full_manifold_random_policy_one_step_parity(pg, oracle, env_id):
     for rec in outl:
         # an outlier sits where the oracle itself moves as far under a rounding-level perturbation
         # of its input, or where the restated algorithm evaluated in fp32 does
-        s_ee, s_ag = _self_sensitivity(oracle, cfg, rec, trials=32)
+        s_ee, s_ag = _self_sensitivity(oracle, cfg, rec, trials=64)
         s_ee, s_ag = max(s_ee, rec["f32_ee"]), max(s_ag, rec["f32_ag"])
         assert rec["err_ee"] <= OUTLIER or s_ee >= rec["err_ee"], (rec["t"], rec["env"], rec["err_ee"], s_ee)
         assert rec["err_ag"] <= OUTLIER or s_ag >= rec["err_ag"], (rec["t"], rec["env"], rec["err_ag"], s_ag)

@@ -2,7 +2,7 @@
 against numpy itself.  What is the reference's: a reset with seed s draws from
 gymnasium's seeding.np_random(s) = Generator(PCG64(SeedSequence(s))), because RobotTaskEnv.reset
 reseeds task.np_random on every reset (core.py:302), in the task's order (reach.py:75-78,
-push.py:75-87, pick_and_place.py:71-85) -- bit-exact here: the fp64 goal in the device state, the
+push.py:75-87, pick_and_place.py:71-85; ReachAO's rejection sampler below) -- bit-exact here: the fp64 goal in the device state, the
 object position (f32 of the fp64 draw) and the stream record.  What is not: a reset without a seed
 (the auto-reset included) gets fresh OS entropy in the reference, so it has no reference value; the
 device continues the env's stream instead, and the tests below pin that continuation against
@@ -38,9 +38,7 @@ def _check_envs(pg, venv, gens, expect):
         assert np.array_equal(st["object"].cpu().numpy()[:3].T, o_ref)
     rec = venv.rng_streams()
     for r, g in zip(rec, gens):
-        s = g.bit_generator.state["state"]
-        m = (1 << 64) - 1
-        assert [int(v) for v in r] == [s["state"] & m, s["state"] >> 64, s["inc"] & m, s["inc"] >> 64]
+        assert np.array_equal(r, pg.pcg64_record(g))
 
 
 @pytest.mark.parametrize("env_id,lanes,contacts", [
@@ -133,7 +131,7 @@ def test_single_env_seeded_reset_then_unseeded_resets_continue_the_stream(pg):
     env.close()
 
 
-def test_back_to_philox_and_reach_ao_refused(pg):
+def test_back_to_philox(pg):
     venv = pg.PandaVecEnv("PandaReach-v3", num_envs=8, device="cuda:0", seed=5, reset_rng="pcg64")
     ref = pg.PandaVecEnv("PandaReach-v3", num_envs=8, device="cuda:0", seed=5)
     assert venv.lib.pgx_set_rng_streams(venv._h, None, venv._stream()) == 0
@@ -145,8 +143,65 @@ def test_back_to_philox_and_reach_ao_refused(pg):
     assert np.array_equal(venv.state()["goal"].cpu().numpy(), ref.state()["goal"].cpu().numpy())
     venv.close()
     ref.close()
-    with pytest.raises(pg.PgxError, match="ReachAO"):
-        pg.PandaVecEnv("PandaReachAO-v3", num_envs=4, device="cuda:0", reset_rng="pcg64")
+
+
+# the ReachAO goal r (sin t cos p, sin t sin p, cos t), r <= 0.8: a last-bit difference of the
+# device's sin / cos / cbrt moves a component by up to a few ulp of r, not of the component
+GOAL_TOL = 4 * 0.8 * np.finfo(np.float64).eps
+
+
+@pytest.mark.parametrize("lanes", [16, 1])
+def test_reach_ao_seeded_reset_on_the_device_then_auto_resets(pg, lanes):
+    """ReachAO (reach_ao.py:965-1082) in the PCG64 mode, no host injection: reset(seed)
+    draws env i's goal and obstacles from Generator(PCG64(SeedSequence(seed + i))) on the device --
+    hollow-sphere uniforms, the obstacle coin, integers(4, 6) and the shuffle of the 6 names, as
+    numpy draws them -- then two auto-resets (TimeLimit 1) continue the stream.  Checked against
+    the host sampler reach_ao.reset_draws on numpy's own Generator: the stream record (numpy's full
+    bit_generator.state, has_uint32 included) bit for bit; the fp64 goal to 4 ulp of its radius
+    (GOAL_TOL) and the obstacle centres (f32) to 1 ulp -- the device's sin / cos / cbrt against the
+    host libm, whose last-bit differences can cross an f32 rounding boundary.  The kernel's
+    accept / reject tests run in fp32 and the host's in fp64, so an env may take the other branch
+    where a host test sits within 1e-4 of its threshold: such envs are counted, must be explained
+    by that margin, and continue from the device's record."""
+    from panda_gym_amd import reach_ao
+    from panda_gym_amd.envs import _ao_geometry
+
+    n, seed = 256, 9000
+    venv = pg.PandaVecEnv("PandaReachAO-v3", num_envs=n, device="cuda:0", seed=1, max_episode_steps=1,
+                          lanes_per_env=lanes, reset_rng="pcg64")
+    geom = _ao_geometry(tuple(venv.spec.base_pos))
+    gens = _gens(seed, n)
+    venv.reset_tensors(seed=seed)
+    zero = torch.zeros((n, venv.action_dim), device="cuda:0")
+    exact_goal, exact_obst, explained = 0, 0, 0
+    for rnd in range(3):
+        st = venv.state()
+        goal = st["goal"].cpu().numpy().T
+        obst = st["obstacles"][:18].cpu().numpy().T.reshape(n, 6, 3)
+        recs = venv.rng_streams()
+        for i in range(n):
+            margins = []
+            g_ref, o_ref = reach_ao.reset_draws(gens[i], geom, margins=margins)
+            of = o_ref.astype(np.float32)
+            same = (np.array_equal(recs[i], pg.pcg64_record(gens[i]))
+                    and np.all(np.abs(obst[i] - of) <= np.spacing(np.abs(of)))
+                    and np.all(np.abs(goal[i] - g_ref) <= GOAL_TOL))
+            exact_obst += int(np.array_equal(obst[i], of))
+            if same:
+                exact_goal += int(np.array_equal(goal[i], g_ref))
+            else:
+                assert min(abs(m) for m in margins) < 1e-4, (
+                    rnd, i, goal[i] - g_ref, recs[i].tolist(), pg.pcg64_record(gens[i]).tolist(),
+                    np.abs(obst[i] - o_ref.astype(np.float32)).max(axis=1).tolist())
+                explained += 1
+                gens[i] = pg.pcg64_from_record(recs[i])
+        if rnd < 2:
+            venv.step_tensors(zero)
+            assert venv.truncated.all().item()
+    print(f"ReachAO pcg64 resets: {3 * n} checked, {explained} explained by a fp32 decision, goals bit-exact "
+          f"{exact_goal} and obstacle centres bit-exact {exact_obst} of {3 * n - explained}")
+    assert explained <= 0.02 * 3 * n
+    venv.close()
 
 
 def test_captured_graph_draws_in_the_mode_of_replay_time(pg):

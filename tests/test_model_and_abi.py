@@ -124,7 +124,8 @@ def test_constants_match_header():
 
     from oracle import oracle as orc
 
-    for name in ("OBJECT_POINTS", "ROBOT_POINTS", "ROBOT_POINTS_ARM", "ROBOT_POINTS_ONE_LANE"):
+    for name in ("OBJECT_POINTS", "ROBOT_POINTS", "ROBOT_POINTS_ARM", "ROBOT_POINTS_ONE_LANE", "MANIFOLD_POOL",
+                 "MANIFOLD_POOL_AO", "MANIFOLD_POINT", "PCG64_WORDS"):
         assert getattr(abi, name) == define("PGX_" + name), name
     assert orc.OBJECT_POINTS == abi.OBJECT_POINTS and orc.ROBOT_MAX >= abi.ROBOT_POINTS
     for name in ("PGX_E_INVALID", "PGX_E_HIP", "PGX_E_UNSUPPORTED", "PGX_E_NOMEM"):

@@ -2,9 +2,11 @@
 against numpy itself (gymnasium's seeding.np_random = Generator(PCG64(SeedSequence(seed))),
 core.py:302), and the host records pgx_set_rng_streams takes.
 
-The restatement below is the kernel's `pcg64_next_double` (csrc/pgx_kernels.hip) in Python
-integers: 128-bit LCG step with numpy's PCG64 multiplier, XSL-RR output of the new state,
-(u >> 11) * 2^-53."""
+The restatement below is the kernel's `pcg64_next64` / `pcg64_next_double` / `pcg64_next32` /
+`pcg64_bounded` / `pcg64_interval` (csrc/pgx_kernels.hip) in Python integers: 128-bit LCG step with
+numpy's PCG64 multiplier, XSL-RR output of the new state, (u >> 11) * 2^-53; next_uint32 hands out a
+64-bit output's low half and keeps the high half (has_uint32 / uinteger); Generator.integers(4, 6)
+by Lemire's bounded draw on next_uint32, Generator.shuffle of a list by random_interval."""
 import numpy as np
 import pytest
 
@@ -29,6 +31,40 @@ def _next_double(rec):
     return (_next64(rec) >> 11) * (1.0 / 9007199254740992.0)
 
 
+def _next32(rec):
+    if rec[4]:
+        v = rec[5]
+        rec[4], rec[5] = 0, 0
+        return v
+    n = _next64(rec)
+    rec[4], rec[5] = 1, n >> 32
+    return n & 0xFFFFFFFF
+
+
+def _bounded(rec, rng):
+    excl = rng + 1
+    m = _next32(rec) * excl
+    left = m & 0xFFFFFFFF
+    if left < excl:
+        thr = (0xFFFFFFFF - rng) % excl
+        while left < thr:
+            m = _next32(rec) * excl
+            left = m & 0xFFFFFFFF
+    return m >> 32
+
+
+def _interval(rec, mx):
+    if mx == 0:
+        return 0
+    mask = mx
+    for sh in (1, 2, 4, 8, 16):
+        mask |= mask >> sh
+    while True:
+        v = _next32(rec) & mask
+        if v <= mx:
+            return v
+
+
 @pytest.mark.parametrize("seed", [0, 1, 12345, 2 ** 40 + 7])
 def test_restatement_matches_numpy_raw_and_doubles(seed):
     rec = [int(v) for v in pg.pcg64_records([seed])[0]]
@@ -41,7 +77,7 @@ def test_restatement_matches_numpy_raw_and_doubles(seed):
 
 def test_records_round_trip_and_continue_the_stream():
     recs = pg.pcg64_records([5, 6, 7])
-    assert recs.dtype == np.uint64 and recs.shape == (3, 4)
+    assert recs.dtype == np.uint64 and recs.shape == (3, abi.PCG64_WORDS)
     for sd, r in zip((5, 6, 7), recs):
         a = np.random.Generator(np.random.PCG64(np.random.SeedSequence(sd)))
         b = pg.pcg64_from_record(r)
@@ -52,8 +88,58 @@ def test_records_round_trip_and_continue_the_stream():
     rec = [int(v) for v in pg.pcg64_records([11])[0]]
     for _ in range(3):
         _next64(rec)
-    st = g.bit_generator.state["state"]
-    assert rec == [st["state"] & M64, st["state"] >> 64, st["inc"] & M64, st["inc"] >> 64]
+    assert rec == [int(v) for v in pg.pcg64_record(g)]
+
+
+@pytest.mark.parametrize("seed", [0, 3, 77, 2024, 2 ** 33 + 5])
+def test_uint32_draws_integers_and_shuffle_match_numpy(seed):
+    """ReachAO.reset's integer draws (set_random_num_obs, reach_ao.py:1062-1082): integers(4, 6) and
+    shuffle of the 6 obstacle names, after some doubles; the half-used 64-bit output carried in the
+    record (has_uint32, uinteger) into the next reset's draws, as numpy carries it."""
+    gen = np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed)))
+    rec = [int(v) for v in pg.pcg64_records([seed])[0]]
+    for rnd in range(6):
+        k = 5 + 3 * rnd
+        assert [_next_double(rec) for _ in range(k)] == list(gen.random(k))
+        n = int(gen.integers(4, 6))
+        assert n == 4 + _bounded(rec, 1)
+        keys = list(range(6))
+        gen.shuffle(keys)
+        perm = list(range(6))
+        for j in range(5, 0, -1):
+            r = _interval(rec, j)
+            perm[j], perm[r] = perm[r], perm[j]
+        assert perm == keys
+        assert rec == [int(v) for v in pg.pcg64_record(gen)]
+    # a record with the cached half round-trips through pcg64_from_record
+    g2 = pg.pcg64_from_record(np.array(rec, dtype=np.uint64))
+    assert int(g2.integers(0, 1000)) == int(gen.integers(0, 1000))
+
+
+def test_reach_ao_reset_draw_order_from_the_record():
+    """The device ReachAO reset's draws from a record (kernel ao_reset: hollow sphere = uniform phi,
+    theta, r^3; obstacle coin random(); integers; shuffle) consume the stream exactly as the host
+    sampler reach_ao.reset_draws does with numpy's Generator: same record after each reset."""
+    from panda_gym_amd import reach_ao
+    from panda_gym_amd.envs import _ao_geometry
+
+    geom = _ao_geometry(tuple(pg.spec("PandaReachAO-v3").base_pos))
+    for seed in (1, 42, 1000):
+        gen = np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed)))
+        rec = [int(v) for v in pg.pcg64_records([seed])[0]]
+        for _ in range(3):
+            trace = []
+            reach_ao.reset_draws(gen, geom, trace=trace)
+            for kind, arg in trace:
+                if kind == "double":
+                    for _k in range(arg):
+                        _next_double(rec)
+                elif kind == "integers":
+                    _bounded(rec, 1)
+                else:
+                    for j in range(5, 0, -1):
+                        _interval(rec, j)
+            assert rec == [int(v) for v in pg.pcg64_record(gen)]
 
 
 @pytest.mark.parametrize("env_id", ["PandaReach-v3", "PandaPush-v3", "PandaPickAndPlace-v3"])

@@ -46,7 +46,7 @@ def run(lib, lanes, contacts, n_substeps, env_id="PandaReach-v3", steps=3, sp=No
 
 def main():
     pg.load_native()
-    rt = os.path.join(os.path.dirname(_native.LIB_PATH), "libpgx_rtmodel.so")
+    rt = os.path.join(os.path.dirname(_native.LIB_PATH), os.environ.get("RT_LIB", "libpgx_rtmodel.so"))
     from panda_gym_amd import abi
 
     dflt = list(abi.default_sim_params().link_friction)

@@ -65,7 +65,8 @@ def run(env_id, n, contacts, launches=100, warm=26):
                   "epilogue_cyc_mean": float(w[:, 9].mean()), "epilogue_cyc_top1pct": float(w[top, 9].mean())}
     per = [buf[k] / (waves * launches) for k in range(24)]
     tot = sum(per[:7]) + per[14] + per[15] + sum(per[19:24])
-    out = {"env_id": env_id, "n": n, "contacts": contacts, "ms_per_step": ms,
+    out = {"lib": os.path.basename(_native.LIB_PATH), "staggered": bool(os.environ.get("PH_STAGGER")),
+           "env_id": env_id, "n": n, "contacts": contacts, "ms_per_step": ms,
            "cycles_per_wave_step": tot, "clock_ghz_est": tot / (ms * 1e6),
            "phases": {NAMES[k]: round(per[k]) for k in range(7)},
            "share": {NAMES[k]: round(per[k] / tot, 3) for k in range(7)},
