@@ -1934,7 +1934,10 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                 const int row0 = (int)(threadIdx.x & ~(unsigned)(GW - 1));
                 bool sorted = false, hit = false;
                 if (chk && slot >= 1) {
-                    const V3 tc = ao_table_c(e), th = ao_table_h(e);
+                    V3 tc = ao_table_c(e), th = ao_table_h(e);
+                    /* recomputed here in every substep: hoisted out of the substep loop, the box
+                     * bounds derived from them were spilled and reloaded (two-wave kernel) */
+                    asm volatile("" : "+v"(tc.x), "+v"(tc.y), "+v"(tc.z), "+v"(th.x), "+v"(th.y), "+v"(th.z));
                     const V3 thi = v3(th.x - kAoMargin, th.y - kAoMargin, th.z - kAoMargin);
                     const float lb = fminf(box_sd(A, tc, thi), box_sd(B, tc, thi)) - 0.5f * norm(B - A) - kAoMargin - r;
                     if (lb <= 0.0f) hit = capsule_box_hit(A, B, r, tc, th);
@@ -3737,12 +3740,15 @@ __device__ __forceinline__ void ee_state_cached(MRef m, const float* qc, const f
 constexpr uint32_t TAG_RESET = 0x52455345u;
 constexpr uint32_t TAG_ACTION = 0x41435430u;
 
-__device__ __forceinline__ double reset_uniform(const PgxDevEnv& e, uint64_t env, uint32_t episode, int kidx) {
+__device__ __forceinline__ double reset_uniform_s(uint64_t seed, uint64_t env, uint32_t episode, int kidx) {
     uint32_t o[4];
-    philox((uint32_t)env, (uint32_t)(env >> 32), episode, TAG_RESET + (uint32_t)(kidx >> 1), (uint32_t)e.seed,
-           (uint32_t)(e.seed >> 32), o);
+    philox((uint32_t)env, (uint32_t)(env >> 32), episode, TAG_RESET + (uint32_t)(kidx >> 1), (uint32_t)seed,
+           (uint32_t)(seed >> 32), o);
     uint64_t u = (kidx & 1) ? ((uint64_t)o[2] | ((uint64_t)o[3] << 32)) : ((uint64_t)o[0] | ((uint64_t)o[1] << 32));
     return (double)(u >> 11) * (1.0 / 9007199254740992.0);
+}
+__device__ __forceinline__ double reset_uniform(const PgxDevEnv& e, uint64_t env, uint32_t episode, int kidx) {
+    return reset_uniform_s(e.seed, env, episode, kidx);
 }
 
 /* numpy's PCG64 (XSL-RR 128/64, the generator gymnasium's seeding.np_random builds,
@@ -4156,24 +4162,24 @@ __device__ __noinline__ bool ao_robot_hit(LT& L, int ln, int lane, int kind, V3 
 /* the reset's draw source: the env's numpy PCG64 stream (g, pgx_set_rng_streams) or the Philox
  * counter (env, episode, draw index) */
 struct AoDraw {
+    uint64_t seed;
     uint64_t env;
     uint32_t episode;
     int k;
     Pcg64* g;
 };
-__device__ __forceinline__ double ao_draw(const PgxDevEnv& e, AoDraw& d) {
-    return d.g ? pcg64_next_double(*d.g) : reset_uniform(e, d.env, d.episode, d.k++);
+__device__ __forceinline__ double ao_draw(AoDraw& d) {
+    return d.g ? pcg64_next_double(*d.g) : reset_uniform_s(d.seed, d.env, d.episode, d.k++);
 }
-__device__ __forceinline__ double ao_uniform(const PgxDevEnv& e, AoDraw& d, double lo, double hi) {
-    return uniform_draw(lo, hi, ao_draw(e, d));
+__device__ __forceinline__ double ao_uniform(AoDraw& d, double lo, double hi) {
+    return uniform_draw(lo, hi, ao_draw(d));
 }
 /* sample_within_hollow_sphere (reach_ao.py:1188-1211) */
-__device__ __noinline__ void ao_hollow_sphere(const PgxDevEnv& e, AoDraw& d, double rmin, double rmax, bool upper,
-                                              double* out) {
+__device__ __noinline__ void ao_hollow_sphere(AoDraw& d, double rmin, double rmax, bool upper, double* out) {
     const double pi = 3.14159265358979323846;
-    const double phi = ao_uniform(e, d, 0.0, 2.0 * pi);
-    const double theta = upper ? ao_uniform(e, d, 0.0, 0.5 * pi) : ao_uniform(e, d, 0.0, pi);
-    const double r = cbrt(ao_uniform(e, d, pow(rmin, 3.0), pow(rmax, 3.0)));
+    const double phi = ao_uniform(d, 0.0, 2.0 * pi);
+    const double theta = upper ? ao_uniform(d, 0.0, 0.5 * pi) : ao_uniform(d, 0.0, pi);
+    const double r = cbrt(ao_uniform(d, pow(rmin, 3.0), pow(rmax, 3.0)));
     out[0] = r * sin(theta) * cos(phi);
     out[1] = r * sin(theta) * sin(phi);
     out[2] = r * cos(theta);
@@ -4185,21 +4191,31 @@ __device__ __noinline__ void ao_hollow_sphere(const PgxDevEnv& e, AoDraw& d, dou
  * (pgx_set_rng_streams; nullptr: Philox), drawn as numpy's Generator draws (uniform / random:
  * next_double; integers(4, 6): Lemire on next_uint32; shuffle of the 6 names: random_interval on
  * next_uint32) and written back by the lead lane unless the reset is injected. */
+/* What ao_reset reads of the env, by value: a reference to the kernel's PgxDevEnv argument would
+ * make every lane copy the whole struct to scratch at kernel start (368 B per lane) for this
+ * rarely taken call. */
+struct AoResetIn {
+    uint64_t seed;
+    V3 tc, th;       /* the table box (centre, half extents) */
+    double ex, ey, ez;   /* get_ee_position after Panda.reset (pgx_config.ao_ee_neutral, or the fp32 FK) */
+};
+__device__ __forceinline__ AoResetIn ao_reset_in(const PgxDevEnv& e, V3 ee) {
+    return AoResetIn{e.seed, ao_table_c(e), ao_table_h(e), e.ao_ee_set ? e.ao_ee[0] : (double)ee.x,
+                     e.ao_ee_set ? e.ao_ee[1] : (double)ee.y, e.ao_ee_set ? e.ao_ee[2] : (double)ee.z};
+}
 template <bool PAR, class LT>
-__device__ __noinline__ bool ao_reset(const PgxDevEnv& e, LT& L, int ln, int lane, uint64_t env, uint32_t episode, V3 ee,
+__device__ __noinline__ bool ao_reset(const AoResetIn& in, LT& L, int ln, int lane, uint64_t env, uint32_t episode,
                                       const double* inject_goal, const double* inject_obst, double* goal,
                                       uint64_t* rec, bool lead) {
     bool failed = false;   /* set_coll_free_obs gave up: the reference raises StopIteration */
-    /* get_ee_position after Panda.reset: the host's fp64 value when given (pgx_config.ao_ee_neutral) */
-    const double ex = e.ao_ee_set ? e.ao_ee[0] : (double)ee.x, ey = e.ao_ee_set ? e.ao_ee[1] : (double)ee.y,
-                 ez = e.ao_ee_set ? e.ao_ee[2] : (double)ee.z;
+    const double ex = in.ex, ey = in.ey, ez = in.ez;
     Pcg64 g{0, 0, 0, 0, 0, 0};
     if (rec) g = pcg64_load(rec);
-    AoDraw d{env, episode, 0, rec ? &g : nullptr};
-    const V3 tc = ao_table_c(e), th = ao_table_h(e);
+    AoDraw d{in.seed, env, episode, 0, rec ? &g : nullptr};
+    const V3 tc = in.tc, th = in.th;
     double dummy[3] = {0.0, 0.0, 0.0};
     for (int i = 0;; i++) {
-        ao_hollow_sphere(e, d, 0.5, 0.8, true, goal);
+        ao_hollow_sphere(d, 0.5, 0.8, true, goal);
         if (i > 9999) { goal[0] = ex; goal[1] = ey; goal[2] = ez; break; }
         dummy[0] = goal[0]; dummy[1] = goal[1]; dummy[2] = goal[2];
         const V3 g = v3((float)goal[0], (float)goal[1], (float)goal[2]);
@@ -4213,9 +4229,9 @@ __device__ __noinline__ bool ao_reset(const PgxDevEnv& e, LT& L, int ln, int lan
         double P[3];
         bool placed = false;
         for (int it = 0; it < 10000; it++) {
-            const double rnd = ao_draw(e, d);
+            const double rnd = ao_draw(d);
             double sm[3];
-            ao_hollow_sphere(e, d, 0.1, 0.5, false, sm);
+            ao_hollow_sphere(d, 0.1, 0.5, false, sm);
             if (rnd > 0.5) { P[0] = sm[0] + goal[0]; P[1] = sm[1] + goal[1]; P[2] = sm[2] + goal[2]; }
             else { P[0] = ex + sm[0]; P[1] = ey + sm[1]; P[2] = ez + sm[2]; }
             const V3 Pf = v3((float)P[0], (float)P[1], (float)P[2]);
@@ -4235,10 +4251,10 @@ __device__ __noinline__ bool ao_reset(const PgxDevEnv& e, LT& L, int ln, int lan
         failed = failed || !placed;
         L.aoC[o][0][ln] = (float)P[0]; L.aoC[o][1][ln] = (float)P[1]; L.aoC[o][2][ln] = (float)P[2];
     }
-    const int n_active = 4 + (rec ? (int)pcg64_bounded(g, 1u) : (int)(ao_draw(e, d) * 2.0));
+    const int n_active = 4 + (rec ? (int)pcg64_bounded(g, 1u) : (int)(ao_draw(d) * 2.0));
     int perm[AO_N] = {0, 1, 2, 3, 4, 5};
     for (int j = AO_N - 1; j > 0; j--) {   /* Fisher-Yates, unrolled so perm stays in VGPRs */
-        int r = rec ? (int)pcg64_interval(g, (uint32_t)j) : (int)(ao_draw(e, d) * (double)(j + 1));
+        int r = rec ? (int)pcg64_interval(g, (uint32_t)j) : (int)(ao_draw(d) * (double)(j + 1));
         r = r > j ? j : r;
         int pj = 0, pr = 0;
 #pragma unroll
@@ -4445,7 +4461,14 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
             /* ReachAO step_check_collision (reach_ao.py:182-188): the check after substep st - 1
              * runs inside substep st's contact detection (the same pose); a hit stops the loop
              * before anything of substep st happens */
-            if (substep_g<OBJ, CONT, PART, AO, FULL>(mp, e, q, qd, tq, ob, L, ln, c, lk, AO && st > 0)) {
+            /* ReachAO (two waves per SIMD, 256 registers): the lane's row slot and lane index made opaque
+             * in every substep, so what derives from them (LDS addresses, lane masks) is recomputed
+             * there instead of hoisted out of the loop, spilled and reloaded in every substep
+             * (scratch 632 -> 280 B per lane with the reset's inputs passed by value and the
+             * collision check's table box opaque; PMC 93 -> 22 MB per ReachAO 8192 launch) */
+            int cl = c, esl = ln;
+            if constexpr (AO) asm volatile("" : "+v"(cl), "+v"(esl));
+            if (substep_g<OBJ, CONT, PART, AO, FULL>(mp, e, q, qd, tq, ob, L, esl, cl, lk, AO && st > 0)) {
                 collided = true;
                 break;
             }
@@ -4534,7 +4557,8 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
             ee_state(mr, q, qd, pos, vel);
             ao_caps(mr, q, *L, ln);
             uint64_t* rec = (e.pcg_on != nullptr && *e.pcg_on != 0) ? e.pcg + PGX_PCG64_WORDS * (size_t)i : nullptr;
-            if (ao_reset<WIDE != 0>(e, *L, ln, c, e.env_id_offset + (uint64_t)i, episode, pos, nullptr, nullptr, goal, rec,
+            const AoResetIn rin = ao_reset_in(e, pos);
+            if (ao_reset<WIDE != 0>(rin, *L, ln, c, e.env_id_offset + (uint64_t)i, episode, nullptr, nullptr, goal, rec,
                                     lead) &&
                 lead)
                 atomicOr(s.errors, PGX_ERR_AO_OBSTACLE);
@@ -4657,7 +4681,8 @@ __global__ __launch_bounds__(64) void reset_kernel(const PgxDevModel* __restrict
         ee_state(m, q, qd, pos, vel);
         ao_caps(m, q, *L, ln);
         uint64_t* rec = (e.pcg_on != nullptr && *e.pcg_on != 0) ? e.pcg + PGX_PCG64_WORDS * (size_t)i : nullptr;
-        if (ao_reset<false>(e, *L, ln, 0, e.env_id_offset + (uint64_t)i, episode, pos,
+        const AoResetIn rin = ao_reset_in(e, pos);
+        if (ao_reset<false>(rin, *L, ln, 0, e.env_id_offset + (uint64_t)i, episode,
                             inject_goal ? inject_goal + 3 * (size_t)i : nullptr,
                             inject_obj ? inject_obj + 3 * AO_N * (size_t)i : nullptr, goal, rec, true))
             atomicOr(s.errors, PGX_ERR_AO_OBSTACLE);

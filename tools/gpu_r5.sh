@@ -5,6 +5,7 @@
 #                         runtime-model library of that tree
 #   tests (unless NO_TESTS=1): pytest -m gpu (PGX_PYTEST_ARGS appended), then smoke()
 #   AB="abl/a.so abl/b.so" AB_CASES=...: tools/ab_libs.py timing of library builds
+#   PMC=1: tools/pmc_r5.sh (rocprofv3 --pmc passes over a short bench run) into gpurun_out/pmc_r5
 #   BENCH=1: bench.py with the driver's arguments (--steps 20 --warmup 5) and the defaults, then
 #            rocprofv3 --kernel-trace --stats of the driver-argument run
 set -o pipefail
@@ -42,7 +43,11 @@ if [ -z "$NO_TESTS" ]; then
   TEST_RC=$?
   grep -E "FAILED|ERROR" gpurun_out/pytest_gpu_$TAG.log | head -40
   tail -3 gpurun_out/pytest_gpu_$TAG.log
-  if [ $TEST_RC -ne 0 ] && [ $TEST_RC -ne 1 ]; then exit $TEST_RC; fi
+  if [ $TEST_RC -ne 0 ] && [ $TEST_RC -ne 1 ]; then if [ -n "$PMC" ]; then   # the PMC passes (tools/pmc_r5.sh), one counter group per rocprofv3 run
+  timeout -k 10 1000 bash tools/pmc_r5.sh > gpurun_out/pmc_$TAG.log 2>&1 || { tail -20 gpurun_out/pmc_$TAG.log; exit 1; }
+  tail -6 gpurun_out/pmc_$TAG.log
+fi
+exit $TEST_RC; fi
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { tail -20 gpurun_out/smoke_$TAG.log; exit 1; }
   cat gpurun_out/smoke_$TAG.log
 fi
@@ -64,5 +69,9 @@ if [ -n "$BENCH" ]; then
   cat gpurun_out/bench_$TAG.json
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1 || { tail -20 gpurun_out/prof_$TAG.log; exit 1; }
   find gpurun_out/prof_$TAG -name "*stats*"
+fi
+if [ -n "$PMC" ]; then   # the PMC passes (tools/pmc_r5.sh), one counter group per rocprofv3 run
+  timeout -k 10 1000 bash tools/pmc_r5.sh > gpurun_out/pmc_$TAG.log 2>&1 || { tail -20 gpurun_out/pmc_$TAG.log; exit 1; }
+  tail -6 gpurun_out/pmc_$TAG.log
 fi
 exit $TEST_RC

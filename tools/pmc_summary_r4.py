@@ -80,8 +80,9 @@ def main(src=os.path.join(ROOT, "gpurun_out", "pmc_r4"), round_tag="r04"):
             alg = her_alg()
         hbm = (2.0 * mean.get("FETCH_SIZE", 0.0) + mean.get("WRITE_SIZE", 0.0)) * 1024.0
         waves = mean.get("SQ_WAVES") or 0.0
-        names = sorted({r["Kernel_Name"].split("(")[0] for r in rows if frag in r["Kernel_Name"]
-                        and (grid is None or int(r["Grid_Size"]) == grid)})
+        # "void (anonymous namespace)::step_kernel<0, 0, 1, 0, 2>(PgxDevModel const*, ...)" -> the template id
+        names = sorted({r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
+                        for r in rows if frag in r["Kernel_Name"] and (grid is None or int(r["Grid_Size"]) == grid)})
         out = {
             "kernel": frag, "kernel_names": names, "num_envs": envs, "grid_threads": grid,
             "robot_points": ROBOT_POINTS.get(name),
@@ -91,8 +92,8 @@ def main(src=os.path.join(ROOT, "gpurun_out", "pmc_r4"), round_tag="r04"):
             "hbm_bytes_per_launch": hbm, "read_bytes_per_launch": 2.0 * mean.get("FETCH_SIZE", 0.0) * 1024.0,
             "write_bytes_per_launch": mean.get("WRITE_SIZE", 0.0) * 1024.0, "alg_bytes_per_launch": alg,
             "traffic_over_alg": hbm / alg if alg else None,
-            "source": f"tools/pmc_r4.sh + tools/pmc_summary_r4.py (rocprofv3 --pmc, one group per run), "
-                      f"profiles/{round_tag}/pmc",
+            "source": f"tools/pmc_{round_tag[0]}{round_tag[2:]}.sh + tools/pmc_summary_r4.py (rocprofv3 --pmc, one group "
+                      f"per run), profiles/{round_tag}/pmc",
         }
         if "SQ_INSTS_VALU" in mean:
             out["valu_instr_per_launch"] = mean["SQ_INSTS_VALU"]
