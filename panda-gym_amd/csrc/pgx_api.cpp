@@ -367,6 +367,9 @@ int pgx_create(const pgx_config* cfg, int device, pgx_handle* out) {
     e.sort_key = 1;    /* PGX_SORT_KEY=0: only the points past the register budget (A/B hook: PickAndPlace
                           16384 3.11 -> 3.73 ms, profiles/r04/ab_env_order_key.log) */
     if (const char* sk = std::getenv("PGX_SORT_KEY")) e.sort_key = std::atoi(sk) ? 1 : 0;
+    e.sort_segs = 0;   /* PGX_SORT_SEGS=1: one global heavy-first order (A/B hook; default: per-XCD segments) */
+    if (const char* sg = std::getenv("PGX_SORT_SEGS")) e.sort_segs = std::atoi(sg) == 1 ? 1 : 0;
+    e.perm_segs = 1;
     e.task = cfg->task;
     e.control = cfg->control;
     e.reward = cfg->reward;

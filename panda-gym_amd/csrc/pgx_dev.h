@@ -83,7 +83,9 @@ struct PgxDevEnv {
     int32_t* perm_buf;
     int32_t sort_mode;
     int32_t sort_key;              /* PGX_SORT_KEY: 1 all robot points (default), 0 only those past CG */
+    int32_t sort_segs;             /* PGX_SORT_SEGS: 0 auto (8 per-XCD segments when N divides), 1 one global order */
     const int32_t* perm;
+    int32_t perm_segs;             /* the launch's segments: 8 = perm is heavy-first within each XCD's env range */
 };
 
 struct PgxDevState {

@@ -4318,7 +4318,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     const int N = e.n_envs;
     /* heavy-first order (e.perm, pgx_launch_step): dispatch order = block order, so the blocks are
      * not dealt out per XCD there; an env's result does not depend on its wave mates */
-    const int slot = (e.perm ? (int)blockIdx.x : xcd_block()) * (WIDE ? EPW : 64) + ln;
+    const int slot = ((e.perm && e.perm_segs == 1) ? (int)blockIdx.x : xcd_block()) * (WIDE ? EPW : 64) + ln;
     if (slot >= N) return;
     const int i = e.perm ? e.perm[slot] : slot;
     /* the prologue loads index by a laundered copy of i: the compiler cannot reuse their
@@ -4781,10 +4781,13 @@ __global__ __launch_bounds__(SORT_BLOCK) void env_sort_keys_kernel(PgxDevState s
     }
 }
 __global__ __launch_bounds__(SORT_BLOCK) void env_sort_scatter_kernel(int N, const uint8_t* keys, const int32_t* blk,
-                                                                      int32_t* perm) {
+                                                                      int32_t* perm, int segs) {
     __shared__ int32_t base[SORT_BINS];
     __shared__ int32_t wc[SORT_BLOCK / 64][SORT_BINS];
-    const int nb = (int)gridDim.x, me = (int)blockIdx.x;
+    /* segs > 1 (N a multiple of segs x SORT_BLOCK): the envs sort within segs equal contiguous
+     * segments (segment x = the env range XCD x steps unsorted, xcd_block), each heavy-first */
+    const int bps = (int)gridDim.x / segs, me = (int)blockIdx.x, sg = me / bps;
+    const int b0 = sg * bps, nb = b0 + bps;
     const int i = me * SORT_BLOCK + threadIdx.x, lane = (int)__lane_id(), w = (int)threadIdx.x / 64;
     /* per bin: the total over all blocks and over the blocks before this one; thread t reads the
      * counts of blocks t, t + 256, ... (independent loads), then a wave and a block reduction */
@@ -4792,7 +4795,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void env_sort_scatter_kernel(int N, con
     int tot[SORT_BINS], pre[SORT_BINS];
 #pragma unroll
     for (int k = 0; k < SORT_BINS; k++) { tot[k] = 0; pre[k] = 0; }
-    for (int bb = threadIdx.x; bb < nb; bb += SORT_BLOCK) {
+    for (int bb = b0 + threadIdx.x; bb < nb; bb += SORT_BLOCK) {
 #pragma unroll
         for (int k = 0; k < SORT_BINS; k++) {
             const int c = blk[(size_t)bb * SORT_BINS + k];
@@ -4816,7 +4819,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void env_sort_scatter_kernel(int N, con
         for (int kk = SORT_BINS - 1; kk > k; kk--)
             for (int ww = 0; ww < SORT_BLOCK / 64; ww++) off += red[ww][0][kk];
         for (int ww = 0; ww < SORT_BLOCK / 64; ww++) off += red[ww][1][k];
-        base[k] = off;
+        base[k] = off + sg * (N / segs);
     }
     const int key = i < N ? (int)keys[i] : -1;
     uint64_t mine_k = 0ull;
@@ -4910,9 +4913,12 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
             int32_t* blk = e.perm_buf + e.n_envs + (e.n_envs + 3) / 4;
             hipLaunchKernelGGL(env_sort_keys_kernel, dim3(nb), dim3(SORT_BLOCK), 0, st, s, e.n_envs, rb, e.sort_key, keys,
                                blk);
+            /* per-XCD segments when the batch divides: a wave's env rows then stay in one L2's range */
+            const int segs = (e.sort_segs != 1 && e.n_envs % (8 * SORT_BLOCK) == 0) ? 8 : 1;
             hipLaunchKernelGGL(env_sort_scatter_kernel, dim3(nb), dim3(SORT_BLOCK), 0, st, e.n_envs,
-                               (const uint8_t*)keys, (const int32_t*)blk, e.perm_buf);
+                               (const uint8_t*)keys, (const int32_t*)blk, e.perm_buf, segs);
             es.perm = e.perm_buf;
+            es.perm_segs = segs;
         }
         const PgxDevEnv& e = es;
         /* the object tasks' per-pair manifold kernels run one wave per SIMD at every batch: their
