@@ -735,6 +735,16 @@ constexpr int robot_budget() {
     return (W == 64 || !FULL) ? PGX_ROBOT_POINTS_ONE_LANE : (OBJ ? PGX_ROBOT_POINTS : PGX_ROBOT_POINTS_ARM);
 }
 static_assert(PGX_ROBOT_POINTS_ONE_LANE == CG, "the one-lane solver holds CG robot points");
+/* robot points whose rows live in VGPRs as Delassus lanes (the rest are substep_g's extra rows,
+ * a 16-lane reduction each): CG, and PGX_CGR_OBJ for the object tasks' per-pair budget kernels,
+ * whose heavy envs (fingers on the cube: 5-7 points, profiles/r05/point_hist.log) set the launch */
+#ifndef PGX_CGR_OBJ
+#define PGX_CGR_OBJ 6
+#endif
+template <int W, int OBJ, int FULL>
+constexpr int robot_regs() {
+    return (W != 64 && OBJ && FULL) ? PGX_CGR_OBJ : CG;
+}
 
 constexpr int CACHE_N = 2 * PGX_CONTACT_SLOTS;
 constexpr int CACHE1 = 2 * CG;           /* robot slots of the cache */
@@ -767,8 +777,9 @@ struct ContactLdsT {
     /* wide layout: rows 3 p + dir of point p (object-scene points first when OBJ): the
      * register rows (NQR, robot points < CG) and every row (NQX, robot points < RB) */
     static constexpr int P0 = OBJ ? CG : 0;
-    static constexpr int NQR = 3 * (P0 + CG), NQX = 3 * (P0 + RB);
-    static constexpr int XR = (W == 64 || RB <= CG) ? 1 : NQX - NQR;   /* extra rows */
+    static constexpr int CGR = robot_regs<W, OBJ, FULL>();   /* robot points in registers */
+    static constexpr int NQR = 3 * (P0 + CGR), NQX = 3 * (P0 + RB);
+    static constexpr int XR = (W == 64 || RB <= CGR) ? 1 : NQX - NQR;   /* extra rows */
     /* Bullet's persistent manifolds of the robot's cube / obstacle pairs (FULL, the wide layout): the
      * pool's capacity in points (pgx.h PGX_MANIFOLD_POOL / _AO; Reach has no such pair) */
     static constexpr int MP = (W == 64 || !FULL) ? 1 : (OBJ ? PGX_MANIFOLD_POOL : PGX_MANIFOLD_POOL_AO);
@@ -810,7 +821,7 @@ struct ContactLdsT {
     float xrhs[XR][W], xlam[XR][W], xlam0[XR][W], xfk[XR][W], xjinv[XR][W];
     /* wide layout, the register points' normal rows: jinv (the cache's impulse lambda' jinv)
      * and lambda' at the solve's start (a redo), kept here through the sweeps */
-    float pjn[W == 64 ? 1 : P0 + CG][W], pl0[W == 64 ? 1 : P0 + CG][W];
+    float pjn[W == 64 ? 1 : P0 + CGR][W], pl0[W == 64 ? 1 : P0 + CGR][W];
     /* wide layout, object tasks: the limit rows' rhs' and lambda' of the all-rows solve (in
      * registers beside the 24 contact rows they set the kernel's register peak) */
     float lrhs[(W == 64 || !OBJ) ? 1 : PGX_N_ROWS - PGX_NJ][W], llam[(W == 64 || !OBJ) ? 1 : PGX_N_ROWS - PGX_NJ][W];
@@ -2735,8 +2746,9 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
 
     /* ---- contact rows: per lane J_c and (M^-1 J^T)_c, per row rhs / jinv / den / lambda */
     constexpr int P0 = OBJ ? CG : 0;            /* group-1 rows follow group 0's */
-    constexpr int NP = P0 + (CONT ? CG : 0);
-    constexpr int RB = CONT ? ContactLdsGT<OBJ, FULL>::RB : CG;   /* robot budget: points CG.. are the extra rows */
+    constexpr int CGR = ContactLdsGT<OBJ, FULL>::CGR;   /* robot points with register (Delassus) rows */
+    constexpr int NP = P0 + (CONT ? CGR : 0);
+    constexpr int RB = CONT ? ContactLdsGT<OBJ, FULL>::RB : CGR;   /* robot budget: points CGR.. are the extra rows */
     constexpr int NQR = ContactLdsGT<OBJ, FULL>::NQR;
     constexpr int NC_ = OBJ ? 13 : NJ;          /* generalized coordinates in lanes */
     /* extra points run in the sweep: multiples of XSTEP, one sweep copy per multiple (round 4:
@@ -2745,8 +2757,8 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
      * a runtime loop over the points instead, row data in LDS: Push 3.0 ms,
      * profiles/r04/ab_extra_rows_*.log) */
     constexpr int XSTEP = 1;
-    int n1x = 0;                                /* the wave's largest robot point count, when above CG */
-    int nxr = 0;                                /* extra points the sweep runs: n1x - CG rounded up to XSTEP */
+    int n1x = 0;                                /* the wave's largest robot point count, when above CGR */
+    int nxr = 0;                                /* extra points the sweep runs: n1x - CGR rounded up to XSTEP */
     float cJ[NP > 0 ? NP : 1][3], cR[NP > 0 ? NP : 1][3], crhs[NP > 0 ? NP : 1][3], cjinv[NP > 0 ? NP : 1][3];
     float cden[NP > 0 ? NP : 1][3], clam[NP > 0 ? NP : 1][3];
     float pmu[NP > 0 ? NP : 1];   /* the points' combined lateral friction (object scene: m.friction) */
@@ -2758,18 +2770,21 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         n1 = L.cnt[1][es];
         const float erp_dt = m.contact_erp * m.inv_dt;
         /* the warm-start cache slots, read once for every point (ids, impulses) */
-        float cid0[CG], cim0[CG], cid1[CG], cim1[CG];
+        float cid0[CG], cim0[CG], cid1[CGR], cim1[CGR];
 #pragma unroll
         for (int s2 = 0; s2 < CG; s2++) {
             cid0[s2] = OBJ ? L.cache[2 * s2][es] : -1.0f;
             cim0[s2] = OBJ ? L.cache[2 * s2 + 1][es] : 0.0f;
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < CGR; s2++) {
             cid1[s2] = L.cache[CACHE1 + 2 * s2][es];
             cim1[s2] = L.cache[CACHE1 + 2 * s2 + 1][es];
         }
-        auto warm_of = [&](const float* ids, const float* ims, float id) __attribute__((always_inline)) {
+        auto warm_of = [&](const float* ids, const float* ims, auto n_c, float id) __attribute__((always_inline)) {
             float w = 0.0f;
 #pragma unroll
-            for (int s2 = 0; s2 < CG; s2++) w = ids[s2] == id ? m.warmstart * ims[s2] : w;
+            for (int s2 = 0; s2 < decltype(n_c)::value; s2++) w = ids[s2] == id ? m.warmstart * ims[s2] : w;
             return w;
         };
 #pragma unroll
@@ -2780,7 +2795,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             const float4 r4 = L.g0q[k][0][es];
             const V3 r = v3(r4.x, r4.y, r4.z);
             const float id = L.g0id[k][es];
-            const float warm = warm_of(cid0, cim0, id);
+            const float warm = warm_of(cid0, cim0, IC<CG>{}, id);
 #pragma unroll
             for (int dir = 0; dir < 3; dir++) {
                 const V3 lin = dir == 0 ? v3(0, 0, 1) : (dir == 1 ? v3(0, -1, 0) : v3(1, 0, 0));
@@ -2809,9 +2824,9 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         const V3 zc = pick_v3(z), oc = pick_v3(o);
         /* the points' records read up front, one batch behind one wait (read inside each point's
          * branch they cost a wait per point) */
-        V3 gP[CG], gN[CG], gRb[CG];
-        int gJ[CG], gW[CG];
-        float gId[CG], gD[CG];
+        V3 gP[CGR], gN[CGR], gRb[CGR];
+        int gJ[CGR], gW[CGR];
+        float gId[CGR], gD[CGR];
         auto read_point = [&](int k) __attribute__((always_inline)) {
             gP[k] = v3(L.g1p[k][0][es], L.g1p[k][1][es], L.g1p[k][2][es]);
             gN[k] = v3(L.g1n[k][0][es], L.g1n[k][1][es], L.g1n[k][2][es]);
@@ -2824,15 +2839,15 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         /* a manifold point's warm start is its own applied impulse (btManifoldPoint::m_appliedImpulse
          * x the warm-starting factor), a fresh table point's its feature's cached one */
         auto warm_pt = [&](int w, float id) __attribute__((always_inline)) {
-            return (PERS && w >= 0) ? m.warmstart * L.mimp[w < 0 ? 0 : w][es] : warm_of(cid1, cim1, id);
+            return (PERS && w >= 0) ? m.warmstart * L.mimp[w < 0 ? 0 : w][es] : warm_of(cid1, cim1, IC<CGR>{}, id);
         };
         /* (ReachAO: points are rare and the o2 kernel's registers scarce: read per point) */
         if (!AO && __any(n1 > 0)) {
 #pragma unroll
-            for (int k = 0; k < CG; k++) read_point(k);
+            for (int k = 0; k < CGR; k++) read_point(k);
         }
 #pragma unroll
-        for (int k = 0; k < (CONT ? CG : 0); k++) {
+        for (int k = 0; k < (CONT ? CGR : 0); k++) {
             const int p = P0 + k;
             act[p] = k < n1;
 #pragma unroll
@@ -2887,18 +2902,18 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 }
             }
         }
-        /* ---- robot points CG..RB-1 (an env with more than CG robot points: fp64 oracle under
+        /* ---- robot points CGR..RB-1 (an env with more than CGR robot points: fp64 oracle under
          * the random policy, Push / PickAndPlace 1.2 % of substeps, Reach 1e-5): the same row
          * setup, kept in LDS for the solve -- (J, M^-1 J^T jinv) per coordinate lane in xd, the
          * row scalars per env -- and solved after the register rows of each half-sweep
          * (extra_rows below).  The sweep runs a compile-time number of extra points, the wave's
          * count rounded up to XSTEP: the rows past an env's own count are zero rows (bounds 0,
          * delta' = 0 exactly), so the points the wave lacks are written as zero rows too. */
-        if constexpr (RB > CG) {
-            for (int k = CG; k < RB && __any(k < n1); k++) n1x = k + 1;
+        if constexpr (RB > CGR) {
+            for (int k = CGR; k < RB && __any(k < n1); k++) n1x = k + 1;
             n1x = __builtin_amdgcn_readfirstlane(n1x);
-            nxr = n1x > CG ? (n1x - CG + XSTEP - 1) / XSTEP * XSTEP : 0;
-            for (int k = CG; k < CG + nxr; k++) {   /* wave-uniform */
+            nxr = n1x > CGR ? (n1x - CGR + XSTEP - 1) / XSTEP * XSTEP : 0;
+            for (int k = CGR; k < CGR + nxr; k++) {   /* wave-uniform */
                 if (k >= n1x) {
 #pragma unroll
                     for (int dir = 0; dir < 3; dir++) {
@@ -2980,12 +2995,11 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     constexpr int NQ = WROWS ? 3 * NP : 1;      /* 12 (Reach), 24 (object tasks) */
     constexpr bool TWO = NQ > GW;
     constexpr int NC = OBJ ? 13 : NJ;           /* generalized coordinates in lanes */
-    bool g1k_any[CG], g0k_any[CG];
+    bool g1k_any[CGR], g0k_any[CG];
 #pragma unroll
-    for (int k = 0; k < CG; k++) {
-        g1k_any[k] = CONT && __any(k < n1);
-        g0k_any[k] = CONT && OBJ && __any(k < n0);
-    }
+    for (int k = 0; k < CGR; k++) g1k_any[k] = CONT && __any(k < n1);
+#pragma unroll
+    for (int k = 0; k < CG; k++) g0k_any[k] = CONT && OBJ && __any(k < n0);
     /* rows of point p live in the wave (slots fill from 0) */
     auto row_live = [&](int pp) __attribute__((always_inline)) { return pp < P0 ? g0k_any[pp] : g1k_any[pp - P0]; };
     float gw = 0.0f, gw2 = 0.0f, Wm[NJ], Wm2[NJ], Wc[NQ], Wc2[NQ];
@@ -3056,10 +3070,10 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         }
     }
     /* the extra rows' scalars into lanes (row x: lane x % 16 of register x / 16) */
-    constexpr int XB = (RB > CG) ? (3 * (RB - CG) + GW - 1) / GW : 1;
+    constexpr int XB = (RB > CGR) ? (3 * (RB - CGR) + GW - 1) / GW : 1;
     float xs_rhs[XB], xs_lam[XB], xs_fk[XB], xs_jinv[XB];
     auto load_xs = [&](bool start) __attribute__((always_inline)) {
-        if constexpr (RB > CG) {
+        if constexpr (RB > CGR) {
             ContactLdsGT<OBJ, FULL>& L = *Lp;
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 #pragma unroll
@@ -3078,7 +3092,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     };
 #pragma unroll
     for (int b = 0; b < XB; b++) { xs_rhs[b] = 0.0f; xs_lam[b] = 0.0f; xs_fk[b] = 0.0f; xs_jinv[b] = 0.0f; }
-    if (RB > CG && nxr > 0) load_xs(true);
+    if (RB > CGR && nxr > 0) load_xs(true);
     PGX_PROF_MARK(23);
 
     /* ---- motor / limit rows (as substep()): per row rhs and lambda, per dof jinv / den */
@@ -3285,7 +3299,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
      * are s_cmp on it (a per-point bool there turns into a VALU mask round trip per row) */
     int n1w = 0;
 #pragma unroll
-    for (int k = 0; k < CG; k++) n1w = g1k_any[k] ? k + 1 : n1w;
+    for (int k = 0; k < CGR; k++) n1w = g1k_any[k] ? k + 1 : n1w;
     n1w = __builtin_amdgcn_readfirstlane(n1w);
     const bool g0_any = CONT && OBJ && __any(n0 > 0);
     const bool g1_any = CONT && __any(n1 > 0);
@@ -3294,7 +3308,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
      * [lambda', lambda'] with lambda' = 0 -> delta' = 0, bit for bit), so no per-point branch
      * sits inside the sweep.  The object-scene rows (P0 points, a resting cube has 4) run in
      * every sweep of the object tasks, idle points predicated the same way. */
-    /* the extra rows (robot points CG..CG+NX-1) of one half-sweep, after the register rows in the
+    /* the extra rows (robot points CGR..CGR+NX-1) of one half-sweep, after the register rows in the
      * same order as the oracle's (normal rows, then friction rows; points by id): the row
      * velocity by a 16-lane reduction (no Delassus lane), (J, M^-1 J^T jinv) per coordinate lane
      * from LDS (one ds_read_b64, independent of the chain: straight-line code, no branch, so the
@@ -3306,7 +3320,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     int rcol = c;   /* the coordinate of lane c's R entry (MODE 3 slot lanes: their dof's) */
     auto extra_rows = [&](auto fr_c, auto nx_c, auto g2_c, float& resid) __attribute__((always_inline)) {
         constexpr int FR = decltype(fr_c)::value, NX = decltype(nx_c)::value;
-        if constexpr (WROWS && RB > CG && NX > 0) {
+        if constexpr (WROWS && RB > CGR && NX > 0) {
             ContactLdsGT<OBJ, FULL>& L = *Lp;
             const float gvb = gv;
             sfor<0, NX>([&](auto kc) __attribute__((always_inline)) {
@@ -3372,7 +3386,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                 });
             }
             if (NW < 0 && !g1_any) continue;
-            sfor<0, (CONT ? (NW >= 0 ? NW : CG) : 0)>([&](auto kc) __attribute__((always_inline)) {
+            sfor<0, (CONT ? (NW >= 0 ? NW : CGR) : 0)>([&](auto kc) __attribute__((always_inline)) {
                 constexpr int k = decltype(kc)::value;
                 if (NW >= 0 || k < n1w) {
                     if (fr) {
@@ -3441,7 +3455,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         constexpr int MODE = decltype(mode_c)::value;   /* 0 far, 1 speculative, 2 all rows, 3 partial */
         constexpr int NW = decltype(nw_c)::value;
         constexpr int K = decltype(k_c)::value;         /* MODE 3: slots in use */
-        /* NX: extra robot points (past CG) the sweep runs, 0 or a multiple of XSTEP */
+        /* NX: extra robot points (past CGR) the sweep runs, 0 or a multiple of XSTEP */
         constexpr bool G2 = TWO && (NW < 0 || 3 * (P0 + NW) > GW);
         const IC<G2 ? 1 : 0> g2_c{};
         for (int it = 0; it < n_it; it += 2) {
@@ -3481,24 +3495,25 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         }
     };
     /* the robot point count fixed at compile time (above) for every mode but far; the extra
-     * points (past CG) only in the speculative and all-rows solves (the partial one hands a wave
+     * points (past CGR) only in the speculative and all-rows solves (the partial one hands a wave
      * with extra points to the all-rows solve) */
     auto solve_w = [&](auto mode_c, auto k_c) __attribute__((always_inline)) {
         constexpr int MODE = decltype(mode_c)::value;
         if constexpr (WROWS) {
             if (n1w == 0) solve(mode_c, IC<0>{}, k_c, IC<0>{});
             else if (n1w <= 2) solve(mode_c, IC<2>{}, k_c, IC<0>{});
-            else if constexpr (RB > CG && MODE != 3) {
+            else if (CGR > 4 && n1w <= 4) solve(mode_c, IC<(CGR > 4 ? 4 : CGR)>{}, k_c, IC<0>{});
+            else if constexpr (RB > CGR && MODE != 3) {
                 if (nxr == 0) {
-                    solve(mode_c, IC<CG>{}, k_c, IC<0>{});
+                    solve(mode_c, IC<CGR>{}, k_c, IC<0>{});
                 } else {   /* one sweep copy per multiple of XSTEP (the wave's count rounded up) */
-                    sfor<1, (RB - CG) / XSTEP + 1>([&](auto ic) __attribute__((always_inline)) {
+                    sfor<1, (RB - CGR) / XSTEP + 1>([&](auto ic) __attribute__((always_inline)) {
                         constexpr int NXC = decltype(ic)::value * XSTEP;
-                        if (nxr == NXC) solve(mode_c, IC<CG>{}, k_c, IC<NXC>{});
+                        if (nxr == NXC) solve(mode_c, IC<CGR>{}, k_c, IC<NXC>{});
                     });
                 }
             } else {
-                solve(mode_c, IC<CG>{}, k_c, IC<0>{});
+                solve(mode_c, IC<CGR>{}, k_c, IC<0>{});
             }
         } else {
             solve(mode_c, IC<-1>{}, k_c, IC<0>{});
@@ -3626,7 +3641,7 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                     clam[p][1] = 0.0f;
                     clam[p][2] = 0.0f;
                 }
-                if (RB > CG && nxr > 0) load_xs(false);
+                if (RB > CGR && nxr > 0) load_xs(false);
                 init_bounds();
                 solve_w(IC<2>{}, IC<0>{});
             }
@@ -3657,11 +3672,14 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     if (CONT) { /* contact cache: this step's features and normal impulses */
         ContactLdsGT<OBJ, FULL>& L = *Lp;
         /* every slot's id and jinv read unconditionally (one batch, one wait), then selected */
-        float gid0[CG], pj0[CG], gid1[CG], pj1[CG];
+        float gid0[CG], pj0[CG], gid1[CGR], pj1[CGR];
 #pragma unroll
         for (int s = 0; s < CG; s++) {
             gid0[s] = OBJ ? L.g0id[s][es] : -1.0f;
             pj0[s] = OBJ ? L.pjn[s][es] : 0.0f;
+        }
+#pragma unroll
+        for (int s = 0; s < CGR; s++) {
             gid1[s] = L.g1id[s][es];
             pj1[s] = L.pjn[P0 + s][es];
         }
@@ -3669,18 +3687,21 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         for (int s = 0; s < CG; s++) {
             L.cache[2 * s][es] = (OBJ && s < n0) ? gid0[s] : -1.0f;
             L.cache[2 * s + 1][es] = (OBJ && s < n0) ? clam[s][0] * pj0[s] : 0.0f;
+        }
+#pragma unroll
+        for (int s = 0; s < CGR; s++) {
             L.cache[CACHE1 + 2 * s][es] = s < n1 ? gid1[s] : -1.0f;
             L.cache[CACHE1 + 2 * s + 1][es] = s < n1 ? clam[P0 + s][0] * pj1[s] : 0.0f;
         }
-        if constexpr (RB > CG) {
-            if (n1x > CG) {   /* the extra normal rows' impulses: lane x % 16 of xs_lam[x / 16] to LDS */
+        if constexpr (RB > CGR) {
+            if (n1x > CGR) {   /* the extra normal rows' impulses: lane x % 16 of xs_lam[x / 16] to LDS */
 #pragma unroll
                 for (int b = 0; b < XB; b++)
-                    if (GW * b + c < 3 * (n1x - CG)) L.xlam[GW * b + c][es] = xs_lam[b];
+                    if (GW * b + c < 3 * (n1x - CGR)) L.xlam[GW * b + c][es] = xs_lam[b];
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             }
-            for (int s = CG; s < RB; s++) {
-                const int xq = 3 * (s - CG);
+            for (int s = CGR; s < RB; s++) {
+                const int xq = 3 * (s - CGR);
                 L.cache[CACHE1 + 2 * s][es] = s < n1 ? L.g1id[s][es] : -1.0f;
                 L.cache[CACHE1 + 2 * s + 1][es] = s < n1 ? L.xlam[xq][es] * L.xjinv[xq][es] : 0.0f;
             }
