@@ -741,9 +741,12 @@ static_assert(PGX_ROBOT_POINTS_ONE_LANE == CG, "the one-lane solver holds CG rob
 #ifndef PGX_CGR_OBJ
 #define PGX_CGR_OBJ 6
 #endif
+#ifndef PGX_CGR_ARM
+#define PGX_CGR_ARM 4
+#endif
 template <int W, int OBJ, int FULL>
 constexpr int robot_regs() {
-    return (W != 64 && OBJ && FULL) ? PGX_CGR_OBJ : CG;
+    return (W != 64 && FULL) ? (OBJ ? PGX_CGR_OBJ : PGX_CGR_ARM) : CG;
 }
 
 constexpr int CACHE_N = 2 * PGX_CONTACT_SLOTS;
