@@ -741,9 +741,13 @@ static_assert(PGX_ROBOT_POINTS_ONE_LANE == CG, "the one-lane solver holds CG rob
 #ifndef PGX_CGR_OBJ
 #define PGX_CGR_OBJ 6
 #endif
+/* the arm tasks' per-pair budget kernels (Reach, ReachAO): four -- eight measured slower (the
+ * rows' build), and two too: the launches whose waves hold 3-5 points then run reduction rows
+ * (Reach 4096 0.390 -> 0.400 ms, ReachAO 8192 0.777 -> 0.984 ms; profiles/r05/ab_register_points_*) */
 #ifndef PGX_CGR_ARM
 #define PGX_CGR_ARM 4
 #endif
+static_assert(PGX_CGR_ARM >= 2 && PGX_CGR_OBJ >= 2, "the sweeps' point counts are 0, 2, 4 (<= the register budget)");
 template <int W, int OBJ, int FULL>
 constexpr int robot_regs() {
     return (W != 64 && FULL) ? (OBJ ? PGX_CGR_OBJ : PGX_CGR_ARM) : CG;
@@ -3503,9 +3507,11 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     auto solve_w = [&](auto mode_c, auto k_c) __attribute__((always_inline)) {
         constexpr int MODE = decltype(mode_c)::value;
         if constexpr (WROWS) {
+            /* (n1w counts register points only: a wave with extra points has n1w = CGR, which is 2
+             * for the arm tasks, so the extra-point copies are chosen by nxr first) */
             if (n1w == 0) solve(mode_c, IC<0>{}, k_c, IC<0>{});
-            else if (n1w <= 2) solve(mode_c, IC<2>{}, k_c, IC<0>{});
-            else if (CGR > 4 && n1w <= 4) solve(mode_c, IC<(CGR > 4 ? 4 : CGR)>{}, k_c, IC<0>{});
+            else if (nxr == 0 && n1w <= 2) solve(mode_c, IC<2>{}, k_c, IC<0>{});
+            else if (CGR > 4 && nxr == 0 && n1w <= 4) solve(mode_c, IC<(CGR > 4 ? 4 : CGR)>{}, k_c, IC<0>{});
             else if constexpr (RB > CGR && MODE != 3) {
                 if (nxr == 0) {
                     solve(mode_c, IC<CGR>{}, k_c, IC<0>{});
