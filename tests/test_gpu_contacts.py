@@ -521,6 +521,62 @@ def test_contact_budget_cases_keep_all_points(pg, oracle, case, lanes):
     venv.close()
 
 
+def test_object_kernel_points_past_the_register_budget(pg, oracle):
+    """Envs holding more robot points than the object kernels keep in register (Delassus) rows --
+    PGX_CGR_OBJ = 6; the rest are the reduction rows read from LDS -- are rare under the random
+    policy (0.015 % of Push env-steps, profiles/r05/point_hist.log), so a test over a few hundred
+    envs may never reach them: found in a 4096-env steady-state rollout, their pre-step states are
+    copied into a small handle and stepped once against the oracle from the same state (an env's
+    result does not depend on its wave mates).  Bar: 1e-4, or the oracle's own move under a
+    rounding-level perturbation of its input (the one-step tests' outlier rule)."""
+    from oracle import oracle as orc
+
+    n, keys = 4096, ("q", "qd", "qc", "goal", "object", "contacts", "elapsed", "episode", "manifolds")
+    big = pg.PandaVecEnv("PandaPush-v3", num_envs=n, device="cuda:0", seed=5)
+    big.reset_tensors(episode_phase="staggered")
+    found = []
+    for t in range(100):
+        st = big.state()
+        pre = {k: st[k].clone() for k in keys}
+        a = big.sample_actions(t).clone()
+        big.step_tensors(a)
+        cnt = (big.state()["contacts"][2 * orc.OBJECT_POINTS::2] >= 0).sum(0)
+        idx = torch.nonzero(cnt > 6).flatten()
+        if len(idx):
+            found.append(({k: pre[k][..., idx] for k in keys}, a[idx]))
+        if sum(len(f[1]) for f in found) >= 12:
+            break
+    big.close()
+    assert found, "no env held more than six robot points"
+    acts = torch.cat([f[1] for f in found], dim=0)
+    m = acts.shape[0]
+    small = pg.PandaVecEnv("PandaPush-v3", num_envs=m, device="cuda:0", seed=5)
+    small.reset_tensors()
+    st = small.state()
+    for k in keys:
+        st[k].copy_(torch.cat([f[0][k] for f in found], dim=-1))
+    st["elapsed"].zero_()   # no TimeLimit reset inside the compared step
+    ref = oracle.OracleVecEnv(small._cfg, m)
+    _state_to_oracle(small, ref)
+    saved = (ref.q.copy(), ref.qd.copy(), ref.goal.copy(), ref.obj.copy(), ref.elapsed.copy(), ref.episode.copy())
+    small.step_tensors(acts)
+    out = ref.step(acts.cpu().numpy())
+    held = (small.state()["contacts"][2 * orc.OBJECT_POINTS::2] >= 0).sum(0).cpu().numpy()
+    assert held.max() > 6, held                        # the step ran rows past the register budget
+    obs, ag = small.obs.cpu().numpy(), small.achieved_goal.cpu().numpy()
+    e_ee = np.abs(obs[:, :3] - out["obs"][:, :3]).max(axis=1)
+    e_ag = np.abs(ag - out["ag"]).max(axis=1)
+    print(f"\n{m} envs past six robot points (held {held.tolist()}): max |ee| {e_ee.max():.2e}, |object| {e_ag.max():.2e}")
+    cfg = type(small._cfg).from_buffer_copy(small._cfg)
+    for i in np.nonzero(np.maximum(e_ee, e_ag) > 1e-4)[0]:
+        rec = {"state": tuple(x[i:i + 1].copy() for x in saved), "action": acts.cpu().numpy()[i:i + 1],
+               "ee": out["obs"][i, :3].copy(), "ag": out["ag"][i].copy()}
+        s_ee, s_ag = _self_sensitivity(oracle, cfg, rec, trials=32)
+        assert e_ee[i] <= 1e-2 and e_ag[i] <= 1e-2, (i, e_ee[i], e_ag[i])
+        assert e_ee[i] <= max(1e-4, s_ee) and e_ag[i] <= max(1e-4, s_ag), (i, e_ee[i], s_ee, e_ag[i], s_ag)
+    small.close()
+
+
 def abi_budget(case):
     from panda_gym_amd import abi
 
