@@ -1,6 +1,8 @@
 """GPU: the heavy-first env order of the per-pair manifold kernels (PGX_SORT_ENVS)
 changes which envs share a wave, never an env's result: the same rollout with the order forced on
-and forced off gives the same bits -- state, observations, rewards, flags -- at every step.  The
+and forced off gives the same bits -- state, observations, rewards, flags -- at every step.  With
+the order on, the launch's permutation is checked against the keys the step read: stable,
+heavy-first, and (a batch that divides into eight 256-env segments) within each XCD's env range.  The
 step kernels are built for this (a wave's idle rows are exact no-ops, every env leaves the solve on
 its own residual, the speculative / partial solves equal the all-rows one bit for bit)."""
 import os
@@ -28,7 +30,10 @@ v.reset_tensors(seed=5)
 h = hashlib.sha256()
 heavy = 0
 moved = 0
+segs = 8 if n % 2048 == 0 else 1   # per-XCD segments when the batch divides (pgx_launch_step)
 for t in range(steps):
+    c0 = v.state()["contacts"].cpu().numpy()
+    keys0 = (c0[8:8 + 2 * 12:2] >= 0).sum(0)          # the sort key: robot points held before the step
     v.step_tensors(v.sample_actions(t))
     st = v.state()
     for k in ("q", "qd", "qc", "goal", "object", "contacts", "elapsed", "episode"):
@@ -42,6 +47,15 @@ for t in range(steps):
         perm = st["env_order"].cpu().numpy()
         assert np.array_equal(np.sort(perm), np.arange(n)), perm
         moved += int((perm != np.arange(n)).any())
+        if st["env_order"].numel() and moved:   # each segment's envs stay in it, most points first, stable
+            S = n // segs
+            for x in range(segs):
+                seg = perm[x * S:(x + 1) * S]
+                assert seg.min() >= x * S and seg.max() < (x + 1) * S, (x, seg)
+                k = keys0[seg]
+                assert np.all(k[:-1] >= k[1:]), (x, k)
+                tie = k[:-1] == k[1:]
+                assert np.all(seg[:-1][tie] < seg[1:][tie]), x
 print(h.hexdigest(), heavy, moved)
 '''
 
@@ -55,7 +69,8 @@ def _run(env_id, n, steps, mode):
     return digest, int(heavy), int(moved)
 
 
-@pytest.mark.parametrize("env_id,n", [("PandaPush-v3", 67), ("PandaPickAndPlace-v3", 256), ("PandaReachAO-v3", 130)])
+@pytest.mark.parametrize("env_id,n", [("PandaPush-v3", 67), ("PandaPickAndPlace-v3", 256), ("PandaReachAO-v3", 130),
+                                     ("PandaPickAndPlace-v3", 2048)])   # 2048: eight per-XCD segments
 def test_heavy_first_order_leaves_every_env_bit_identical(env_id, n):
     d_on, heavy, moved = _run(env_id, n, 40, "1")
     d_off, _, _ = _run(env_id, n, 40, "0")
