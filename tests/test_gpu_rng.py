@@ -145,6 +145,36 @@ def test_back_to_philox(pg):
     ref.close()
 
 
+def test_mode_switch_captured_in_a_default_torch_graph(pg):
+    """pgx_set_rng_streams(NULL) -- the mode word, written by a one-thread kernel, not a memset node
+    (a memset node replays garbage from its second launch under torch's
+    default capture, which destroys the graph after instantiating it) -- captured with a step into
+    a default torch.cuda.CUDAGraph: every replay switches to Philox and auto-resets from it, as a
+    Philox handle stepping eagerly does."""
+    n, seed = 16, 321
+    venv = pg.PandaVecEnv("PandaReach-v3", num_envs=n, device="cuda:0", seed=seed, max_episode_steps=1,
+                          reset_rng="pcg64")
+    ref = pg.PandaVecEnv("PandaReach-v3", num_envs=n, device="cuda:0", seed=seed, max_episode_steps=1)
+    venv.reset_tensors()
+    ref.reset_tensors()
+    zero = torch.zeros((n, 3), device="cuda:0")
+    venv.step_tensors(zero)          # warm-up outside the capture (pcg64 draws)
+    ref.step_tensors(zero)
+    g = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g):
+        assert venv.lib.pgx_set_rng_streams(venv._h, None, venv._stream()) == 0
+        venv.step_tensors(zero)
+    for _ in range(3):
+        g.replay()
+        ref.step_tensors(zero)
+        torch.cuda.synchronize()
+        assert np.array_equal(venv.state()["goal"].cpu().numpy(), ref.state()["goal"].cpu().numpy())
+    del g
+    venv.close()
+    ref.close()
+
+
 # the ReachAO goal r (sin t cos p, sin t sin p, cos t), r <= 0.8: a last-bit difference of the
 # device's sin / cos / cbrt moves a component by up to a few ulp of r, not of the component
 GOAL_TOL = 4 * 0.8 * np.finfo(np.float64).eps
