@@ -139,7 +139,7 @@ def test_struct_layout_matches_c(tmp_path):
     fields = {"pgx_model": ["n_rows", "jpos", "jrot", "mass", "lower", "upper"],
               "pgx_sim_params": ["dt", "ik_max_angle", "n_substeps", "flags"],
               "pgx_config": ["no_auto_reset", "seed", "base_pos", "joint_forces", "model", "params",
-                             "terminate_on_success", "collision_reward"],
+                             "terminate_on_success", "collision_reward", "ao_ee_neutral"],
               "pgx_step_out": ["terminal_achieved_goal", "terminal_desired_goal"],
               "pgx_replay_config": ["reward_type", "distance_threshold", "her_ratio", "seed"],
               "pgx_transition": ["next_obs", "done", "timeout"],
