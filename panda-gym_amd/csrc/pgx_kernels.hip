@@ -4351,6 +4351,14 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     const int slot = ((e.perm && e.perm_segs == 1) ? (int)blockIdx.x : xcd_block()) * (WIDE ? EPW : 64) + ln;
     if (slot >= N) return;
     const int i = e.perm ? e.perm[slot] : slot;
+#ifdef PGX_CHECK_PERM
+    /* debug builds (make dbg DBG=-DPGX_CHECK_PERM): the heavy-first permutation is a bijection of
+     * [0, N) (env_sort_scatter_kernel); an entry outside it would index every state row out of range */
+    if ((unsigned)i >= (unsigned)N) {
+        printf("pgx: perm[%d] = %d outside [0, %d)\n", slot, i, N);
+        __builtin_trap();
+    }
+#endif
     /* the prologue loads index by a laundered copy of i: the compiler cannot reuse their
      * 64-bit addresses for the epilogue stores and keep ~17 address pairs live across the
      * whole step (recomputing them at the end is a few adds) */
