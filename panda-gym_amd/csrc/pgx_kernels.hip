@@ -178,7 +178,25 @@ template <int W>
 __device__ __forceinline__ V3 lds3(const float (*a)[W], int ln) { return v3(a[0][ln], a[1][ln], a[2][ln]); }
 
 typedef float f2 __attribute__((ext_vector_type(2)));   /* packed fp32 pair (v_pk_*_f32) */
-constexpr int GW = 16;          /* lanes per env: one DPP row */
+/* PGS rows with packed (coordinate, Delassus) updates (pk_fma_acc), bit 0 joint rows, bit 1
+ * contact rows; per kernel family, as measured (profiles/r05/ab_packed_rows.log): the ReachAO
+ * kernels gain with the contact rows packed (0.779 -> 0.768 ms at 8192, scratch unchanged; both
+ * kinds 0.766 ms but 32 B more scratch per lane), every other kernel loses 0.4-4.6 % to the
+ * register pairs' alignment (more AGPR copies, or spills in the two-wave builds) */
+#ifndef PGX_PK
+#define PGX_PK 0
+#endif
+#ifndef PGX_PK_AO
+#define PGX_PK_AO 2
+#endif
+/* {a, b} += {ca, cb} s as one v_pk_fma_f32: each half is the fused multiply-add of the scalar
+ * form, bit for bit, in one issue instead of two (a PGS row's coordinate and Delassus updates) */
+__device__ __forceinline__ void pk_fma_acc(float& a, float& b, f2 cab, float s) {
+    const f2 r = __builtin_elementwise_fma(cab, (f2){s, s}, (f2){a, b});
+    a = r.x;
+    b = r.y;
+}
+constexpr int GW = 16;         /* lanes per env: one DPP row */
 constexpr int EPW = 64 / GW;    /* envs per wave */
 
 template <int V>
@@ -3159,6 +3177,13 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
      * coordinate updates take the columns pre-multiplied by jinv.  Chain per row:
      * v_sub_dpp -> med3 -> fmac (the next broadcast's source). */
     float mcs[NJ], wms[NJ], wms2[NJ];
+    /* PKM / PKC (WROWS): a joint (contact) row's coordinate and Delassus coefficients as one pair,
+     * {mcs, wms} ({cR, Wc}), so that the row's gv / gw updates are one pk_fma_acc.  Per kernel:
+     * the pairs' aligned registers raise the register peak, which costs more than the issue
+     * saved except in the ReachAO kernels (PGX_PK / PGX_PK_AO, above) */
+    constexpr int PK = AO ? PGX_PK_AO : PGX_PK;
+    constexpr bool PKM = WROWS && (PK & 1) != 0, PKC = WROWS && (PK & 2) != 0;
+    f2 mw[NJ], crw[NQ];
     /* motor rows: the shifted bound pair (lo' - lambda', hi' - lambda') tracked instead of
      * lambda', one v_pk_add_f32 per row update (lambda' itself is not needed after the solve:
      * joint rows are not warm-started); limit rows keep lambda' (fewer live registers) */
@@ -3208,8 +3233,12 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             lam[r] += delta;
         }
         const float sd = kind == 2 ? -delta : delta;
-        gv += mcs[d] * sd;
-        if constexpr (WROWS) gw += wms[d] * sd;
+        if constexpr (PKM) {
+            pk_fma_acc(gv, gw, mw[d], sd);
+        } else {
+            gv += mcs[d] * sd;
+            if constexpr (WROWS) gw += wms[d] * sd;
+        }
         if constexpr (TWO && decltype(g2_c)::value) gw2 += wms2[d] * sd;
         resid = fmaxf(resid, fabsf(delta));
     };
@@ -3264,6 +3293,14 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         for (int q = 0; q < NQ; q++) { Wc[q] = -Wc[q]; Wc2[q] = -Wc2[q]; }
 #pragma unroll
         for (int d = 0; d < NJ; d++) { wms[d] = -wms[d]; wms2[d] = -wms2[d]; }
+        if constexpr (PKM) {
+#pragma unroll
+            for (int d = 0; d < NJ; d++) mw[d] = (f2){mcs[d], wms[d]};
+        }
+        if constexpr (PKC) {
+#pragma unroll
+            for (int q = 0; q < NQ; q++) crw[q] = (f2){cR[q / 3][q % 3], Wc[q]};
+        }
     }
     /* shifted bounds as for the joint rows: delta' = clamp(rhs' - w, lo' - lambda', hi' - lambda').
      * A normal row's upper bound is +inf (0 with lambda' = 0 for an unusable row; in the object
@@ -3297,8 +3334,12 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         const float x = q < GW ? bcast16<q % GW>(gw) : bcast16<q % GW>(gw2);   /* rhs' - w */
         const float delta = __builtin_amdgcn_fmed3f(x, lo, hi);
         clam[p][dir] = lm + delta;
-        gv += cR[p][dir] * delta;
-        gw += Wc[q] * delta;
+        if constexpr (PKC) {
+            pk_fma_acc(gv, gw, crw[q], delta);
+        } else {
+            gv += cR[p][dir] * delta;
+            gw += Wc[q] * delta;
+        }
         if constexpr (TWO && decltype(g2_c)::value) gw2 += Wc2[q] * delta;
         resid = fmaxf(resid, fabsf(delta));
     };
@@ -3446,14 +3487,19 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
     constexpr int SL0 = OBJ ? 13 : NJ;   /* first slot lane: the first lane past the coordinates */
     unsigned dmask = 0u;
     float smcs[KMAX], swms[KMAX], swms2[KMAX], srh[KMAX][2], slhi[KMAX], slam[KMAX][2];
+    f2 smw[KMAX];   /* PKM: {smcs, swms} */
     auto srow = [&](auto sc, auto kc, auto g2_c, float& resid) __attribute__((always_inline)) {
         constexpr int S = decltype(sc)::value, KIND = decltype(kc)::value;   /* 1 lower, 2 upper */
         const float x = KIND == 2 ? srh[S][1] + bcast16<SL0 + S>(gv) : srh[S][0] - bcast16<SL0 + S>(gv);
         const float delta = __builtin_amdgcn_fmed3f(x, -slam[S][KIND - 1], slhi[S] - slam[S][KIND - 1]);
         slam[S][KIND - 1] += delta;
         const float sd = KIND == 2 ? -delta : delta;
-        gv += smcs[S] * sd;
-        if constexpr (WROWS) gw += swms[S] * sd;
+        if constexpr (PKM) {
+            pk_fma_acc(gv, gw, smw[S], sd);
+        } else {
+            gv += smcs[S] * sd;
+            if constexpr (WROWS) gw += swms[S] * sd;
+        }
         if constexpr (TWO && decltype(g2_c)::value) gw2 += swms2[S] * sd;
         resid = fmaxf(resid, fabsf(delta));
     };
@@ -3601,25 +3647,44 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                     if (KMAX > 1 && nk > 1) x = lane_sel<SL0 + 1>(__shfl(x, src + ds[1]), x);
                 };
 #pragma unroll
-                for (int d = 0; d < NJ; d++) mirror(mcs[d]);
+                for (int d = 0; d < NJ; d++) {
+                    if constexpr (PKM) {   /* (mcs / cR live on only as the pairs' halves) */
+                        float t = mw[d].x;
+                        mirror(t);
+                        mw[d].x = t;
+                    } else {
+                        mirror(mcs[d]);
+                    }
+                }
                 mirror(gv);
                 if (g1_any) {
 #pragma unroll
                     for (int p = 0; p < NP; p++)
 #pragma unroll
-                        for (int dir = 0; dir < 3; dir++) mirror(cR[p][dir]);
+                        for (int dir = 0; dir < 3; dir++) {
+                            if constexpr (PKC) {
+                                float t = crw[3 * p + dir].x;
+                                mirror(t);
+                                crw[3 * p + dir].x = t;
+                            } else {
+                                mirror(cR[p][dir]);
+                            }
+                        }
                 }
                 /* the slots' row data: dof d_S's entries, selected with uniform masks */
 #pragma unroll
                 for (int S = 0; S < KMAX; S++) {
-                    smcs[S] = mcs[0]; swms[S] = wms[0]; swms2[S] = wms2[0]; slhi[S] = lhi[0];
+                    if constexpr (PKM) smw[S] = mw[0];
+                    else { smcs[S] = mcs[0]; swms[S] = wms[0]; }
+                    swms2[S] = wms2[0]; slhi[S] = lhi[0];
                     srh[S][0] = rl[0]; srh[S][1] = ru[0];
                     slam[S][0] = 0.0f; slam[S][1] = 0.0f;
                     sfor<1, NJ>([&](auto dc) __attribute__((always_inline)) {
                         constexpr int d = decltype(dc)::value;
                         const bool hit = ds[S] == d;   /* wave-uniform */
                         auto sel = [&](float a, float o) __attribute__((always_inline)) { return hit ? a : o; };
-                        smcs[S] = sel(mcs[d], smcs[S]); swms[S] = sel(wms[d], swms[S]);
+                        if constexpr (PKM) smw[S] = hit ? mw[d] : smw[S];
+                        else { smcs[S] = sel(mcs[d], smcs[S]); swms[S] = sel(wms[d], swms[S]); }
                         swms2[S] = sel(wms2[d], swms2[S]);
                         slhi[S] = sel(lhi[d], slhi[S]);
                         srh[S][0] = sel(rl[d], srh[S][0]); srh[S][1] = sel(ru[d], srh[S][1]);
