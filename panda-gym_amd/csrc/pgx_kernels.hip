@@ -1985,6 +1985,9 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                 V3 Cs[AO_N];   /* the obstacle centres, one LDS batch */
 #pragma unroll
                 for (int o = 0; o < AO_N; o++) Cs[o] = lds3(Lp->aoC[o], es);
+#ifdef PGX_AB_NO_OBST   /* timing bound only (wrong results): the obstacle pairs skipped */
+                if (true) {} else
+#endif
 #pragma unroll
                 for (int o = 0; o < AO_N; o++) {
                     const V3 C = Cs[o];
@@ -1996,7 +1999,11 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                     if (cap_on || chk) {
                         if (o < 3) d = len - r - kAoSize;
                         else if (len - r - kAoCubeBound < (cap_on ? tau : 0.0f))
+#ifdef PGX_AB_NO_BOXPAIR   /* timing bound only (wrong results): the bound for the box query */
+                            d = len - r - kAoCubeBound;
+#else
                             d = capsule_box_pair<true>(A, B, r, C, hcube, &P, &n);
+#endif
                     }
                     hit = hit || (chk && d <= 0.0f);
                     const bool cand = cap_on && d < tau;
