@@ -178,13 +178,15 @@ template <int W>
 __device__ __forceinline__ V3 lds3(const float (*a)[W], int ln) { return v3(a[0][ln], a[1][ln], a[2][ln]); }
 
 typedef float f2 __attribute__((ext_vector_type(2)));   /* packed fp32 pair (v_pk_*_f32) */
-/* PGS rows with packed (coordinate, Delassus) updates (pk_fma_acc), bit 0 joint rows, bit 1
- * contact rows; per kernel family, as measured (profiles/r05/ab_packed_rows.log): the ReachAO
- * kernels gain with the contact rows packed (0.779 -> 0.768 ms at 8192, scratch unchanged; both
- * kinds 0.766 ms but 32 B more scratch per lane), every other kernel loses 0.4-4.6 % to the
- * register pairs' alignment (more AGPR copies, or spills in the two-wave builds) */
+/* PGS rows with packed updates (pk_fma_acc): bit 0 joint rows and bit 1 contact rows pair the
+ * coordinate and Delassus registers {gv, gw}; bit 2 pairs the two Delassus registers {gw, gw2}
+ * (object tasks, full manifold).  Per kernel family, as measured (profiles/r05/ab_packed_rows.log):
+ * ReachAO gains with its contact rows paired (0.779 -> 0.768 ms at 8192, scratch unchanged; both
+ * kinds 0.766 ms but 32 B more scratch per lane); the object kernels gain with {gw, gw2} (Push 4096
+ * 1.212 -> 1.199 ms, PickAndPlace 16384 2.909 -> 2.855, no scratch); {gv, gw} pairs lose 0.4-5.8 %
+ * everywhere else (the pairs' aligned registers: more AGPR copies, or spills in two-wave builds) */
 #ifndef PGX_PK
-#define PGX_PK 0
+#define PGX_PK 4
 #endif
 #ifndef PGX_PK_AO
 #define PGX_PK_AO 2
@@ -3190,7 +3192,10 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
      * saved except in the ReachAO kernels (PGX_PK / PGX_PK_AO, above) */
     constexpr int PK = AO ? PGX_PK_AO : PGX_PK;
     constexpr bool PKM = WROWS && (PK & 1) != 0, PKC = WROWS && (PK & 2) != 0;
-    f2 mw[NJ], crw[NQ];
+    /* PKD (bit 2; the object tasks' full-manifold kernels, two Delassus registers, neither PKM nor
+     * PKC): the pair is {gw, gw2} instead, coefficients {wms, wms2} / {Wc, Wc2} */
+    constexpr bool PKD = TWO && FULL && !PKM && !PKC && (PK & 4) != 0;
+    f2 mw[NJ], crw[NQ], mw2[NJ], cw2[NQ];
     /* motor rows: the shifted bound pair (lo' - lambda', hi' - lambda') tracked instead of
      * lambda', one v_pk_add_f32 per row update (lambda' itself is not needed after the solve:
      * joint rows are not warm-started); limit rows keep lambda' (fewer live registers) */
@@ -3240,13 +3245,19 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
             lam[r] += delta;
         }
         const float sd = kind == 2 ? -delta : delta;
-        if constexpr (PKM) {
-            pk_fma_acc(gv, gw, mw[d], sd);
-        } else {
+        if constexpr (PKD) {
             gv += mcs[d] * sd;
-            if constexpr (WROWS) gw += wms[d] * sd;
+            if constexpr (decltype(g2_c)::value) pk_fma_acc(gw, gw2, mw2[d], sd);
+            else gw += mw2[d].x * sd;
+        } else {
+            if constexpr (PKM) {
+                pk_fma_acc(gv, gw, mw[d], sd);
+            } else {
+                gv += mcs[d] * sd;
+                if constexpr (WROWS) gw += wms[d] * sd;
+            }
+            if constexpr (TWO && decltype(g2_c)::value) gw2 += wms2[d] * sd;
         }
-        if constexpr (TWO && decltype(g2_c)::value) gw2 += wms2[d] * sd;
         resid = fmaxf(resid, fabsf(delta));
     };
     /* contact rows in scaled units too: lambda' = lambda den, friction bounds
@@ -3308,6 +3319,12 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
 #pragma unroll
             for (int q = 0; q < NQ; q++) crw[q] = (f2){cR[q / 3][q % 3], Wc[q]};
         }
+        if constexpr (PKD) {
+#pragma unroll
+            for (int d = 0; d < NJ; d++) mw2[d] = (f2){wms[d], wms2[d]};
+#pragma unroll
+            for (int q = 0; q < NQ; q++) cw2[q] = (f2){Wc[q], Wc2[q]};
+        }
     }
     /* shifted bounds as for the joint rows: delta' = clamp(rhs' - w, lo' - lambda', hi' - lambda').
      * A normal row's upper bound is +inf (0 with lambda' = 0 for an unusable row; in the object
@@ -3341,13 +3358,19 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
         const float x = q < GW ? bcast16<q % GW>(gw) : bcast16<q % GW>(gw2);   /* rhs' - w */
         const float delta = __builtin_amdgcn_fmed3f(x, lo, hi);
         clam[p][dir] = lm + delta;
-        if constexpr (PKC) {
-            pk_fma_acc(gv, gw, crw[q], delta);
-        } else {
+        if constexpr (PKD) {
             gv += cR[p][dir] * delta;
-            gw += Wc[q] * delta;
+            if constexpr (decltype(g2_c)::value) pk_fma_acc(gw, gw2, cw2[q], delta);
+            else gw += cw2[q].x * delta;
+        } else {
+            if constexpr (PKC) {
+                pk_fma_acc(gv, gw, crw[q], delta);
+            } else {
+                gv += cR[p][dir] * delta;
+                gw += Wc[q] * delta;
+            }
+            if constexpr (TWO && decltype(g2_c)::value) gw2 += Wc2[q] * delta;
         }
-        if constexpr (TWO && decltype(g2_c)::value) gw2 += Wc2[q] * delta;
         resid = fmaxf(resid, fabsf(delta));
     };
     /* the wave's largest robot-point count, a scalar: the per-point branches in the sweep
@@ -3682,8 +3705,8 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
 #pragma unroll
                 for (int S = 0; S < KMAX; S++) {
                     if constexpr (PKM) smw[S] = mw[0];
-                    else { smcs[S] = mcs[0]; swms[S] = wms[0]; }
-                    swms2[S] = wms2[0]; slhi[S] = lhi[0];
+                    else { smcs[S] = mcs[0]; swms[S] = PKD ? mw2[0].x : wms[0]; }
+                    swms2[S] = PKD ? mw2[0].y : wms2[0]; slhi[S] = lhi[0];
                     srh[S][0] = rl[0]; srh[S][1] = ru[0];
                     slam[S][0] = 0.0f; slam[S][1] = 0.0f;
                     sfor<1, NJ>([&](auto dc) __attribute__((always_inline)) {
@@ -3691,8 +3714,8 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
                         const bool hit = ds[S] == d;   /* wave-uniform */
                         auto sel = [&](float a, float o) __attribute__((always_inline)) { return hit ? a : o; };
                         if constexpr (PKM) smw[S] = hit ? mw[d] : smw[S];
-                        else { smcs[S] = sel(mcs[d], smcs[S]); swms[S] = sel(wms[d], swms[S]); }
-                        swms2[S] = sel(wms2[d], swms2[S]);
+                        else { smcs[S] = sel(mcs[d], smcs[S]); swms[S] = sel(PKD ? mw2[d].x : wms[d], swms[S]); }
+                        swms2[S] = sel(PKD ? mw2[d].y : wms2[d], swms2[S]);
                         slhi[S] = sel(lhi[d], slhi[S]);
                         srh[S][0] = sel(rl[d], srh[S][0]); srh[S][1] = sel(ru[d], srh[S][1]);
                     });
