@@ -192,13 +192,13 @@ typedef float f2 __attribute__((ext_vector_type(2)));   /* packed fp32 pair (v_p
 #define PGX_PK_AO 2
 #endif
 /* {a, b} += {ca, cb} s as one v_pk_fma_f32: each half is the fused multiply-add of the scalar
- * form, bit for bit, in one issue instead of two (a PGS row's coordinate and Delassus updates) */
+ * form, bit for bit, in one issue instead of two (two of a PGS row's register updates) */
 __device__ __forceinline__ void pk_fma_acc(float& a, float& b, f2 cab, float s) {
     const f2 r = __builtin_elementwise_fma(cab, (f2){s, s}, (f2){a, b});
     a = r.x;
     b = r.y;
 }
-constexpr int GW = 16;         /* lanes per env: one DPP row */
+constexpr int GW = 16;          /* lanes per env: one DPP row */
 constexpr int EPW = 64 / GW;    /* envs per wave */
 
 template <int V>
