@@ -249,6 +249,14 @@ typedef struct pgx_config {
                                      get_ee_position it reads after Panda.reset) and its goal
                                      fallback, a model constant computed once on the host; all zero:
                                      the kernel's own fp32 FK of that pose */
+    /* ReachAO: the robot's capsules at the neutral pose in world coordinates, fp64, per capsule of
+     * the model (model.n_capsules, the base's included) end A [3], end B [3], radius -- the geometry
+     * of the reset sampler's accept / reject tests (reach_ao.py:1101-1161, get_distances against the
+     * robot; host restatement panda-gym_amd/reach_ao.py RobotGeometry), which the device evaluates in
+     * fp64 on exactly these values so that a reset drawn on the device decides every test as the
+     * host's does.  All zero: pgx_create computes them by an fp64 FK of neutral_q from the model
+     * (the same values to rounding). */
+    double ao_capsules_neutral[PGX_MAX_CAPSULES][7];
 } pgx_config;
 
 typedef struct pgx_env* pgx_handle;
@@ -290,7 +298,8 @@ typedef struct pgx_state_view {
     uint32_t* errors;   /* [1] sticky PGX_ERR_* bits set by the kernels; the host clears them */
     int32_t robot_points;  /* the robot contact budget of this handle's kernels (0: no contacts) */
     int32_t* env_order;    /* [N] the env order of the last step launch that sorted its envs heavy-first
-                              (per-pair manifold kernels; position -> env id), NULL without one;
+                              (per-pair manifold kernels; position -> env id), the identity before
+                              the first such launch, NULL for handles without the per-pair budget;
                               not state (the next sorted launch rewrites it) */
     float* manifolds;      /* [1 + manifold_pool * PGX_MANIFOLD_POINT][N] the persistent manifold pool
                               (PGX_MANIFOLD_POOL above), NULL without one */
@@ -364,7 +373,9 @@ int pgx_release(pgx_handle h, int32_t state_id);
  * seed s draws from PCG64(SeedSequence(s)), which is what a record set from s reproduces bit for bit
  * (goal / object in the task's order, reach.py:75-78, push.py:75-87, pick_and_place.py:71-85;
  * ReachAO's rejection sampler, reach_ao.py:965-1082, with Generator.uniform / random / integers /
- * shuffle as numpy draws them).  A reset without a seed -- the step's auto-reset included -- gets a
+ * shuffle as numpy draws them, and every accept / reject test decided in fp64 on the host's
+ * capsules, pgx_config.ao_capsules_neutral -- the draws and the record bit for bit, ReachAO's goal
+ * to a few ulp: the device's sin / cos / cbrt are not the host libm's).  A reset without a seed -- the step's auto-reset included -- gets a
  * fresh OS-entropy generator in the reference, so no reference value exists for it: here it
  * continues stream i, a reproducible stand-in with the same distribution, not the reference's
  * draws.  states: [N][PGX_PCG64_WORDS] uint64 per env {state_lo, state_hi, inc_lo, inc_hi,

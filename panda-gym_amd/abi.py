@@ -97,6 +97,7 @@ class PgxConfig(C.Structure):
         ("table_center", C.c_double * 3), ("table_half", C.c_double * 3), ("plane_z", C.c_double),
         ("terminate_on_success", C.c_int32), ("pad3", C.c_int32), ("collision_reward", C.c_double),
         ("ao_ee_neutral", C.c_double * 3),
+        ("ao_capsules_neutral", (C.c_double * 7) * MAX_CAPSULES),
     ]
 
 

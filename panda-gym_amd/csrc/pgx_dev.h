@@ -65,6 +65,10 @@ struct PgxDevEnv {
     double collision_reward;
     double ao_ee[3];               /* pgx_config.ao_ee_neutral: the reset sampler's EE centre, fp64 */
     int32_t ao_ee_set;             /* 0: the kernel's fp32 FK of the neutral pose instead */
+    const double* ao_geo;          /* ReachAO reset geometry, fp64, device (allocated with the handle):
+                                      [PGX_NCAP][7] capsules A, B, r at the neutral pose
+                                      (pgx_config.ao_capsules_neutral), then the table centre [3] and
+                                      half extents [3]; nullptr for the other tasks */
     int32_t lanes_per_env;         /* step layout: 1 (env per lane) or 16 (env per DPP row) */
     int32_t pgs_mode;              /* test hook (PGX_PGS_MODE): 0 auto, 2 never speculate on the limit
                                       rows, 3 always redo the speculative solve with them */

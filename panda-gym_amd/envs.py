@@ -18,6 +18,7 @@ as torch tensors on the env's device.  There is no CPU physics fallback.
 from __future__ import annotations
 
 import ctypes as C
+import importlib
 import math
 import os
 from dataclasses import replace
@@ -35,9 +36,29 @@ except ImportError:  # pragma: no cover - torch is part of the image
     torch = None
 
 
+# ------------------------------------------------- gymnasium / SB3 identity
+def _optional(name: str):
+    try:
+        return importlib.import_module(name)
+    except ImportError:
+        return None
+
+
+# Where gymnasium / stable-baselines3 are importable, the env classes ARE their classes' subclasses
+# and the spaces are gymnasium's (RobotTaskEnv(gym.Env) with spaces.Dict of spaces.Box, core.py:4-7,
+# 255, 274-280; SB3's make_vec_env(..., SubprocVecEnv) consumer, setup_training.py:43-47), so SB3's
+# isinstance checks (VecEnv wrapping, spaces.Dict for MultiInputPolicy) accept them; elsewhere the
+# stand-ins below keep the same surface.
+_gym = _optional("gymnasium")
+_gym_spaces = _optional("gymnasium.spaces") if _gym is not None else None
+_sb3_vec = _optional("stable_baselines3.common.vec_env")
+_EnvBase = _gym.Env if _gym is not None else object
+_VecEnvBase = _sb3_vec.VecEnv if _sb3_vec is not None else object
+
+
 # ----------------------------------------------------------------- spaces
 class Box:
-    """Minimal gymnasium.spaces.Box stand-in (gymnasium is not installed here)."""
+    """Minimal gymnasium.spaces.Box stand-in (used where gymnasium is not installed)."""
 
     def __init__(self, low: float, high: float, shape: Tuple[int, ...], dtype=np.float32):
         self.low = np.full(shape, low, dtype=dtype)
@@ -65,6 +86,20 @@ class DictSpace(dict):
         return dict(self)
 
 
+def make_spaces(obs_dim: int, action_dim: int):
+    """(observation_space, action_space) of RobotTaskEnv (core.py:274-280): Dict(observation,
+    desired_goal, achieved_goal) of Box(-10, 10) and Box(-1, 1) of the action, float32 --
+    gymnasium's classes where gymnasium imports, the stand-ins otherwise."""
+    if _gym_spaces is not None:
+        box = lambda lo, hi, n: _gym_spaces.Box(lo, hi, shape=(n,), dtype=np.float32)  # noqa: E731
+        obs = _gym_spaces.Dict(dict(observation=box(-10.0, 10.0, obs_dim), desired_goal=box(-10.0, 10.0, 3),
+                                    achieved_goal=box(-10.0, 10.0, 3)))
+        return obs, box(-1.0, 1.0, action_dim)
+    obs = DictSpace(observation=Box(-10.0, 10.0, (obs_dim,)), desired_goal=Box(-10.0, 10.0, (3,)),
+                    achieved_goal=Box(-10.0, 10.0, (3,)))
+    return obs, Box(-1.0, 1.0, (action_dim,))
+
+
 # --------------------------------------------------------------- registry
 _REGISTRY: Dict[str, abi.EnvSpec] = {}
 
@@ -86,6 +121,11 @@ def register_envs(max_ep_steps: int = 50) -> None:
     # panda_gym/__init__.py:15-20, 51-56; PandaReachAOEnv (panda_tasks.py:132-159) with TrainConfig
     # defaults and scenario "reachao_rand" (the config this build runs)
     _REGISTRY["PandaReachAO-v3"] = abi.EnvSpec.reach_ao(max_episode_steps=max_ep_steps)
+    if _gym is not None:   # gym.make("PandaReach-v3") as the reference registers it (__init__.py:23-91)
+        for env_id in _REGISTRY:
+            if env_id not in getattr(_gym, "registry", {}):
+                _gym.register(id=env_id, entry_point="panda_gym_amd.envs:PandaEnv", kwargs={"env_id": env_id},
+                              max_episode_steps=max_ep_steps)
 
 
 def registered_ids() -> List[str]:
@@ -178,8 +218,9 @@ def pcg64_from_record(rec: np.ndarray) -> np.random.Generator:
 
 
 # ------------------------------------------------------------ vec env
-class PandaVecEnv:
-    """N independent Panda envs stepped in lockstep by one HIP kernel launch.
+class PandaVecEnv(_VecEnvBase):
+    """N independent Panda envs stepped in lockstep by one HIP kernel launch (an SB3 ``VecEnv``
+    subclass where stable-baselines3 imports).
 
     ``lanes_per_env`` picks the kernel layout (results agree to fp32 rounding): 16 gives
     each env a 16-lane DPP row (the solver's coordinates split over the lanes; fastest
@@ -198,9 +239,13 @@ class PandaVecEnv:
     (core.py:302).  A reset without a seed, the auto-reset included, gets fresh OS entropy in the
     reference, so there is no reference value to match: here it continues the env's stream (a
     reproducible stand-in with the reference's distribution).  ReachAO draws its rejection sampler
-    (reach_ao.py:965-1082) from the stream with numpy's uniform / random / integers / shuffle; its
-    accept / reject tests are the kernel's fp32 geometry, so a seed whose numpy-side test sits
-    within fp32 rounding of its threshold can take the other branch."""
+    (reach_ao.py:965-1082) from the stream with numpy's uniform / random / integers / shuffle, and
+    decides every accept / reject test in fp64 on the host's capsules with the host sampler's
+    arithmetic (``reach_ao.reset_draws``), so it takes the same branches and draws; its goal agrees
+    to a few ulp (the device's sin / cos / cbrt against the host libm)."""
+
+    metadata = {"render_modes": []}
+    render_mode = None
 
     def __init__(self, env_id: str = "PandaReach-v3", num_envs: int = 4096, device: Any = "cuda:0", seed: int = 0,
                  env_id_offset: int = 0, max_episode_steps: Optional[int] = None, auto_reset: bool = True,
@@ -239,10 +284,17 @@ class PandaVecEnv:
         self._cfg = abi.make_config(self.spec, self.num_envs, self._model, self._params, seed=seed,
                                     env_id_offset=env_id_offset, contacts=contacts, lanes_per_env=lanes_per_env,
                                     full_manifold=full_manifold)
-        if self.spec.task == abi.TASK_REACH_AO:   # the reset sampler's EE centre, fp64 (pgx.h ao_ee_neutral)
-            ee = _ao_geometry(tuple(self.spec.base_pos), model_name).ee
+        if self.spec.task == abi.TASK_REACH_AO:
+            # the reset sampler's EE centre and its capsules at the neutral pose, fp64 (pgx.h
+            # ao_ee_neutral, ao_capsules_neutral): the device's accept / reject tests run on these values
+            geom = _ao_geometry(tuple(self.spec.base_pos), model_name)
             for i in range(3):
-                self._cfg.ao_ee_neutral[i] = float(ee[i])
+                self._cfg.ao_ee_neutral[i] = float(geom.ee[i])
+            for c in range(len(geom.r)):
+                for k in range(3):
+                    self._cfg.ao_capsules_neutral[c][k] = float(geom.A[c][k])
+                    self._cfg.ao_capsules_neutral[c][3 + k] = float(geom.B[c][k])
+                self._cfg.ao_capsules_neutral[c][6] = float(geom.r[c])
         # auto_reset=False: a finished env keeps its terminal state until reset (one gymnasium env)
         self._cfg.no_auto_reset = 0 if auto_reset else 1
         self.auto_reset = bool(auto_reset)
@@ -278,9 +330,7 @@ class PandaVecEnv:
                                    self.truncated.data_ptr(), self.terminal_obs.data_ptr(), self.terminal_ag.data_ptr(),
                                    self.terminal_dg.data_ptr(),
                                    self.task_trunc.data_ptr() if self.spec.task == abi.TASK_REACH_AO else None)
-        self.observation_space = DictSpace(observation=Box(-10.0, 10.0, (od,)), desired_goal=Box(-10.0, 10.0, (3,)),
-                                           achieved_goal=Box(-10.0, 10.0, (3,)))
-        self.action_space = Box(-1.0, 1.0, (self.action_dim,))
+        self.observation_space, self.action_space = make_spaces(od, self.action_dim)
         self.distance_threshold = self.spec.distance_threshold
         if self.spec.task == abi.TASK_REACH_AO:
             self.reward_type = "sparse_ao"   # ReachAO.compute_reward sparse/reach (reach_ao.py:1317-1320)
@@ -296,6 +346,8 @@ class PandaVecEnv:
             except Exception:
                 self.close()
                 raise
+        if _VecEnvBase is not object:   # SB3's VecEnv bookkeeping (reset_infos, seeds, render_mode)
+            _VecEnvBase.__init__(self, n, self.observation_space, self.action_space)
 
     # ---------------------------------------------------------------- core
     def _check(self, rc: int, what: str) -> None:
@@ -604,6 +656,11 @@ class PandaVecEnv:
             return [self.compute_reward(*args, **kwargs)]
         return [getattr(self, method_name)(*args, **kwargs)]
 
+    def env_is_wrapped(self, wrapper_class, indices=None) -> List[bool]:
+        """SB3 VecEnv.env_is_wrapped: the envs are kernel lanes, wrapped in nothing."""
+        n = self.num_envs if indices is None else len(list(indices))
+        return [False] * n
+
     def get_attr(self, attr_name: str, indices=None):
         val = getattr(self, attr_name)
         n = self.num_envs if indices is None else len(list(indices))
@@ -662,13 +719,13 @@ class _RobotView:
 
     @property
     def block_gripper(self) -> bool:
-        return bool(self._env.spec.block_gripper)
+        return bool(self._env._vec.spec.block_gripper)
 
     def get_obs(self) -> np.ndarray:
         """Panda.get_obs (panda.py:264-288): EE position, EE velocity (+ fingers width; ReachAO:
         + q, qd, the "js" observation)."""
         o = self._obs()
-        n = 20 if self._env.spec.task == abi.TASK_REACH_AO else 6 + (0 if self.block_gripper else 1)
+        n = 20 if self._env._vec.spec.task == abi.TASK_REACH_AO else 6 + (0 if self.block_gripper else 1)
         return o[:n]
 
     def get_ee_position(self) -> np.ndarray:   # panda.py:306-308 (getLinkState's cached pose)
@@ -712,7 +769,7 @@ class _TaskView:
 
     @property
     def distance_threshold(self) -> float:
-        return float(self._env.spec.distance_threshold)
+        return float(self._env._vec.spec.distance_threshold)
 
     @property
     def reward_type(self) -> str:
@@ -764,10 +821,12 @@ class _SimView:
         self._env.remove_state(state_id)
 
 
-class PandaEnv:
-    """One env with the RobotTaskEnv + TimeLimit surface (gym.make("PandaReach-v3") in the reference)."""
+class PandaEnv(_EnvBase):
+    """One env with the RobotTaskEnv + TimeLimit surface (gym.make("PandaReach-v3") in the reference;
+    a ``gymnasium.Env`` subclass where gymnasium imports)."""
 
     metadata = {"render_modes": []}
+    render_mode = None
 
     def __init__(self, env_id: str = "PandaReach-v3", device: Any = "cuda:0", max_episode_steps: Optional[int] = None,
                  seed: int = 0, reset_rng: str = "philox"):
@@ -777,6 +836,7 @@ class PandaEnv:
         draws there, not a reference value (PandaVecEnv)."""
         self._vec = PandaVecEnv(env_id, num_envs=1, device=device, seed=seed, auto_reset=False,
                                 max_episode_steps=max_episode_steps, reset_rng=reset_rng)
+        # (gymnasium.make replaces env.spec with its registry EnvSpec: the env reads self._vec.spec)
         self.spec = self._vec.spec
         self.observation_space = self._vec.observation_space
         self.action_space = self._vec.action_space
@@ -784,7 +844,7 @@ class PandaEnv:
         self.robot, self.task, self.sim = _RobotView(self), _TaskView(self), _SimView(self)
 
     def reset(self, seed: Optional[int] = None, options: Optional[dict] = None):
-        r = None if self._vec.reset_rng == "pcg64" else seeded_reset(self.spec, seed)
+        r = None if self._vec.reset_rng == "pcg64" else seeded_reset(self._vec.spec, seed)
         if self._vec.reset_rng == "pcg64":   # reseed the device stream (seed given) or continue it
             self._vec.reset_tensors(seed=seed)
         elif r is None:

@@ -101,8 +101,10 @@ def test_device_reset_draws_match_oracle(pg, oracle):
                      axis=(1, 2))
     act_ok = np.all(st["obstacles"][18:].T == ref.active, axis=1)
     ok = goal_ok & obst_ok & act_ok
-    # fp32 rejection tests can flip a sample that sits within rounding of a margin
-    assert ok.mean() >= 0.99, (goal_ok.mean(), obst_ok.mean(), act_ok.mean())
+    print(f"ReachAO Philox resets: device and oracle resets agree in {int(ok.sum())} of {n} envs")
+    # the device decides the rejection tests in fp64 (round 6) and the oracle's C geometry agrees
+    # with the host's numpy to ~1e-12, so a flip needs a test within ~1e-12 of its threshold
+    assert ok.all(), (np.flatnonzero(~ok)[:8], goal_ok.mean(), obst_ok.mean(), act_ok.mean())
     obs, _, _ = _obs(venv)
     err = _obs_err(obs[ok], out["obs"][ok])
     assert err["ee"] <= 1e-5 and err["dist"] <= 2e-5 and _unit_ok(obs[ok], out["obs"][ok]), err

@@ -189,10 +189,12 @@ def test_reach_ao_seeded_reset_on_the_device_then_auto_resets(pg, lanes):
     the host sampler reach_ao.reset_draws on numpy's own Generator: the stream record (numpy's full
     bit_generator.state, has_uint32 included) bit for bit; the fp64 goal to 4 ulp of its radius
     (GOAL_TOL) and the obstacle centres (f32) to 1 ulp -- the device's sin / cos / cbrt against the
-    host libm, whose last-bit differences can cross an f32 rounding boundary.  The kernel's
-    accept / reject tests run in fp32 and the host's in fp64, so an env may take the other branch
-    where a host test sits within 1e-4 of its threshold: such envs are counted, must be explained
-    by that margin, and continue from the device's record."""
+    host libm, whose last-bit differences can cross an f32 rounding boundary.  Every accept / reject
+    test runs in fp64 on the host's capsules with the host's arithmetic (round 6; round 5's fp32
+    tests let up to 2 % of resets take the other branch), so no reset may decide differently: a
+    different decision consumes a different number of draws and shows as a different record.  The
+    count of tests within 1e-6 of their threshold is printed beside the result (the margins that
+    an fp32 evaluation could have flipped)."""
     from panda_gym_amd import reach_ao
     from panda_gym_amd.envs import _ao_geometry
 
@@ -203,7 +205,7 @@ def test_reach_ao_seeded_reset_on_the_device_then_auto_resets(pg, lanes):
     gens = _gens(seed, n)
     venv.reset_tensors(seed=seed)
     zero = torch.zeros((n, venv.action_dim), device="cuda:0")
-    exact_goal, exact_obst, explained = 0, 0, 0
+    exact_goal, exact_obst, flips, tests, near = 0, 0, [], 0, [0, 0]
     for rnd in range(3):
         st = venv.state()
         goal = st["goal"].cpu().numpy().T
@@ -212,6 +214,9 @@ def test_reach_ao_seeded_reset_on_the_device_then_auto_resets(pg, lanes):
         for i in range(n):
             margins = []
             g_ref, o_ref = reach_ao.reset_draws(gens[i], geom, margins=margins)
+            tests += len(margins)
+            near[0] += sum(abs(m) < 1e-4 for m in margins)
+            near[1] += sum(abs(m) < 1e-6 for m in margins)
             of = o_ref.astype(np.float32)
             same = (np.array_equal(recs[i], pg.pcg64_record(gens[i]))
                     and np.all(np.abs(obst[i] - of) <= np.spacing(np.abs(of)))
@@ -220,17 +225,15 @@ def test_reach_ao_seeded_reset_on_the_device_then_auto_resets(pg, lanes):
             if same:
                 exact_goal += int(np.array_equal(goal[i], g_ref))
             else:
-                assert min(abs(m) for m in margins) < 1e-4, (
-                    rnd, i, goal[i] - g_ref, recs[i].tolist(), pg.pcg64_record(gens[i]).tolist(),
-                    np.abs(obst[i] - o_ref.astype(np.float32)).max(axis=1).tolist())
-                explained += 1
+                flips.append((rnd, i, min(abs(m) for m in margins)))
                 gens[i] = pg.pcg64_from_record(recs[i])
         if rnd < 2:
             venv.step_tensors(zero)
             assert venv.truncated.all().item()
-    print(f"ReachAO pcg64 resets: {3 * n} checked, {explained} explained by a fp32 decision, goals bit-exact "
-          f"{exact_goal} and obstacle centres bit-exact {exact_obst} of {3 * n - explained}")
-    assert explained <= 0.02 * 3 * n
+    print(f"ReachAO pcg64 resets ({lanes} lanes): {3 * n} checked, {tests} accept/reject tests ({near[0]} within "
+          f"1e-4 and {near[1]} within 1e-6 of their threshold), {len(flips)} decided differently; goals bit-exact "
+          f"{exact_goal} and obstacle centres bit-exact {exact_obst} of {3 * n}")
+    assert not flips, flips
     venv.close()
 
 

@@ -1,7 +1,7 @@
 """Phase breakdown of the step kernel (s_memtime per wave, libpgx_prof.so = make -C
 panda-gym_amd/csrc prof).  Prints mean cycles per wave per env step by phase and the
 PGS sweeps per substep the waves ran.
-Usage: PGX_LIB=panda-gym_amd/libpgx_prof.so python tools/prof_phases.py [env_id] [n] [contacts]"""
+Usage: PGX_LIB=abl/libpgx_prof.so python tools/prof_phases.py [env_id] [n] [contacts]"""
 import ctypes as C
 import json
 import os
