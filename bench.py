@@ -154,6 +154,9 @@ def host_cores() -> dict:
             "cpu_model": model}
 
 
+CPU_THREADS_MAX = 64   # thread cap of the CPU baseline where no OMP_NUM_THREADS share is set
+
+
 def cpu_baseline(venv, seconds: float):
     """fp64 oracle on the host cores (threads; ctypes releases the GIL) over a bounded sample: one
     thread per core this process may use, capped by the box's CPU share for a one-GPU job
@@ -164,25 +167,38 @@ def cpu_baseline(venv, seconds: float):
 
     n = venv.num_envs
     hc = host_cores()
-    threads = hc["affinity"] if hc["omp_num_threads"] is None else min(hc["affinity"], hc["omp_num_threads"])
+    # the box's one-GPU share (OMP_NUM_THREADS); without one, the affinity mask capped at CPU_THREADS_MAX
+    threads = min(hc["affinity"], CPU_THREADS_MAX) if hc["omp_num_threads"] is None \
+        else min(hc["affinity"], hc["omp_num_threads"])
     threads = max(1, threads)
-    shards = np.array_split(np.arange(n), threads)
-    envs = []
-    for sh in shards:
-        cfg = type(venv._cfg).from_buffer_copy(venv._cfg)
-        cfg.n_envs = len(sh)
-        cfg.env_id_offset = int(sh[0])
-        e = O.OracleVecEnv(cfg, len(sh))
-        e.reset()
-        envs.append(e)
-    steps = 0
-    t0 = time.perf_counter()
-    with cf.ThreadPoolExecutor(threads) as ex:
-        while time.perf_counter() - t0 < seconds and steps < 200:
-            list(ex.map(lambda e: e.step(e.sample_actions(steps)), envs))
-            steps += 1
-    dt = time.perf_counter() - t0
+
+    def run(n_envs: int, n_threads: int, budget: float):
+        shards = np.array_split(np.arange(n_envs), n_threads)
+        envs = []
+        for sh in shards:
+            cfg = type(venv._cfg).from_buffer_copy(venv._cfg)
+            cfg.n_envs = len(sh)
+            cfg.env_id_offset = int(sh[0])
+            e = O.OracleVecEnv(cfg, len(sh))
+            e.reset()
+            envs.append(e)
+        steps = 0
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(n_threads) as ex:
+            while time.perf_counter() - t0 < budget and steps < 200:
+                list(ex.map(lambda e: e.step(e.sample_actions(steps)), envs))
+                steps += 1
+        return steps, time.perf_counter() - t0
+
+    steps, dt = run(n, threads, seconds)
+    # one core (BASELINE.md section 2's single-core figure): a 256-env slice of the same workload
+    n1 = min(n, 256)
+    steps1, dt1 = run(n1, 1, max(2.0, seconds / 4))
     return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port", **hc,
+            "single_core": {"value": n1 * steps1 / dt1, "unit": "env-steps/s", "cores": 1,
+                            "sample": f"{n1} envs x {steps1} steps = {n1 * steps1} env-steps in {dt1:.1f} s on one thread"},
+            "cores_note": "'cores' is the CPU share the GPU box grants one GPU (OMP_NUM_THREADS), not the whole "
+                          "machine (nproc): the multi-thread leg is capped at that share by design",
             "sample": f"fp64 C oracle (CPU restatement, not PyBullet): {n} PandaReach envs x {steps} steps "
                       f"= {n * steps} env-steps in {dt:.1f} s on {threads} host threads (nproc {hc['nproc']}, "
                       f"{hc['affinity']} in this process's affinity, OMP_NUM_THREADS {hc['omp_num_threads']}: "

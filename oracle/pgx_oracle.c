@@ -35,8 +35,12 @@
  * points per substep [64,80), IK iterations [80,112), substeps ending with a joint-limit
  * impulse [112], with robot contacts [113], both [114]; not part of the restatement */
 int64_t pgxo_diag_hist[128];
+/* the histograms are bumped with relaxed atomics: bench.py's cpu_baseline steps oracle shards in threads */
+#define PGXO_HIST_ADD(h, i, v) __atomic_fetch_add(&(h)[(i)], (int64_t)(v), __ATOMIC_RELAXED)
 void pgxo_diag_read(int64_t* out, int clear) {
-    for (int i = 0; i < 128; i++) { out[i] = pgxo_diag_hist[i]; if (clear) pgxo_diag_hist[i] = 0; }
+    for (int i = 0; i < 128; i++)
+        out[i] = clear ? __atomic_exchange_n(&pgxo_diag_hist[i], 0, __ATOMIC_RELAXED)
+                       : __atomic_load_n(&pgxo_diag_hist[i], __ATOMIC_RELAXED);
 }
 /* optional trace of every solve's sweep count, in call order (env-major within a vec step) */
 static int32_t* diag_trace;
@@ -532,7 +536,9 @@ static int robot_budget = -1;
 int64_t pgxo_pair_hist[PGXO_ROBOT_HIST];
 void pgxo_set_robot_budget(int b) { robot_budget = b < 0 ? -1 : (b > PGXO_ROBOT_MAX ? PGXO_ROBOT_MAX : b); }
 void pgxo_pair_hist_read(int64_t* out, int clear) {
-    for (int i = 0; i < PGXO_ROBOT_HIST; i++) { out[i] = pgxo_pair_hist[i]; if (clear) pgxo_pair_hist[i] = 0; }
+    for (int i = 0; i < PGXO_ROBOT_HIST; i++)
+        out[i] = clear ? __atomic_exchange_n(&pgxo_pair_hist[i], 0, __ATOMIC_RELAXED)
+                       : __atomic_load_n(&pgxo_pair_hist[i], __ATOMIC_RELAXED);
 }
 /* per-thread scratch: bench.py's cpu_baseline steps one env shard per host thread */
 #ifdef __cplusplus
@@ -734,7 +740,7 @@ static int man_add(double* P, int cap, int key, const double* np, double thr2) {
     }
     if (n < 4) {
         const int cnt = (int)P[0];
-        if (cnt >= cap) { pgxo_diag_hist[120]++; return -1; }
+        if (cnt >= cap) { PGXO_HIST_ADD(pgxo_diag_hist, 120, 1); return -1; }
         double* c = pool_pt(P, cnt);
         memcpy(c, np, MAN_PT * sizeof(double));
         c[MP_KID] = key + n;
@@ -996,7 +1002,7 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
     const int n0 = select_points(&s0, PGX_OBJECT_POINTS, out, NULL);
     const int budget = robot_budget >= 0 ? robot_budget : W->robot_points;
     const int n1 = select_points(&s1, budget, out + n0, &np1);
-    pgxo_pair_hist[np1 < PGXO_ROBOT_HIST - 1 ? np1 : PGXO_ROBOT_HIST - 1]++;
+    PGXO_HIST_ADD(pgxo_pair_hist, np1 < PGXO_ROBOT_HIST - 1 ? np1 : PGXO_ROBOT_HIST - 1, 1);
     sort_by_id(out, n0);
     sort_by_id(out + n0, n1);
     last_n = n0 + n1;
@@ -1233,14 +1239,14 @@ static void substep_impl(const pgx_model* m, const pgx_sim_params* p, const doub
         if (!(p->flags & PGX_FLAG_NO_RESIDUAL_EXIT) && resid <= p->residual_threshold) break;
     }
     if (st) st->solver_iterations = it_used;
-    pgxo_diag_hist[it_used < 63 ? it_used : 63]++;
+    PGXO_HIST_ADD(pgxo_diag_hist, it_used < 63 ? it_used : 63, 1);
     if (diag_trace && diag_trace_pos < diag_trace_cap) diag_trace[diag_trace_pos++] = it_used;
-    pgxo_diag_hist[64 + (ncon < 15 ? ncon : 15)]++;
+    PGXO_HIST_ADD(pgxo_diag_hist, 64 + (ncon < 15 ? ncon : 15), 1);
     {
         int lim = 0, rob = 0;
         for (int r = 0; r < nr; r++) lim |= m->row_kind[r] != PGX_ROW_MOTOR && lam[r] != 0.0;
         for (int c2 = 0; c2 < ncon; c2++) rob |= con[c2].grp != 0;
-        pgxo_diag_hist[112] += lim; pgxo_diag_hist[113] += rob; pgxo_diag_hist[114] += lim && rob;
+        PGXO_HIST_ADD(pgxo_diag_hist, 112, lim); PGXO_HIST_ADD(pgxo_diag_hist, 113, rob); PGXO_HIST_ADD(pgxo_diag_hist, 114, lim && rob);
     }
     PGXO_PHASE(5);
     double vn[D];
@@ -1425,7 +1431,7 @@ int pgxo_ik(const pgx_model* m, const pgx_sim_params* p, const double base[3], c
     }
     if (it == 0) memcpy(q_out, q_start, sizeof(double) * nd);
     if (st) { st->ik_iterations = it; st->ik_residual = diff; }
-    pgxo_diag_hist[80 + (it < 31 ? it : 31)]++;
+    PGXO_HIST_ADD(pgxo_diag_hist, 80 + (it < 31 ? it : 31), 1);
     return it;
 }
 

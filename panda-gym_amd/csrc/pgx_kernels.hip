@@ -786,9 +786,10 @@ static_assert(PGX_NCAP <= 16, "PgxDevModel.cap_mu holds 16 capsules");
  * cube's pair (m.friction). */
 template <int AO, int FULL = 0>
 __device__ __forceinline__ float point_mu(MRef m, float id) {
-    /* (FULL: ReachAO's manifold points 32 + 24 c + 4 o + slot; the cube's 32 + 16 c + slot) */
+    /* (FULL with AO_PERS: ReachAO's manifold points 32 + 24 c + 4 o + slot; the PGX_AO_FRESH A/B build's
+     * fresh candidates and the one-lane layout 32 + 6 c + o; the cube's 32 + 16 c + slot) */
     const float cf = id < kTableIdLimit ? id * 0.5f
-                   : (id - kTableIdLimit) * (AO ? (FULL ? (1.0f / 24.0f) : (1.0f / 6.0f)) : 0.0625f);
+                   : (id - kTableIdLimit) * (AO ? ((FULL && AO_PERS) ? (1.0f / 24.0f) : (1.0f / 6.0f)) : 0.0625f);
     const int cap = (int)(cf + 1e-3f);   /* (ids are exact small integers; the margin covers 1/6's rounding) */
     float mu = m.friction;
     sfor<0, PGX_NCAP>([&](auto kc) __attribute__((always_inline)) {
