@@ -141,6 +141,12 @@ typedef struct pgx_model {
     double cap_a[PGX_MAX_CAPSULES][3];
     double cap_b[PGX_MAX_CAPSULES][3];
     double cap_radius[PGX_MAX_CAPSULES];
+    /* Bullet's link compound AABB (btCompoundShape::getAabb with the identity) in the link's COM
+     * frame, child and compound margins included: centre and half extents.  The link's angular
+     * motion disc |half| + |centre| scales its contact breaking threshold
+     * (pgx_sim_params.contact_distance, btCollisionShape::getContactBreakingThreshold). */
+    double link_aabb_center[PGX_MAX_LINKS][3];
+    double link_aabb_half[PGX_MAX_LINKS][3];
 } pgx_model;
 
 #define PGX_CAP_VS_TABLE 1                 /* capsule end spheres collide with table / plane */
@@ -165,7 +171,15 @@ typedef struct pgx_sim_params {
     int32_t num_iterations;       /* numSolverIterations 50 */
     int32_t ik_max_iters;         /* maxNumIterations 20 */
     int32_t flags;                /* PGX_FLAG_* hypotheses (oracle only) */
-    double contact_distance;      /* contact processing threshold 0.02 (gContactBreakingThreshold) */
+    double contact_distance;      /* gContactBreakingThreshold 0.02.  Bullet's dispatcher scales it per
+                                     pair (btCollisionDispatcher::getNewManifold with its default flag
+                                     CD_USE_RELATIVE_CONTACT_BREAKING_THRESHOLD): the pair's manifold
+                                     breaking threshold is the smaller of the two shapes'
+                                     getContactBreakingThreshold(0.02) = angular motion disc x 0.02 --
+                                     the distance within which the narrow phase reports a point
+                                     (btManifoldResult::addContactPoint), merges it into a cached one
+                                     (getCacheEntry) and keeps it (refreshContactPoints).  DESIGN.md
+                                     section 2 "Contact breaking threshold". */
     double contact_erp;           /* ERP of multibody contact rows (m_erp 0.2) */
     double friction;              /* combined lateral friction of the cube against the table / plane:
                                      0.5 * 0.5 (each body's pybullet default; btManifoldResult
@@ -195,6 +209,9 @@ typedef struct pgx_sim_params {
 #define PGX_FLAG_FRESH_MANIFOLD 64        /* study: with PGX_CONTACTS_FULL, round 4's rule for the cube /
                                              obstacle pairs -- each pair's 4 deepest candidates of the
                                              substep -- instead of Bullet's persistent manifolds */
+#define PGX_FLAG_GLOBAL_BREAKING 128      /* study: every pair's breaking threshold the global
+                                             contact_distance (rounds 2-5) instead of Bullet's relative
+                                             per-pair threshold */
 
 typedef struct pgx_config {
     int32_t task;                 /* PGX_TASK_* */

@@ -41,6 +41,9 @@ int pgxo_flops_nphase(void) { return PGXO_NPHASE; }
 }
 #define pgxo_flops g_flops[g_phase]
 #define PGXO_PHASE(k) (g_phase = (k))
+/* model constants computed per call (the contact breaking thresholds): not counted */
+#define PGXO_CONST_BEGIN pgxo_flops_t pgxo_saved_[PGXO_NPHASE]; memcpy(pgxo_saved_, g_flops, sizeof g_flops)
+#define PGXO_CONST_END memcpy(g_flops, pgxo_saved_, sizeof g_flops)
 
 struct fcd {
     double v;

@@ -127,6 +127,18 @@ def pair_hist(clear: bool = True) -> np.ndarray:
     return h
 
 
+def breaking_thresholds(cfg) -> dict:
+    """The contact breaking threshold of every pair the oracle uses (Bullet's relative rule,
+    pgx_oracle.c breaking_thresholds; the global contact_distance under FLAG_GLOBAL_BREAKING):
+    per capsule against the table / plane / cube / an obstacle, and the cube against the table /
+    plane."""
+    nc = 16
+    out = np.zeros(4 * nc + 2)
+    lib().pgxo_breaking_thresholds(C.byref(cfg), out.ctypes.data_as(C.c_void_p))
+    return {"table": out[:nc], "plane": out[nc:2 * nc], "cube": out[2 * nc:3 * nc], "obstacle": out[3 * nc:4 * nc],
+            "cube_table": float(out[4 * nc]), "cube_plane": float(out[4 * nc + 1])}
+
+
 def last_contacts():
     """The points of the oracle's last contact detection: (group, feature id, link, separation) arrays."""
     m = OBJECT_POINTS + ROBOT_MAX

@@ -33,7 +33,11 @@
 /* ----------------------------------------------------------------- small vec */
 /* diagnostics (tools/diag_iterations.py): histograms of PGS sweeps [0,64), contact
  * points per substep [64,80), IK iterations [80,112), substeps ending with a joint-limit
- * impulse [112], with robot contacts [113], both [114]; not part of the restatement */
+ * impulse [112], with robot contacts [113], both [114]; the persistent manifolds' branches:
+ * a point dropped because the pool was full [120], addContactPoint merging into a cached point
+ * (replaceContactPoint) [121], appending (addManifoldPoint) [122], replacing sortCachedPoints' slot
+ * [123], refreshContactPoints removing a point past the threshold [124] or slid off [125]; not part
+ * of the restatement */
 int64_t pgxo_diag_hist[128];
 /* the histograms are bumped with relaxed atomics: bench.py's cpu_baseline steps oracle shards in threads */
 #define PGXO_HIST_ADD(h, i, v) __atomic_fetch_add(&(h)[(i)], (int64_t)(v), __ATOMIC_RELAXED)
@@ -570,6 +574,11 @@ typedef struct {
     double tc[3], th[3], plane_z;
     const double* obst;   /* ReachAO: obstacle centres [6][3] (static colliders), else NULL */
     int robot_points;     /* the robot group's budget (pgx_config.contacts: 4, or PGX_CONTACTS_FULL's) */
+    /* the pairs' contact breaking thresholds (world_of, breaking_thresholds): capsule ci's link against
+     * the table / plane / cube / an obstacle, and the cube against the table / plane */
+    double tau_table[PGX_MAX_CAPSULES], tau_plane[PGX_MAX_CAPSULES], tau_cube[PGX_MAX_CAPSULES],
+        tau_obst[PGX_MAX_CAPSULES];
+    double tau_cube_table, tau_cube_plane;
 } world_t;
 
 /* closest pair of a capsule and an obstacle (ReachAO section below): signed distance d,
@@ -736,11 +745,13 @@ static int man_add(double* P, int cap, int key, const double* np, double thr2) {
     if (near >= 0) {   /* replaceContactPoint: the cached impulse stays */
         double* c = pool_pt(P, idx[near]);
         memcpy(c + MP_LA, np + MP_LA, (MP_IMP - MP_LA) * sizeof(double));
+        PGXO_HIST_ADD(pgxo_diag_hist, 121, 1);
         return near;
     }
     if (n < 4) {
         const int cnt = (int)P[0];
         if (cnt >= cap) { PGXO_HIST_ADD(pgxo_diag_hist, 120, 1); return -1; }
+        PGXO_HIST_ADD(pgxo_diag_hist, 122, 1);
         double* c = pool_pt(P, cnt);
         memcpy(c, np, MAN_PT * sizeof(double));
         c[MP_KID] = key + n;
@@ -749,6 +760,7 @@ static int man_add(double* P, int cap, int key, const double* np, double thr2) {
         return n;
     }
     const int slot = man_sort_cached(P, idx, np);
+    PGXO_HIST_ADD(pgxo_diag_hist, 123, 1);
     double* c = pool_pt(P, idx[slot]);
     memcpy(c + MP_LA, np + MP_LA, (MP_IMP - MP_LA) * sizeof(double));
     c[MP_IMP] = 0.0;
@@ -757,7 +769,7 @@ static int man_add(double* P, int cap, int key, const double* np, double thr2) {
 /* refreshContactPoints of every manifold in the pool, from the points' world positions pa, pb:
  * distance along the stored normal, then per manifold in reverse slot order the removals (the
  * last slot's point takes a removed point's slot); the pool keeps the survivors' order */
-static void pool_refresh(double* P, const double (*pa)[3], const double (*pb)[3], double thr) {
+static void pool_refresh(double* P, const double (*pa)[3], const double (*pb)[3], const double* thr) {
     const int cnt = (int)P[0];
     int drop[PGXO_POOL_MAX];
     for (int i = 0; i < cnt; i++) {
@@ -765,11 +777,13 @@ static void pool_refresh(double* P, const double (*pa)[3], const double (*pb)[3]
         const double* n = c + MP_N;
         const double d = (pa[i][0] - pb[i][0]) * n[0] + (pa[i][1] - pb[i][1]) * n[1] + (pa[i][2] - pb[i][2]) * n[2];
         c[MP_D] = d;
-        drop[i] = d > thr;
-        if (!drop[i]) {
+        drop[i] = d > thr[i];
+        if (drop[i]) PGXO_HIST_ADD(pgxo_diag_hist, 124, 1);
+        else {
             double e[3];
             for (int j = 0; j < 3; j++) e[j] = pb[i][j] - (pa[i][j] - n[j] * d);
-            drop[i] = v3_dot(e, e) > thr * thr;
+            drop[i] = v3_dot(e, e) > thr[i] * thr[i];
+            if (drop[i]) PGXO_HIST_ADD(pgxo_diag_hist, 125, 1);
         }
     }
     int seen[PGXO_POOL_MAX] = {0};
@@ -811,10 +825,12 @@ int pgxo_manifold_add(double* P, int cap, int key, const double* point, double t
     return man_add(P, cap, key, point, thr * thr);
 }
 void pgxo_manifold_refresh_static(double* P, double thr) {
-    double pa[PGXO_POOL_MAX][3], pb[PGXO_POOL_MAX][3];
-    for (int i = 0; i < (int)P[0]; i++)
+    double pa[PGXO_POOL_MAX][3], pb[PGXO_POOL_MAX][3], th[PGXO_POOL_MAX];
+    for (int i = 0; i < (int)P[0]; i++) {
         for (int j = 0; j < 3; j++) { pa[i][j] = pool_pt(P, i)[MP_LA + j]; pb[i][j] = pool_pt(P, i)[MP_LB + j]; }
-    pool_refresh(P, pa, pb, thr);
+        th[i] = thr;
+    }
+    pool_refresh(P, pa, pb, th);
 }
 
 /* a pair's new point: the contact, its manifold key and its merge order */
@@ -822,9 +838,20 @@ typedef struct { contact_t c; int key, order; } newpt_t;
 #define NEWPT_MAX (4 * PGX_MAX_CAPSULES + PGX_MAX_CAPSULES * PGX_AO_OBSTACLES)
 
 /* contact detection; returns the number of contacts (grouped, each group sorted by id) */
+/* the breaking threshold of manifold `key`'s pair: capsule vs cube / obstacle, or (study mode) a table /
+ * plane end sphere -- for a table key of a new point `c` gives its box, else the key's code */
+static double key_threshold(const world_t* W, int key, const contact_t* c) {
+    (void)c;
+    if (key >= KEY_TABLE) {
+        const int ci = (key - KEY_TABLE) / 64, code = ((key - KEY_TABLE) >> 3) & 7;
+        return code == PAIR_PLANE ? W->tau_plane[ci] : W->tau_table[ci];
+    }
+    const int ci = key_capsule(key, W->has_object);
+    return W->has_object ? W->tau_cube[ci] : W->tau_obst[ci];
+}
+
 static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W, const kin_t* k, double* obj,
                   contact_t* out) {
-    const double tau = p->contact_distance;
     static PGXO_TLS cands_t s0, s1;   /* per thread (cpu_baseline runs shards in threads) */
     s0.n = 0; s1.n = 0;
     /* Bullet's persistent manifolds for the cube / obstacle pairs (the default budget), and with the
@@ -843,7 +870,7 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
             for (int i = 0; i < 3; i++) P[i] += obj[i];
             double zt = ground_z(W, P);
             double d = P[2] - zt;
-            if (d < tau) {
+            if (d < (zt == W->plane_z ? W->tau_cube_plane : W->tau_cube_table)) {
                 contact_t c = {0, v, -1, {0, 0, 1}, {P[0], P[1], P[2]}, {P[0], P[1], zt}, d, NULL, 0.0, 0};
                 cand_add(&s0, &c, zt == W->plane_z ? PAIR_PLANE : PAIR_TABLE);
             }
@@ -864,7 +891,7 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
                 const double* P = e ? B : A;
                 double zt = ground_z(W, P);
                 double d = P[2] - r - zt;
-                if (d < tau) {
+                if (d < (zt == W->plane_z ? W->tau_plane[ci] : W->tau_table[ci])) {
                     contact_t c = {1, 2 * ci + e, li, {0, 0, 1}, {P[0], P[1], P[2] - r}, {P[0], P[1], zt}, d, NULL,
                                    0.0, 0};
                     const int code = zt == W->plane_z ? PAIR_PLANE : PAIR_TABLE;
@@ -905,7 +932,7 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
                     qb[ax] = sg * h;
                     depth = -bst - r;
                 }
-                if (depth < tau) {
+                if (depth < W->tau_cube[ci]) {
                     contact_t c;
                     c.grp = 2; c.id = 32 + ci * 16 + s; c.link = li; c.dist = depth;
                     c.mp = NULL; c.imp = 0.0; c.sub = 0;
@@ -932,9 +959,9 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
             for (int o = 0; o < PGX_AO_OBSTACLES; o++) {
                 /* the axis-to-centre distance minus the radii bounds the pair from below: a pair
                  * that cannot be within tau is not measured (the same candidates) */
-                if (ao_pair_lower_bound(A, B, r, o, W->obst) >= tau) continue;
+                if (ao_pair_lower_bound(A, B, r, o, W->obst) >= W->tau_obst[ci]) continue;
                 const cdist_t cd = ao_capsule_obstacle(A, B, r, o, W->obst);
-                if (cd.d < tau) {
+                if (cd.d < W->tau_obst[ci]) {
                     contact_t c = {1, 32 + 6 * ci + o, li, {-cd.n[0], -cd.n[1], -cd.n[2]},
                                    {cd.pa[0], cd.pa[1], cd.pa[2]}, {cd.pb[0], cd.pb[1], cd.pb[2]}, cd.d, NULL, 0.0, 0};
                     if (pers) {
@@ -952,8 +979,8 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
     if (pers) {
         double* P = obj + OBJ_MAN;
         const int cap = pers_table ? PGXO_POOL_MAX : (W->has_object ? PGX_MANIFOLD_POOL : PGX_MANIFOLD_POOL_AO);
-        const double thr = tau;   /* the breaking threshold (gContactBreakingThreshold 0.02) */
-        /* 1. addContactPoint in merge order (insertion sort by order) */
+        /* 1. addContactPoint in merge order (insertion sort by order), within the pair's breaking
+         * threshold */
         for (int i = 1; i < nnp; i++)
             for (int j = i; j > 0 && np[j].order < np[j - 1].order; j--) { newpt_t t = np[j]; np[j] = np[j - 1]; np[j - 1] = t; }
         for (int j = 0; j < nnp; j++) {
@@ -973,12 +1000,17 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
             pt[MP_D] = c->dist;
             pt[MP_KID] = 0.0;
             pt[MP_IMP] = 0.0;
+            const double thr = key_threshold(W, np[j].key, &np[j].c);
             man_add(P, cap, np[j].key, pt, thr * thr);
         }
-        /* 2. refreshContactPoints: move the points with their bodies, drop the broken ones */
+        /* 2. refreshContactPoints: move the points with their bodies, drop the broken ones (each
+         * against its pair's threshold) */
         const int cnt = (int)P[0];
-        double pa[PGXO_POOL_MAX][3], pb[PGXO_POOL_MAX][3];
-        for (int i = 0; i < cnt; i++) man_world(m, k, obj, W->has_object, pool_pt(P, i), pa[i], pb[i]);
+        double pa[PGXO_POOL_MAX][3], pb[PGXO_POOL_MAX][3], thr[PGXO_POOL_MAX];
+        for (int i = 0; i < cnt; i++) {
+            man_world(m, k, obj, W->has_object, pool_pt(P, i), pa[i], pb[i]);
+            thr[i] = key_threshold(W, (int)pool_pt(P, i)[MP_KID] & ~3, NULL);
+        }
         pool_refresh(P, pa, pb, thr);
         /* 3. the manifold points are the group's candidates after the fresh table ones, in pool order,
          * each its own pair (a manifold holds <= 4 already) */
@@ -1301,7 +1333,69 @@ void pgxo_substep(const pgx_model* m, const pgx_sim_params* p, const double base
     substep_impl(m, p, base, q, qd, motors, st, NULL, NULL);
 }
 
+/* Bullet's contact breaking threshold per pair (btCollisionDispatcher::getNewManifold: with
+ * CD_USE_RELATIVE_CONTACT_BREAKING_THRESHOLD, which btCollisionDispatcher's constructor sets and
+ * pybullet keeps, the smaller of the two collision shapes' getContactBreakingThreshold(
+ * gContactBreakingThreshold); btCollisionShape::getContactBreakingThreshold = getAngularMotionDisc()
+ * x that, getAngularMotionDisc = the bounding sphere of the shape's AABB at the identity, radius
+ * |max - min| / 2, plus |its centre|).  The shapes: a robot link's compound (pgx_model.link_aabb_*,
+ * child and compound margins included), and the scene's createMultiBody boxes and spheres, each a
+ * URDF-importer compound of one child at its origin (AABB half extents + the compound margin 0.001):
+ * the table and the plane (create_plane: half extents 3 x 3 x 0.01, pybullet.py:759-778), the cube
+ * (object_half), the obstacles (sphere radius / cuboid half extent 0.05, reach_ao.py:819-860).
+ * PGX_FLAG_GLOBAL_BREAKING: the global contact_distance for every pair (rounds 2-5). */
+#define URDF_COMPOUND_MARGIN 0.001
+static double box_disc(double hx, double hy, double hz) {
+    const double a = hx + URDF_COMPOUND_MARGIN, b = hy + URDF_COMPOUND_MARGIN, c = hz + URDF_COMPOUND_MARGIN;
+    return sqrt(a * a + b * b + c * c);
+}
+static double dmin2(double a, double b) { return a < b ? a : b; }
+/* (model constants, not per-step work: the operation-counting build leaves them out of the count) */
+#ifndef PGXO_CONST_BEGIN
+#define PGXO_CONST_BEGIN ((void)0)
+#define PGXO_CONST_END ((void)0)
+#endif
+static void breaking_thresholds(const pgx_config* c, world_t* W) {
+    PGXO_CONST_BEGIN;
+    const pgx_model* m = c->model;
+    const double tau = c->params->contact_distance;
+    const int rel = !(c->params->flags & PGX_FLAG_GLOBAL_BREAKING);
+    const double t_table = rel ? box_disc(c->table_half[0], c->table_half[1], c->table_half[2]) * tau : tau;
+    const double t_plane = rel ? box_disc(3.0, 3.0, 0.01) * tau : tau;
+    const double t_cube = rel ? box_disc(c->object_half, c->object_half, c->object_half) * tau : tau;
+    const double t_obst = rel ? box_disc(0.05, 0.05, 0.05) * tau : tau;
+    for (int ci = 0; ci < m->n_capsules; ci++) {
+        const int li = m->cap_link[ci];
+        double t_link = tau;
+        if (rel && li >= 0) t_link = (v3_norm(m->link_aabb_half[li]) + v3_norm(m->link_aabb_center[li])) * tau;
+        W->tau_table[ci] = dmin2(t_link, t_table);
+        W->tau_plane[ci] = dmin2(t_link, t_plane);
+        W->tau_cube[ci] = dmin2(t_link, t_cube);
+        W->tau_obst[ci] = dmin2(t_link, t_obst);
+    }
+    W->tau_cube_table = dmin2(t_cube, t_table);
+    W->tau_cube_plane = dmin2(t_cube, t_plane);
+    PGXO_CONST_END;
+}
+
+/* test entry point: out[4 * PGX_MAX_CAPSULES + 2] = the table, plane, cube and obstacle thresholds per
+ * capsule, then the cube's against the table and the plane */
+void pgxo_breaking_thresholds(const pgx_config* c, double* out) {
+    world_t W;
+    memset(&W, 0, sizeof W);
+    breaking_thresholds(c, &W);
+    for (int i = 0; i < PGX_MAX_CAPSULES; i++) {
+        out[i] = W.tau_table[i];
+        out[PGX_MAX_CAPSULES + i] = W.tau_plane[i];
+        out[2 * PGX_MAX_CAPSULES + i] = W.tau_cube[i];
+        out[3 * PGX_MAX_CAPSULES + i] = W.tau_obst[i];
+    }
+    out[4 * PGX_MAX_CAPSULES] = W.tau_cube_table;
+    out[4 * PGX_MAX_CAPSULES + 1] = W.tau_cube_plane;
+}
+
 static void world_of(const pgx_config* c, world_t* W) {
+    breaking_thresholds(c, W);
     W->contacts = c->contacts;
     W->has_object = c->task == PGX_TASK_PUSH || c->task == PGX_TASK_PICK_AND_PLACE;
     W->half = c->object_half;

@@ -71,6 +71,7 @@ void pgxo_set_robot_budget(int budget);
 int pgxo_manifold_add(double* pool, int cap, int key, const double* point, double thr);
 void pgxo_manifold_refresh_static(double* pool, double thr);
 void pgxo_pair_hist_read(int64_t* out, int clear);
+void pgxo_breaking_thresholds(const pgx_config* c, double* out);
 /* the last contact detection's points (group 0 object-scene / 1 robot-table / 2 robot-object,
  * feature id, robot link or -1, separation); returns their number */
 int pgxo_last_contacts(int32_t* grp, int32_t* id, int32_t* link, double* dist);

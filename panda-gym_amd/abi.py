@@ -42,6 +42,7 @@ FLAG_LINKSTATE_CURRENT = 8   # getLinkState at the pose after the last substep (
 FLAG_DYN_RECURSIVE = 16      # oracle: M, b by CRBA + Newton-Euler (the kernel's formulation), for the op count
 FLAG_PERSISTENT_MANIFOLD = 32  # oracle study: the table / plane pairs through persistent manifolds too
 FLAG_FRESH_MANIFOLD = 64       # oracle study: round 4's per-substep rule for the cube / obstacle pairs
+FLAG_GLOBAL_BREAKING = 128     # oracle study: the global 0.02 breaking threshold for every pair (rounds 2-5)
 
 HER_FUTURE, HER_FINAL, HER_EPISODE = 0, 1, 2
 
@@ -64,6 +65,7 @@ class PgxModel(C.Structure):
         ("cap_link", C.c_int32 * MAX_CAPSULES), ("cap_flags", C.c_int32 * MAX_CAPSULES),
         ("cap_a", (C.c_double * 3) * MAX_CAPSULES), ("cap_b", (C.c_double * 3) * MAX_CAPSULES),
         ("cap_radius", C.c_double * MAX_CAPSULES),
+        ("link_aabb_center", (C.c_double * 3) * MAX_LINKS), ("link_aabb_half", (C.c_double * 3) * MAX_LINKS),
     ]
 
 
@@ -185,6 +187,11 @@ def make_model(model: Model, ee_link: int = 11) -> PgxModel:
         m.cap_link[i], m.cap_flags[i], m.cap_radius[i] = c["link"], c["flags"], c["r"]
         for k in range(3):
             m.cap_a[i][k], m.cap_b[i][k] = c["a"][k], c["b"][k]
+    assert len(model.aabb_half) == model.n_links, "model table without link AABBs: rerun tools/build_models.py"
+    for i in range(model.n_links):
+        for k in range(3):
+            m.link_aabb_center[i][k] = model.aabb_center[i][k]
+            m.link_aabb_half[i][k] = model.aabb_half[i][k]
     return m
 
 
@@ -208,7 +215,7 @@ def default_sim_params(n_substeps: int = 20, flags: int = 0) -> PgxSimParams:
     p.num_iterations = 50                    # pybullet numSolverIterations
     p.ik_max_iters = 20                      # calculateInverseKinematics maxNumIterations
     p.flags = flags
-    p.contact_distance = 0.02                # gContactBreakingThreshold (contact processing threshold)
+    p.contact_distance = 0.02                # gContactBreakingThreshold (scaled per pair: pgx.h)
     p.contact_erp = 0.2                      # btMultiBodyConstraintSolver: contacts use m_erp
     p.friction = 0.5 * 0.5                   # default lateral friction 0.5 per body, product combine
     p.warmstart = 0.85                       # btContactSolverInfo m_warmstartingFactor

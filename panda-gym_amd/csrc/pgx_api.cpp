@@ -295,6 +295,35 @@ static int build_dev_model(const pgx_config* cfg, PgxDevModel* dm) {
         const int li = m->cap_link[c];
         dm->cap_mu[c] = (float)(li >= 0 && li < PGX_MAX_LINKS ? p->link_friction[li] : p->friction);
     }
+    /* Bullet's contact breaking threshold per pair (btCollisionDispatcher::getNewManifold with its
+     * default CD_USE_RELATIVE_CONTACT_BREAKING_THRESHOLD): the smaller of the two collision shapes'
+     * angular motion disc (|AABB half extents| + |AABB centre|) x contact_distance.  The robot links'
+     * compounds from the model (link_aabb_*); the scene's createMultiBody shapes are URDF-importer
+     * compounds of one child at the origin (+ the compound margin 0.001): the table, the plane (half
+     * extents 3 x 3 x 0.01, panda_gym/pybullet.py:759-778), the cube, the obstacles (0.05,
+     * reach_ao.py:819-860).  The oracle restates the same (oracle/pgx_oracle.c breaking_thresholds). */
+    {
+        const double tau = p->contact_distance, mg = 0.001;
+        auto box_disc = [&](double hx, double hy, double hz) {
+            return std::sqrt((hx + mg) * (hx + mg) + (hy + mg) * (hy + mg) + (hz + mg) * (hz + mg));
+        };
+        auto nrm = [](const double* v) { return std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); };
+        const double t_table = box_disc(cfg->table_half[0], cfg->table_half[1], cfg->table_half[2]) * tau;
+        const double t_plane = box_disc(3.0, 3.0, 0.01) * tau;
+        const double t_obj = box_disc(cfg->object_half, cfg->object_half, cfg->object_half) * tau;
+        const double t_obst = box_disc(0.05, 0.05, 0.05) * tau;
+        for (int c = 0; c < 16; c++) {
+            const int li = c < m->n_capsules ? m->cap_link[c] : -1;
+            const double t_link = (li >= 0 && li < PGX_MAX_LINKS)
+                                      ? (nrm(m->link_aabb_half[li]) + nrm(m->link_aabb_center[li])) * tau : tau;
+            dm->tau_table[c] = (float)std::fmin(t_link, t_table);
+            dm->tau_plane[c] = (float)std::fmin(t_link, t_plane);
+            dm->tau_obj[c] = (float)std::fmin(t_link, t_obj);
+            dm->tau_obst[c] = (float)std::fmin(t_link, t_obst);
+        }
+        dm->tau_obj_table = (float)std::fmin(t_obj, t_table);
+        dm->tau_obj_plane = (float)std::fmin(t_obj, t_plane);
+    }
     if (p->flags != 0) return fail(PGX_E_UNSUPPORTED, "modelling flags are oracle-only");
     int rc = check_compiled_tables(*dm);
     if (!rc) rc = check_capsules(m, R, O);

@@ -44,6 +44,11 @@ struct PgxDevModel {
                                  test resid * resid <= residual_thr as one compare, resid <= t */
     float cap_mu[16];         /* combined lateral friction of capsule c's link against the scene
                                  (pgx_sim_params.link_friction of its link; PGX_NCAP used) */
+    /* contact breaking thresholds per pair (Bullet's relative rule, pgx.h contact_distance): capsule
+     * c's link against the table, the plane, the cube and an obstacle; the cube against the table
+     * and the plane -- the distance within which a point is reported, merged and kept */
+    float tau_table[16], tau_plane[16], tau_obj[16], tau_obst[16];
+    float tau_obj_table, tau_obj_plane;
 };
 
 struct PgxDevEnv {

@@ -747,6 +747,25 @@ constexpr bool AO_PERS = false;
 constexpr bool AO_PERS = true;
 #endif
 
+/* Capsule c's contact breaking threshold against the table / plane / cube / an obstacle (PgxDevModel
+ * tau_*: Bullet's relative per-pair rule, pgx.h contact_distance), selected from the block by
+ * compile-time index -- folded to constants in the default build, where the cube and obstacle pairs
+ * take one value for every capsule (the scene body's disc is the smaller) */
+enum { TAU_TABLE = 0, TAU_PLANE = 1, TAU_OBJ = 2, TAU_OBST = 3 };
+template <int W>
+__device__ __forceinline__ float tau_at(MRef m, int k) {
+    return W == TAU_TABLE ? m.tau_table[k] : W == TAU_PLANE ? m.tau_plane[k] : W == TAU_OBJ ? m.tau_obj[k] : m.tau_obst[k];
+}
+template <int W>
+__device__ __forceinline__ float cap_tau(MRef m, int c) {
+    float v = tau_at<W>(m, 0);
+    sfor<1, PGX_NCAP>([&](auto kc) __attribute__((always_inline)) {
+        constexpr int K = decltype(kc)::value;
+        v = c == K ? tau_at<W>(m, K) : v;
+    });
+    return v;
+}
+
 /* robot points kept per env: the one-lane layout holds its rows in LDS for 64 envs (4); the
  * wide layout 4 in VGPRs, and with FULL (PGX_FLAG_FULL_MANIFOLD) the rest, up to
  * PGX_ROBOT_POINTS / _ARM, in LDS (substep_g's "extra rows") */
@@ -902,8 +921,11 @@ __device__ __forceinline__ void plane_space(V3 n, V3& p, V3& q) {
     }
 }
 
+__device__ __forceinline__ bool on_table(const PgxDevEnv& e, float x, float y) {
+    return fabsf(x - e.table_cx) <= e.table_hx && fabsf(y - e.table_cy) <= e.table_hy;
+}
 __device__ __forceinline__ float ground_z(const PgxDevEnv& e, float x, float y) {
-    return (fabsf(x - e.table_cx) <= e.table_hx && fabsf(y - e.table_cy) <= e.table_hy) ? e.table_top : e.plane_z;
+    return on_table(e, x, y) ? e.table_top : e.plane_z;
 }
 
 /* keep the CG deepest candidates of group 0 (stable: an equal depth does not displace) */
@@ -1255,14 +1277,17 @@ __device__ __forceinline__ void joint_frame(const M3& Rl, V3 ol, int j, M3& R, V
  * after the table candidates, in pool order) as its own row: id = kid, pool index in g1w.
  * OBJ: B is the cube (Rc, op), else a static obstacle (local B = world). */
 template <int OBJ, int AO, class LT>
-__device__ __forceinline__ void man_refresh_insert_g(LT& L, int es, int c, const M3& Rl, V3 ol, const M3& Rc, V3 op,
-                                                     float thr) {
+__device__ __forceinline__ void man_refresh_insert_g(MRef m, LT& L, int es, int c, const M3& Rl, V3 ol, const M3& Rc,
+                                                     V3 op) {
     const int cnt = L.mcnt[es];
     const bool mine = c < cnt;
     const int p = mine ? c : 0;
     const int kid = (int)L.mkid[p][es], key = kid & ~3;
     const int cap = man_capsule<AO>(key < 32 ? 32 : key);
-    const int j = kCapJ[cap < 0 ? 0 : (cap >= PGX_NCAP ? PGX_NCAP - 1 : cap)];
+    const int capc = cap < 0 ? 0 : (cap >= PGX_NCAP ? PGX_NCAP - 1 : cap);
+    const int j = kCapJ[capc];
+    /* the point's pair's breaking threshold: its capsule against the cube / the obstacle */
+    const float thr = AO ? cap_tau<TAU_OBST>(m, capc) : cap_tau<TAU_OBJ>(m, capc);
     M3 R;
     V3 o;
     joint_frame(Rl, ol, j, R, o);
@@ -1469,7 +1494,7 @@ __device__ __forceinline__ void ao_obstacle_candidates(LT& L, int ln, int c, flo
  * along the axis), from the world end points the FK pass left in LDS.  A runtime loop
  * over the capsule table (wave-uniform index: scalar loads) keeps the code compact. */
 template <int OBJ, class LT, int AO = 0>
-__device__ __forceinline__ void robot_contacts(const PgxDevEnv& e, float tau, LT& L, int ln, const ObjState& ob,
+__device__ __forceinline__ void robot_contacts(MRef m, const PgxDevEnv& e, LT& L, int ln, const ObjState& ob,
                                             const M3& Rc) {
     for (int c = 0; c < PGX_NCAP; c++) {
         const V3 A = v3(L.capA[c][0][ln], L.capA[c][1][ln], L.capA[c][2][ln]);
@@ -1479,16 +1504,21 @@ __device__ __forceinline__ void robot_contacts(const PgxDevEnv& e, float tau, LT
         if (flags & PGX_CAP_VS_TABLE) {
             for (int end = 0; end < (ns == 1 ? 1 : 2); end++) {
                 const V3 P = end ? B : A;
-                const float zt = ground_z(e, P.x, P.y);
+                const bool ont = on_table(e, P.x, P.y);
+                const float zt = ont ? e.table_top : e.plane_z;
                 const float d = P.z - r - zt;
-                if (d < tau) g1_insert(L, ln, d, (float)(2 * c + end), jc, v3(P.x, P.y, P.z - r), v3(0.0f, 0.0f, 1.0f),
-                                       v3(0.0f, 0.0f, 0.0f));
+                if (d < (ont ? cap_tau<TAU_TABLE>(m, c) : cap_tau<TAU_PLANE>(m, c)))
+                    g1_insert(L, ln, d, (float)(2 * c + end), jc, v3(P.x, P.y, P.z - r), v3(0.0f, 0.0f, 1.0f),
+                              v3(0.0f, 0.0f, 0.0f));
             }
         }
-        if (OBJ && (flags & PGX_CAP_VS_OBJECT)) object_candidates(e, tau, L, ln, ob, Rc, c, true);
+        if (OBJ && (flags & PGX_CAP_VS_OBJECT)) object_candidates(e, cap_tau<TAU_OBJ>(m, c), L, ln, ob, Rc, c, true);
         /* flags 0: the base and panda_link1, whose capsule lies on the joint-1 axis and cannot
          * move towards an obstacle (the reset keeps them 0.03 clear) */
-        if (AO && flags != 0 && ao_capsule_near(L, ln, c, tau)) ao_obstacle_candidates(L, ln, c, tau);
+        if (AO && flags != 0) {
+            const float tau = cap_tau<TAU_OBST>(m, c);
+            if (ao_capsule_near(L, ln, c, tau)) ao_obstacle_candidates(L, ln, c, tau);
+        }
     }
 }
 
@@ -1542,16 +1572,19 @@ __device__ __forceinline__ CapLane cap_lane() {
  * broadcast only when an env has more -- and every kept candidate goes straight to its id-ordered slot
  * (ids 2c + end grow with the lane), so sort_groups has nothing left to do. */
 template <class LT>
-__device__ __forceinline__ void robot_table_contacts_g(const PgxDevEnv& e, float tau, LT& L, int es, int c) {
+__device__ __forceinline__ void robot_table_contacts_g(MRef m, const PgxDevEnv& e, LT& L, int es, int c) {
     const int cc = c < PGX_NCAP ? c : 0;
     const CapLane cl = cap_lane();
     const bool on = c < PGX_NCAP && (cl.flags & PGX_CAP_VS_TABLE);
     const V3 A = lds3(L.capA[cc], es), B = lds3(L.capB[cc], es);
     const float r = cl.r;
     const bool two = cl.ns != 1;
-    const float d0 = A.z - r - ground_z(e, A.x, A.y);
-    const float d1 = B.z - r - ground_z(e, B.x, B.y);
-    const bool c0 = on && d0 < tau, c1 = on && two && d1 < tau;
+    /* each end against the box under it, within the pair's breaking threshold (cap_tau) */
+    const float tt = cap_tau<TAU_TABLE>(m, cc), tp = cap_tau<TAU_PLANE>(m, cc);
+    const bool t0 = on_table(e, A.x, A.y), t1 = on_table(e, B.x, B.y);
+    const float d0 = A.z - r - (t0 ? e.table_top : e.plane_z);
+    const float d1 = B.z - r - (t1 ? e.table_top : e.plane_z);
+    const bool c0 = on && d0 < (t0 ? tt : tp), c1 = on && two && d1 < (t1 ? tt : tp);
     unsigned m0 = row_ballot(c0), m1 = row_ballot(c1);
     const int total = __builtin_popcount(m0) + __builtin_popcount(m1);
     bool k0 = c0, k1 = c1;
@@ -1616,8 +1649,9 @@ __device__ __forceinline__ void substep_dyn(MRef m, const PgxDevEnv& e, const fl
         for (int vtx = 0; vtx < 8; vtx++) {
             const V3 r = mul(Rc, v3((vtx & 1) ? h : -h, (vtx & 2) ? h : -h, (vtx & 4) ? h : -h));
             const V3 P = ob.p + r;
-            const float d = P.z - ground_z(e, P.x, P.y);
-            if (d < m.contact_dist) g0_insert(*Lp, ln, d, (float)vtx, r);
+            const bool ont = on_table(e, P.x, P.y);
+            const float d = P.z - (ont ? e.table_top : e.plane_z);
+            if (d < (ont ? m.tau_obj_table : m.tau_obj_plane)) g0_insert(*Lp, ln, d, (float)vtx, r);
         }
     }
     /* FK fused with the per-link quantities the dynamics need, so the 3x3
@@ -1655,9 +1689,9 @@ __device__ __forceinline__ void substep_dyn(MRef m, const PgxDevEnv& e, const fl
     }
     if (CONT) {
         if constexpr (PAR && !OBJ && !AO) {
-            robot_table_contacts_g(e, m.contact_dist, *Lp, ln, lane);
+            robot_table_contacts_g(m, e, *Lp, ln, lane);
         } else {
-            robot_contacts<OBJ, LT, AO>(e, m.contact_dist, *Lp, ln, ob, Rc);
+            robot_contacts<OBJ, LT, AO>(m, e, *Lp, ln, ob, Rc);
             sort_groups(*Lp, ln);
         }
     }
@@ -1895,8 +1929,9 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
         const int vtx = c & 7;
         const V3 r = mul(Rc, v3((vtx & 1) ? h : -h, (vtx & 2) ? h : -h, (vtx & 4) ? h : -h));
         const V3 P = ob.p + r;
-        const float d = P.z - ground_z(e, P.x, P.y);
-        const bool cand = c < 8 && d < m.contact_dist;
+        const bool ont = on_table(e, P.x, P.y);
+        const float d = P.z - (ont ? e.table_top : e.plane_z);
+        const bool cand = c < 8 && d < (ont ? m.tau_obj_table : m.tau_obj_plane);
         const float dd = cand ? d : 3.0e38f;
         int rank = 0;
         sfor<0, 8>([&](auto uc) __attribute__((always_inline)) {
@@ -1948,7 +1983,7 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
     }
     if (CONT) {
         if constexpr (!OBJ) {
-            robot_table_contacts_g(e, m.contact_dist, *Lp, es, c);
+            robot_table_contacts_g(m, e, *Lp, es, c);
             if constexpr (AO) {
                 /* obstacle contacts (ao_obstacle_candidates), lane-parallel: per obstacle, lane c
                  * measures capsule c's pair (the cull first, the exact query only where the pair
@@ -1957,8 +1992,8 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                  * values, and finally put in id order.  Obstacle-major insertion instead of
                  * robot_contacts' capsule-major order: only an exact depth tie could order
                  * differently. */
-                const float tau = m.contact_dist;
                 const int cc = c < PGX_NCAP ? c : 0;
+                const float tau = cap_tau<TAU_OBST>(m, cc);   /* this lane's capsule against an obstacle */
                 const CapLane cl = cap_lane();
                 const bool cap_on = c < PGX_NCAP && cl.flags != 0;
                 /* check (every substep but the first): the step loop's check_collided of the
@@ -2079,13 +2114,14 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                                 const V3 pbk = v3(__shfl(pb.x, src), __shfl(pb.y, src), __shfl(pb.z, src));
                                 const V3 nk = v3(__shfl(n.x, src), __shfl(n.y, src), __shfl(n.z, src));
                                 const float dk = __shfl(d, src);
-                                man_add_g(*Lp, es, c, 32 + 24 * k + 4 * o, lak, pbk, (-1.0f) * nk, dk, tau * tau);
+                                const float tk = cap_tau<TAU_OBST>(m, k);
+                                man_add_g(*Lp, es, c, 32 + 24 * k + 4 * o, lak, pbk, (-1.0f) * nk, dk, tk * tk);
                             }
                         }
                     }
                     if (__any(Lp->mcnt[es] > 0))
-                        man_refresh_insert_g<0, 1>(*Lp, es, c, Rl, ol, M3{{1, 0, 0, 0, 1, 0, 0, 0, 1}}, v3(0.0f, 0.0f, 0.0f),
-                                                   tau);
+                        man_refresh_insert_g<0, 1>(m, *Lp, es, c, Rl, ol, M3{{1, 0, 0, 0, 1, 0, 0, 0, 1}},
+                                                   v3(0.0f, 0.0f, 0.0f));
                 }
             }
         } else {
@@ -2103,14 +2139,14 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                 float t = l2 > 0.0f ? dot(ob.p - A, ab) * fast_rcp(l2) : 0.0f;
                 t = fminf(fmaxf(t, 0.0f), 1.0f);
                 const V3 cp = A + t * ab - ob.p;
-                const float reach = cl.r + 1.7320508f * e.obj_half + m.contact_dist;
+                const float reach = cl.r + 1.7320508f * e.obj_half + cap_tau<TAU_OBJ>(m, cc);
                 near = dot(cp, cp) < reach * reach;
             }
             /* table candidates lane-parallel (id-ordered, so re-sorted by depth: ids grow with
              * discovery among them), then the near capsules' object spheres inserted by depth
              * (g1_insert), then id order; only exact depth ties between a table and an object
              * candidate could order differently from robot_contacts' discovery order */
-            robot_table_contacts_g(e, m.contact_dist, *Lp, es, c);
+            robot_table_contacts_g(m, e, *Lp, es, c);
             const uint64_t bn = __ballot(near);
             unsigned wm = (unsigned)((bn | (bn >> 16) | (bn >> 32) | (bn >> 48)) & 0xFFFFu);
             if constexpr (FULL) {
@@ -2122,9 +2158,9 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                 while (wm) {
                     const int cn = __builtin_ctz(wm);
                     wm &= wm - 1u;
-                    object_new_point_g(e, m.contact_dist, *Lp, es, ob, Rc, cn, c, ((rm >> cn) & 1u) != 0, Rl, ol);
+                    object_new_point_g(e, cap_tau<TAU_OBJ>(m, cn), *Lp, es, ob, Rc, cn, c, ((rm >> cn) & 1u) != 0, Rl, ol);
                 }
-                if (__any(Lp->mcnt[es] > 0)) man_refresh_insert_g<1, 0>(*Lp, es, c, Rl, ol, Rc, ob.p, m.contact_dist);
+                if (__any(Lp->mcnt[es] > 0)) man_refresh_insert_g<1, 0>(m, *Lp, es, c, Rl, ol, Rc, ob.p);
                 PGX_PROF_MARK(21);
             } else if (wm) {
                 const unsigned rm = row_ballot(near);
@@ -2133,7 +2169,7 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
                 while (wm) {
                     const int cn = __builtin_ctz(wm);
                     wm &= wm - 1u;
-                    object_candidates_g(e, m.contact_dist, *Lp, es, ob, Rc, cn, c, ((rm >> cn) & 1u) != 0);
+                    object_candidates_g(e, cap_tau<TAU_OBJ>(m, cn), *Lp, es, ob, Rc, cn, c, ((rm >> cn) & 1u) != 0);
                 }
                 PGX_PROF_MARK(21);
                 sort_groups(*Lp, es);

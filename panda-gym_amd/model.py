@@ -88,6 +88,10 @@ class Model:
     collision: List[dict] = field(default_factory=list)
     # constraint order after Bullet's island quicksort: list of (kind, dof) with kind 'limit'|'motor'
     constraint_order: List[Tuple[str, int]] = field(default_factory=list)
+    # per link: Bullet's link compound AABB in the link COM frame, the compound margin included
+    # (btCompoundShape::getAabb with the identity): centre [3], half extents [3]
+    aabb_center: List[List[float]] = field(default_factory=list)
+    aabb_half: List[List[float]] = field(default_factory=list)
 
     @property
     def n_links(self) -> int:
@@ -319,13 +323,16 @@ def parse_urdf(path: str, mesh_root: Optional[str] = None, name: Optional[str] =
         if mins:
             lo, hi = np.min(mins, axis=0), np.max(maxs, axis=0)
             half = (hi - lo) * 0.5 + URDF_MARGIN     # link compound margin
+            center = (hi + lo) * 0.5
         else:
             half = np.full(3, URDF_MARGIN)          # empty compound: zero extents + margin
-        return half, prims
+            center = np.zeros(3)
+        return half, prims, center
 
     parent, jtype, dof_of_link, link_of_dof = [], [], [], []
     jpos, jrot, axis, com, mass, inertia = [], [], [], [], [], []
     lower, upper, has_limit, effort, names, prims_all = [], [], [], [], [], []
+    aabb_center, aabb_half = [], []
     for li, (cname, j) in enumerate(order):
         pname = j.find("parent").get("link")
         parent.append(index.get(pname, -1))
@@ -348,8 +355,10 @@ def parse_urdf(path: str, mesh_root: Optional[str] = None, name: Optional[str] =
         assert np.allclose(crot, np.eye(3)), "rotated inertial frames are not supported"
         com.append(cxyz.tolist())
         mass.append(m)
-        half, prims = collision_aabb_and_prims(cname, li)
+        half, prims, center = collision_aabb_and_prims(cname, li)
         prims_all += prims
+        aabb_center.append(center.tolist())
+        aabb_half.append(half.tolist())
         lx, ly, lz = 2 * half
         if m != 0.0:
             inertia.append([m / 12.0 * (ly * ly + lz * lz), m / 12.0 * (lx * lx + lz * lz),
@@ -384,7 +393,7 @@ def parse_urdf(path: str, mesh_root: Optional[str] = None, name: Optional[str] =
                  jtype=jtype, dof_of_link=dof_of_link, link_of_dof=link_of_dof, jpos=jpos, jrot=jrot,
                  axis=axis, com=com, mass=mass, inertia=inertia, lower=lower, upper=upper,
                  has_limit=has_limit, effort=effort, base_com=bxyz.tolist(), collision=prims_all,
-                 constraint_order=cons)
+                 constraint_order=cons, aabb_center=aabb_center, aabb_half=aabb_half)
 
 
 def load_model(name: str = "panda_custom0") -> Model:

@@ -96,6 +96,8 @@ def _one_step_errors(pg, oracle, env_id, n, steps, seed, actions=None, lanes=0, 
                  ref.episode.copy())
         if actions is None:
             a = venv.sample_actions(t).clone()
+        elif callable(actions):   # a policy of the device observation before the step
+            a = torch.as_tensor(actions(venv.obs.cpu().numpy(), t), device="cuda:0")
         else:   # one action for every env, or one per env
             at = np.asarray(actions[t], np.float32)
             a = torch.as_tensor(at if at.ndim == 2 else np.repeat(at[None], n, 0), device="cuda:0")
@@ -270,6 +272,49 @@ def test_full_manifold_random_policy_one_step_parity(pg, oracle, env_id):
         assert rec["err_ee"] <= OUTLIER or s_ee >= rec["err_ee"], (rec["t"], rec["env"], rec["err_ee"], s_ee)
         assert rec["err_ag"] <= OUTLIER or s_ag >= rec["err_ag"], (rec["t"], rec["env"], rec["err_ag"], s_ag)
     assert final["object"].cpu().numpy()[2].min() > -0.4
+
+
+@pytest.mark.parametrize("env_id", ["PandaPush-v3", "PandaPickAndPlace-v3"])
+def test_persistent_manifold_branches_under_a_scripted_push(pg, oracle, env_id):
+    """Bullet's persistent manifolds where the arm works the cube (tests/scripted_push.py: per env a
+    randomised approach that brings the tool bar and the hand down beside the cube and pushes it),
+    from the same state every step, 256 envs x 40 steps: every branch of the oracle's manifold --
+    addContactPoint's merge (replaceContactPoint), append and sortCachedPoints replacement,
+    refreshContactPoints' removal past the threshold and by sliding -- runs at least 100 times
+    (oracle diagnostics), the device and oracle pools agree point for point in >= 999 of 1000
+    env-steps, and the per-step position bars of the random-policy test hold."""
+    import ctypes as C
+
+    from scripted_push import ScriptedPush
+
+    n, steps = 256, 40
+    pol = ScriptedPush(n, seed=7, obj_col=6 if env_id == "PandaPush-v3" else 7)
+    act = (lambda obs, t: pol(obs, t)) if env_id == "PandaPush-v3" else \
+        (lambda obs, t: np.concatenate([pol(obs, t), np.zeros((n, 1), np.float32)], axis=1))
+    diag = np.zeros(128, np.int64)
+    oracle.lib().pgxo_diag_read(diag.ctypes.data_as(C.c_void_p), 1)
+    outl, env, pools = [], {}, {}
+    ee, ag, final = _one_step_errors(pg, oracle, env_id, n, steps, 3, actions=act, lanes=16, outliers=outl,
+                                     full=True, envelope=env, pools=pools)
+    cfg, _keep = outl.pop()
+    oracle.lib().pgxo_diag_read(diag.ctypes.data_as(C.c_void_p), 1)
+    branches = {"merge": int(diag[121]), "append": int(diag[122]), "replace": int(diag[123]),
+                "drop_distance": int(diag[124]), "drop_slide": int(diag[125]), "pool_full": int(diag[120])}
+    print(f"\n{env_id} scripted push: manifold branches {branches}, pools {pools}")
+    for k in ("merge", "append", "replace", "drop_distance", "drop_slide"):
+        assert branches[k] >= 100, branches
+    assert pools.get("mismatch", 0) <= pools["env_steps"] // 1000, pools
+    for name, e, f in (("ee", ee, env["ee"]), ("object", ag, env["ag"])):
+        print(f"{name}: p99 {np.percentile(e, 99):.2e} p99.9 {np.percentile(e, 99.9):.2e} max {e.max():.2e}")
+        assert np.percentile(e, 99) <= 1e-5, (name, np.percentile(e, 99))
+        _inside_envelope(name, e, f, pcts=(99.9,))
+        assert e.max() <= 1e-2, (name, e.max())
+    assert len(outl) <= ee.size // 2000, len(outl)
+    for rec in outl:
+        s_ee, s_ag = _self_sensitivity(oracle, cfg, rec, trials=64)
+        s_ee, s_ag = max(s_ee, rec["f32_ee"]), max(s_ag, rec["f32_ag"])
+        assert rec["err_ee"] <= OUTLIER or s_ee >= rec["err_ee"], (rec["t"], rec["env"], rec["err_ee"], s_ee)
+        assert rec["err_ag"] <= OUTLIER or s_ag >= rec["err_ag"], (rec["t"], rec["env"], rec["err_ag"], s_ag)
 
 
 def test_scripted_push_moves_cube_like_oracle(pg, oracle):
@@ -453,7 +498,7 @@ def test_contact_budget_cases_keep_all_points(pg, oracle, case, lanes):
     into at most 4 per pair; the one-lane kernels keep their default budget of 4, the deepest
     candidates.  One substep per env step, so after a step the device's contact cache holds the
     rows of that substep: the oracle's feature ids; and the step matches."""
-    from test_oracle_contacts import TWO_LINKS_ON_TABLE_Q
+    from test_oracle_contacts import TWO_LINKS_ON_TABLE_REL_Q as TWO_LINKS_ON_TABLE_Q   # (the device's rule)
 
     n = 4
     env_id = "PandaReach-v3" if case == "two_links_on_table" else "PandaPush-v3"
@@ -531,14 +576,19 @@ def test_object_kernel_points_past_the_register_budget(pg, oracle):
     rounding-level perturbation of its input (the one-step tests' outlier rule)."""
     from oracle import oracle as orc
 
+    from scripted_push import ScriptedPush
+
     n, keys = 4096, ("q", "qd", "qc", "goal", "object", "contacts", "elapsed", "episode", "manifolds")
     big = pg.PandaVecEnv("PandaPush-v3", num_envs=n, device="cuda:0", seed=5)
-    big.reset_tensors(episode_phase="staggered")
+    big.reset_tensors()
+    # the scripted push (tests/scripted_push.py): with Bullet's relative breaking thresholds (round 6)
+    # the random policy's arm almost never holds seven robot points
+    pol = ScriptedPush(n, seed=11)
     found = []
     for t in range(100):
         st = big.state()
         pre = {k: st[k].clone() for k in keys}
-        a = big.sample_actions(t).clone()
+        a = torch.as_tensor(pol(big.obs.cpu().numpy(), t), device="cuda:0")
         big.step_tensors(a)
         cnt = (big.state()["contacts"][2 * orc.OBJECT_POINTS::2] >= 0).sum(0)
         idx = torch.nonzero(cnt > 6).flatten()

@@ -162,6 +162,10 @@ def test_euler_matches_pybullet_convention(oracle, rpy):
 # closed fingertips.
 TWO_LINKS_ON_TABLE_Q = [-1.1690350756013894, 0.6106566125901616, 0.23087389083588095, -2.3777880820996167,
                         0.6961929207547803, 1.5588531369310048, -0.6269433985552224]
+# the same case at Bullet's relative thresholds (round 6, found by sampling joint space, every end at
+# least 3e-4 from its pair's threshold): panda_link8's three capsules and the hand, 5 points within
+# 1.5 mm of the table top
+TWO_LINKS_ON_TABLE_REL_Q = [0.526566, 1.546148, -1.128492, -1.578053, 2.257213, 0.547753, 0.653782]
 
 
 def _detect(oracle, cfg, q, obj, budget=-1):
@@ -184,8 +188,12 @@ def _robot(pts):
 
 
 def test_two_links_on_table_keep_all_points(oracle):
+    """The budget's mechanics on five table points of two links (at the global 0.02 threshold of the
+    study flag, which reports them all); at Bullet's relative per-pair threshold (the default) the
+    same pose reports the subset within each link's own threshold."""
     cfg = _cfg(task=abi.TASK_REACH)
     cfg.contacts = abi.CONTACTS_FULL
+    cfg.params.contents.flags = abi.FLAG_GLOBAL_BREAKING
     obj = _obj((0.0, 0.0, 0.0))
     pts, n_pair = _detect(oracle, cfg, TWO_LINKS_ON_TABLE_Q, obj)
     ids, links, d = _robot(pts)
@@ -196,6 +204,22 @@ def test_two_links_on_table_keep_all_points(oracle):
     pts4, _ = _detect(oracle, cfg, TWO_LINKS_ON_TABLE_Q, obj)
     ids4, _, d4 = _robot(pts4)
     assert len(ids4) == 4 and d4.max() <= np.sort(d)[3]
+    cfg.contacts = abi.CONTACTS_FULL
+    cfg.params.contents.flags = 0                               # Bullet's relative threshold
+    ptsr, _ = _detect(oracle, cfg, TWO_LINKS_ON_TABLE_Q, obj)
+    idsr, linksr, dr = _robot(ptsr)
+    thr = oracle.breaking_thresholds(cfg)["table"]
+    caps = idsr // 2
+    keep = np.array([dd < thr[(i // 2)] for i, dd in zip(ids, d)])
+    assert np.array_equal(idsr, ids[keep]) and np.all(dr < thr[caps])
+    # the relative-threshold pose: all five kept at budget 8, the 4 deepest at the default budget
+    ptsr, n_pair = _detect(oracle, cfg, TWO_LINKS_ON_TABLE_REL_Q, obj)
+    idsr, linksr, dr = _robot(ptsr)
+    assert n_pair == 5 and len(idsr) == 5 and len(set(linksr.tolist())) == 2 and np.all(idsr < 32)
+    assert np.all(dr < thr[idsr // 2]) and np.all(np.diff(idsr) > 0)
+    cfg.contacts = 1
+    ids4, _, d4 = _robot(_detect(oracle, cfg, TWO_LINKS_ON_TABLE_REL_Q, obj)[0])
+    assert len(ids4) == 4 and d4.max() <= np.sort(dr)[3]
 
 
 def test_link_on_cube_keeps_all_points_per_pair_cap(oracle):
@@ -366,3 +390,46 @@ def test_table_manifolds_equal_the_fresh_table_rule(oracle):
     assert n0 >= 1 and n0 == n1          # the bar touches the table in both
     assert pool0 == 0 and pool1 >= 1     # only the study mode keeps manifolds for the table
     assert np.abs(q0 - q1).max() < 1e-9 and np.abs(qd0 - qd1).max() < 1e-7
+
+
+# ---------------------------------------------------------------- contact breaking threshold
+def test_relative_breaking_thresholds(oracle):
+    """Bullet's relative per-pair rule (btCollisionDispatcher::getNewManifold's default
+    CD_USE_RELATIVE_CONTACT_BREAKING_THRESHOLD): min over the pair of (|AABB half| + |AABB centre|)
+    x 0.02, the link compounds' AABBs from the URDF import, the scene's createMultiBody boxes as
+    compounds with margin 0.001.  Restated by hand here, against the oracle's table; the device
+    block (pgx_dev_model_bytes, host only) carries the same values in float; the study flag gives
+    the global 0.02 everywhere."""
+    from panda_gym_amd._native import load
+
+    model = load_model("panda_custom0")
+    m = 0.001
+    disc = lambda *h: float(np.linalg.norm(np.array(h) + m))  # noqa: E731
+    for task in (abi.TASK_REACH, abi.TASK_PUSH):
+        cfg = _cfg(task=task)
+        thr = oracle.breaking_thresholds(cfg)
+        caps = model.capsules(base_capsule=True)
+        for c, cap in enumerate(caps):
+            li = cap["link"]
+            t_link = 0.02 if li < 0 else 0.02 * (np.linalg.norm(model.aabb_half[li]) + np.linalg.norm(model.aabb_center[li]))
+            assert thr["table"][c] == pytest.approx(min(t_link, 0.02 * disc(0.55, 0.35, 0.2)), rel=1e-12)
+            assert thr["plane"][c] == pytest.approx(min(t_link, 0.02 * disc(3.0, 3.0, 0.01)), rel=1e-12)
+            assert thr["cube"][c] == pytest.approx(min(t_link, 0.02 * disc(0.02, 0.02, 0.02)), rel=1e-12)
+            assert thr["obstacle"][c] == pytest.approx(min(t_link, 0.02 * disc(0.05, 0.05, 0.05)), rel=1e-12)
+        assert thr["cube_table"] == pytest.approx(0.02 * disc(0.02, 0.02, 0.02), rel=1e-12)
+        # the robot's links: 2.2 - 7.4 mm against the table; every robot / cube pair at the cube's 0.73 mm
+        arm = [c for c, cap in enumerate(caps) if cap["flags"]]
+        assert 0.002 < thr["table"][arm].min() and thr["table"][arm].max() < 0.008
+        assert np.allclose(thr["cube"][arm], 0.02 * disc(0.02, 0.02, 0.02))
+        lib = load()
+        import ctypes as C
+        lib.pgx_dev_model_bytes.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        buf = np.zeros(312, dtype=np.float32)
+        assert lib.pgx_dev_model_bytes(C.byref(cfg), buf.ctypes.data_as(C.c_void_p), buf.nbytes) == 0
+        for k, name in enumerate(("table", "plane", "cube", "obstacle")):
+            dev = buf[246 + 16 * k: 246 + 16 * k + len(caps)]
+            assert np.array_equal(dev, thr[name][:len(caps)].astype(np.float32)), name
+        assert buf[310] == np.float32(thr["cube_table"]) and buf[311] == np.float32(thr["cube_plane"])
+        cfg.params.contents.flags = abi.FLAG_GLOBAL_BREAKING
+        g = oracle.breaking_thresholds(cfg)
+        assert np.all(g["table"][:len(caps)] == 0.02) and g["cube_table"] == 0.02

@@ -24,13 +24,15 @@ kw = json.loads(os.environ.get("AB_KW", "{}"))   # e.g. AB_KW='{"lanes_per_env":
 if full >= 0:
     kw["full_manifold"] = bool(full)
 venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=0, contacts=contacts, **kw)
-venv.reset_tensors()
-for t in range(30):
+stagger = os.environ.get("AB_STAGGER") == "1"   # steady state: staggered episode phases, one episode of warmup
+venv.reset_tensors(episode_phase="staggered" if stagger else None)
+warm = 60 if stagger else 30
+for t in range(warm):
     venv.step_tensors(venv.sample_actions(t))
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 torch.cuda.synchronize(); e0.record()
 for t in range(100):
-    venv.step_tensors(venv.sample_actions(30 + t))
+    venv.step_tensors(venv.sample_actions(warm + t))
 e1.record(); torch.cuda.synchronize()
 print(e0.elapsed_time(e1) / 100)
 '''
