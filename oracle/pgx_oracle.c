@@ -595,6 +595,37 @@ static void quat_to_mat(const double* q, double* R) {
     R[6] = 2 * (x * z - y * w);     R[7] = 2 * (y * z + x * w);     R[8] = 1 - 2 * (x * x + y * y);
 }
 
+/* A cube vertex P against the table box (top z = tc + th): its signed distance, the contact normal
+ * from the box to P and the point on the box.  Inside the box, the face of least penetration (the top
+ * first, then x, then y on a tie); outside, the closest point of the box -- one face's distance when
+ * only one coordinate lies outside the box's slab (the top face: exactly P.z - top, as rounds 2-5). */
+static double vertex_vs_table(const world_t* W, const double* P, double* n, double* pb) {
+    const double top = W->tc[2] + W->th[2], bot = W->tc[2] - W->th[2];
+    const double qx = P[0] - W->tc[0], qy = P[1] - W->tc[1];
+    const double ex = fabs(qx) - W->th[0], ey = fabs(qy) - W->th[1];
+    const double up = P[2] - top, dn = bot - P[2];
+    const double ez = up >= dn ? up : dn;
+    const double sx = qx < 0 ? -1.0 : 1.0, sy = qy < 0 ? -1.0 : 1.0, sz = up >= dn ? 1.0 : -1.0;
+    pb[0] = P[0]; pb[1] = P[1]; pb[2] = P[2];
+    n[0] = n[1] = n[2] = 0.0;
+    if (ex <= 0 && ey <= 0 && ez <= 0) {   /* inside: the face of least penetration */
+        if (ez >= ex && ez >= ey) { n[2] = sz; pb[2] = sz > 0 ? top : bot; return ez; }
+        if (ex >= ey) { n[0] = sx; pb[0] = W->tc[0] + sx * W->th[0]; return ex; }
+        n[1] = sy; pb[1] = W->tc[1] + sy * W->th[1];
+        return ey;
+    }
+    const double ox = ex > 0 ? ex : 0.0, oy = ey > 0 ? ey : 0.0, oz = ez > 0 ? ez : 0.0;
+    if (ox > 0) pb[0] = W->tc[0] + sx * W->th[0];
+    if (oy > 0) pb[1] = W->tc[1] + sy * W->th[1];
+    if (oz > 0) pb[2] = sz > 0 ? top : bot;
+    if (ox == 0 && oy == 0) { n[2] = sz; return oz; }
+    if (oy == 0 && oz == 0) { n[0] = sx; return ox; }
+    if (ox == 0 && oz == 0) { n[1] = sy; return oy; }
+    const double d = sqrt(ox * ox + oy * oy + oz * oz);
+    n[0] = sx * ox / d; n[1] = sy * oy / d; n[2] = sz * oz / d;
+    return d;
+}
+
 /* top of the static box under (x, y): the table top inside its footprint, else the plane */
 static double ground_z(const world_t* W, const double* P) {
     if (fabs(P[0] - W->tc[0]) <= W->th[0] && fabs(P[1] - W->tc[1]) <= W->th[1]) return W->tc[2] + W->th[2];
@@ -862,17 +893,35 @@ static int detect(const pgx_model* m, const pgx_sim_params* p, const world_t* W,
     int nnp = 0;
     double Rc[9];
     if (W->has_object) {
+        /* round 6: the cube's vertices against the whole table box -- its top and its side walls --
+         * and against the plane's top (candidates: the table's for every vertex, ids 0-7, then the
+         * plane's, ids 8-15).  Rounds 2-5 took each vertex against the top face of the box under it,
+         * so a vertex that crossed the table's edge below the top met the top face from inside, its
+         * whole depth as penetration (a cube knocked over the edge was thrown back up: DESIGN.md
+         * section 2). */
         quat_to_mat(obj + 3, Rc);
         const double h = W->half;
+        double P8[8][3];
         for (int v = 0; v < 8; v++) {
-            double lc[3] = {(v & 1) ? h : -h, (v & 2) ? h : -h, (v & 4) ? h : -h}, P[3];
-            m3_v(Rc, lc, P);
-            for (int i = 0; i < 3; i++) P[i] += obj[i];
-            double zt = ground_z(W, P);
-            double d = P[2] - zt;
-            if (d < (zt == W->plane_z ? W->tau_cube_plane : W->tau_cube_table)) {
-                contact_t c = {0, v, -1, {0, 0, 1}, {P[0], P[1], P[2]}, {P[0], P[1], zt}, d, NULL, 0.0, 0};
-                cand_add(&s0, &c, zt == W->plane_z ? PAIR_PLANE : PAIR_TABLE);
+            double lc[3] = {(v & 1) ? h : -h, (v & 2) ? h : -h, (v & 4) ? h : -h};
+            m3_v(Rc, lc, P8[v]);
+            for (int i = 0; i < 3; i++) P8[v][i] += obj[i];
+        }
+        for (int v = 0; v < 8; v++) {
+            const double* P = P8[v];
+            double n[3], pb[3];
+            const double d = vertex_vs_table(W, P, n, pb);
+            if (d < W->tau_cube_table) {
+                contact_t c = {0, v, -1, {n[0], n[1], n[2]}, {P[0], P[1], P[2]}, {pb[0], pb[1], pb[2]}, d, NULL, 0.0, 0};
+                cand_add(&s0, &c, PAIR_TABLE);
+            }
+        }
+        for (int v = 0; v < 8; v++) {
+            const double* P = P8[v];
+            const double d = P[2] - W->plane_z;
+            if (d < W->tau_cube_plane) {
+                contact_t c = {0, 8 + v, -1, {0, 0, 1}, {P[0], P[1], P[2]}, {P[0], P[1], W->plane_z}, d, NULL, 0.0, 0};
+                cand_add(&s0, &c, PAIR_PLANE);
             }
         }
     }

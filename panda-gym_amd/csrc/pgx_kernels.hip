@@ -833,9 +833,10 @@ struct ContactLdsT {
     /* the object-scene arrays exist in the object tasks' layouts only (ReachAO's two-wave kernel
      * fits its LDS budget without them) */
     static constexpr int G0 = (W == 64 || OBJ) ? CG : 1;
-    /* group 0: object vertices vs table / plane (normal +z) */
+    /* group 0: object vertices vs the table box / the plane top (round 6: the table's side walls too) */
     float4 g0q[G0][4][W];         /* [0] = contact point - object COM; [1 + dir] = (jinv, den, rhs, lambda) */
     float g0d[G0][W], g0id[G0][W];
+    float g0n[G0][3][W];          /* the contact normal, from the table / plane to the cube */
     /* group 1: robot vs table / plane / object / obstacles */
     float g1p[RB][3][W];          /* point on the robot */
     float g1n[RB][3][W];          /* normal, from the other body to the robot */
@@ -927,10 +928,37 @@ __device__ __forceinline__ bool on_table(const PgxDevEnv& e, float x, float y) {
 __device__ __forceinline__ float ground_z(const PgxDevEnv& e, float x, float y) {
     return on_table(e, x, y) ? e.table_top : e.plane_z;
 }
+/* A cube vertex P against the table box (oracle vertex_vs_table, the same rule in fp32): its signed
+ * distance and the normal from the box to P.  Inside, the face of least penetration (the top, then
+ * x, then y on a tie); outside, the closest point of the box -- one face's distance (the top:
+ * exactly P.z - top) when only one coordinate lies outside the box's slab. */
+__device__ __forceinline__ float vertex_vs_table(const PgxDevEnv& e, V3 P, V3& n) {
+    const float bot = e.table_top - 2.0f * e.table_hz;
+    const float qx = P.x - e.table_cx, qy = P.y - e.table_cy;
+    const float ex = fabsf(qx) - e.table_hx, ey = fabsf(qy) - e.table_hy;
+    const float up = P.z - e.table_top, dn = bot - P.z;
+    const bool top = up >= dn;
+    const float ez = top ? up : dn;
+    const float sx = qx < 0.0f ? -1.0f : 1.0f, sy = qy < 0.0f ? -1.0f : 1.0f, sz = top ? 1.0f : -1.0f;
+    if (ex <= 0.0f && ey <= 0.0f && ez <= 0.0f) {
+        if (ez >= ex && ez >= ey) { n = v3(0.0f, 0.0f, sz); return ez; }
+        if (ex >= ey) { n = v3(sx, 0.0f, 0.0f); return ex; }
+        n = v3(0.0f, sy, 0.0f);
+        return ey;
+    }
+    const float ox = fmaxf(ex, 0.0f), oy = fmaxf(ey, 0.0f), oz = fmaxf(ez, 0.0f);
+    if (ox == 0.0f && oy == 0.0f) { n = v3(0.0f, 0.0f, sz); return oz; }
+    if (oy == 0.0f && oz == 0.0f) { n = v3(sx, 0.0f, 0.0f); return ox; }
+    if (ox == 0.0f && oz == 0.0f) { n = v3(0.0f, sy, 0.0f); return oy; }
+    const float d = sqrtf(ox * ox + oy * oy + oz * oz);
+    const float inv = 1.0f / d;
+    n = v3(sx * ox * inv, sy * oy * inv, sz * oz * inv);
+    return d;
+}
 
 /* keep the CG deepest candidates of group 0 (stable: an equal depth does not displace) */
 template <class LT>
-__device__ __forceinline__ void g0_insert(LT& L, int ln, float d, float id, V3 r) {
+__device__ __forceinline__ void g0_insert(LT& L, int ln, float d, float id, V3 r, V3 n) {
     int c = L.cnt[0][ln], pos;
     if (c < CG) { pos = c; L.cnt[0][ln] = c + 1; }
     else if (d < L.g0d[CG - 1][ln]) pos = CG - 1;
@@ -939,10 +967,12 @@ __device__ __forceinline__ void g0_insert(LT& L, int ln, float d, float id, V3 r
         L.g0d[pos][ln] = L.g0d[pos - 1][ln];
         L.g0id[pos][ln] = L.g0id[pos - 1][ln];
         L.g0q[pos][0][ln] = L.g0q[pos - 1][0][ln];
+        for (int k = 0; k < 3; k++) L.g0n[pos][k][ln] = L.g0n[pos - 1][k][ln];
         pos--;
     }
     L.g0d[pos][ln] = d; L.g0id[pos][ln] = id;
     L.g0q[pos][0][ln] = make_float4(r.x, r.y, r.z, 0.0f);
+    L.g0n[pos][0][ln] = n.x; L.g0n[pos][1][ln] = n.y; L.g0n[pos][2][ln] = n.z;
 }
 template <class LT>
 __device__ __forceinline__ void g1_copy(LT& L, int ln, int to, int from) {
@@ -993,6 +1023,9 @@ __device__ __forceinline__ void sort_groups(LT& L, int ln) {
             float t = L.g0id[j][ln]; L.g0id[j][ln] = L.g0id[j - 1][ln]; L.g0id[j - 1][ln] = t;
             t = L.g0d[j][ln]; L.g0d[j][ln] = L.g0d[j - 1][ln]; L.g0d[j - 1][ln] = t;
             const float4 tq = L.g0q[j][0][ln]; L.g0q[j][0][ln] = L.g0q[j - 1][0][ln]; L.g0q[j - 1][0][ln] = tq;
+            for (int k = 0; k < 3; k++) {
+                const float tn = L.g0n[j][k][ln]; L.g0n[j][k][ln] = L.g0n[j - 1][k][ln]; L.g0n[j - 1][k][ln] = tn;
+            }
         }
     const int c1 = L.cnt[1][ln];
     for (int i = 1; i < c1; i++)
@@ -1645,13 +1678,15 @@ __device__ __forceinline__ void substep_dyn(MRef m, const PgxDevEnv& e, const fl
     if (CONT) { Lp->cnt[0][ln] = 0; Lp->cnt[1][ln] = 0; }
     if (OBJ) { /* object vertices vs the box top under them */
         const float h = e.obj_half;
+        /* every vertex against the table box (ids 0-7), then against the plane's top (ids 8-15) */
 #pragma unroll
-        for (int vtx = 0; vtx < 8; vtx++) {
+        for (int k = 0; k < 16; k++) {
+            const int vtx = k & 7;
             const V3 r = mul(Rc, v3((vtx & 1) ? h : -h, (vtx & 2) ? h : -h, (vtx & 4) ? h : -h));
             const V3 P = ob.p + r;
-            const bool ont = on_table(e, P.x, P.y);
-            const float d = P.z - (ont ? e.table_top : e.plane_z);
-            if (d < (ont ? m.tau_obj_table : m.tau_obj_plane)) g0_insert(*Lp, ln, d, (float)vtx, r);
+            V3 n = v3(0.0f, 0.0f, 1.0f);
+            const float d = k < 8 ? vertex_vs_table(e, P, n) : P.z - e.plane_z;
+            if (d < (k < 8 ? m.tau_obj_table : m.tau_obj_plane)) g0_insert(*Lp, ln, d, (float)k, r, n);
         }
     }
     /* FK fused with the per-link quantities the dynamics need, so the 3x3
@@ -1922,19 +1957,19 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
     D.coll = false;
     if (OBJ) Rc = quat_mat(ob);
     if (CONT) { Lp->cnt[0][es] = 0; Lp->cnt[1][es] = 0; }
-    if (OBJ) { /* object vertices vs the box top under them, lane v tests vertex v: the 4
-                * deepest by (depth, vertex) as g0_insert keeps them, in vertex (= id) order
-                * as sort_groups leaves them */
+    if (OBJ) { /* object vertices vs the table box (lane c < 8: vertex c) and the plane's top (lane c >= 8:
+                * vertex c - 8), the candidates' discovery order and ids as the one-lane walk's: the 4
+                * deepest by (depth, id) as g0_insert keeps them, in id order as sort_groups leaves them */
         const float h = e.obj_half;
         const int vtx = c & 7;
         const V3 r = mul(Rc, v3((vtx & 1) ? h : -h, (vtx & 2) ? h : -h, (vtx & 4) ? h : -h));
         const V3 P = ob.p + r;
-        const bool ont = on_table(e, P.x, P.y);
-        const float d = P.z - (ont ? e.table_top : e.plane_z);
-        const bool cand = c < 8 && d < (ont ? m.tau_obj_table : m.tau_obj_plane);
+        V3 nrm = v3(0.0f, 0.0f, 1.0f);
+        const float d = c < 8 ? vertex_vs_table(e, P, nrm) : P.z - e.plane_z;
+        const bool cand = d < (c < 8 ? m.tau_obj_table : m.tau_obj_plane);
         const float dd = cand ? d : 3.0e38f;
         int rank = 0;
-        sfor<0, 8>([&](auto uc) __attribute__((always_inline)) {
+        sfor<0, 16>([&](auto uc) __attribute__((always_inline)) {
             constexpr int U = decltype(uc)::value;
             const float du = bcast16<U>(dd);
             rank += (du < dd || (du == dd && U < c)) ? 1 : 0;
@@ -1944,8 +1979,9 @@ __device__ __forceinline__ void substep_dyn_g(MRef m, const PgxDevEnv& e, const 
         const int sl = __builtin_popcount(mk & ((1u << (c & 15)) - 1u));
         if (keep) {
             Lp->g0d[sl][es] = d;
-            Lp->g0id[sl][es] = (float)vtx;
+            Lp->g0id[sl][es] = (float)c;
             Lp->g0q[sl][0][es] = make_float4(r.x, r.y, r.z, 0.0f);
+            Lp->g0n[sl][0][es] = nrm.x; Lp->g0n[sl][1][es] = nrm.y; Lp->g0n[sl][2][es] = nrm.z;
         }
         Lp->cnt[0][es] = __builtin_popcount(mk);
         PGX_PROF_MARK(19);
@@ -2362,11 +2398,14 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
                 const V3 r = v3(r4.x, r4.y, r4.z);
                 const float id = L.g0id[k][ln];
                 const float warm = warm_lookup<CG>(L, ln, 0, id, m.warmstart);
+                V3 t1, t2;
+                const V3 nk = lds3(L.g0n[k], ln);
+                plane_space(nk, t1, t2);
 #pragma unroll
                 for (int dir = 0; dir < 3; dir++) {
-                    /* u = +z, -y, +x (btPlaneSpace1(+z)); ang = r x u */
-                    const V3 lin = dir == 0 ? v3(0, 0, 1) : (dir == 1 ? v3(0, -1, 0) : v3(1, 0, 0));
-                    const V3 ang = dir == 0 ? v3(r.y, -r.x, 0) : (dir == 1 ? v3(r.z, 0, -r.x) : v3(0, r.z, -r.y));
+                    /* u = n, then btPlaneSpace1(n); ang = r x u */
+                    const V3 lin = dir == 0 ? nk : (dir == 1 ? t1 : t2);
+                    const V3 ang = cross(r, lin);
                     const float den = inv_m + dot(ang, ang) * inv_i;
                     const float jinv = den > 2.220446e-16f ? fast_rcp(den) : 0.0f;
                     const float rel = dot(lin, vcu) + dot(ang, wcu);
@@ -2547,27 +2586,27 @@ __device__ __forceinline__ void substep(MPtr mp, const PgxDevEnv& e, float* q, f
                         const float4 r4 = L.g0q[k][0][ln];
                         const V3 r = v3(r4.x, r4.y, r4.z);
                         const float ln_n = lam0[k][0];
+                        /* the point's normal (a side wall's since round 6) and btPlaneSpace1 of it */
+                        V3 nk = lds3(L.g0n[k], ln), t1, t2;
+                        nk = act ? nk : v3(0.0f, 0.0f, 1.0f);
+                        plane_space(nk, t1, t2);
 #pragma unroll
                         for (int dir = fr ? 1 : 0; dir < (fr ? 3 : 1); dir++) {
-                            /* u = +z, -y, +x and ang = r x u written out by component: as V3 products
-                             * the zero entries would cost an fma each (x + s * 0 does not fold) */
+                            const V3 u = dir == 0 ? nk : (dir == 1 ? t1 : t2);
+                            const V3 a = cross(r, u);
                             const float4 rw = L.g0q[k][1 + dir][ln];
                             const float jv = rw.x, dn = rw.y, rh = rw.z, lm = lam0[k][dir];
                             const float lo = fr ? -mu * ln_n : 0.0f;
                             const float hi = fr ? mu * ln_n : 1e10f;
-                            float jdv;
-                            if (dir == 0) jdv = dvl.z + (r.y * dvw.x - r.x * dvw.y);
-                            else if (dir == 1) jdv = (r.z * dvw.x - r.x * dvw.z) - dvl.y;
-                            else jdv = dvl.x + (r.z * dvw.y - r.y * dvw.z);
+                            const float jdv = dot(u, dvl) + dot(a, dvw);
                             float delta = rh - jdv * jv;
                             const float nl = __builtin_amdgcn_fmed3f(lm + delta, lo, hi);
                             /* a friction row waits for a positive normal impulse */
                             delta = (!act || (fr && !(ln_n > 0.0f))) ? 0.0f : nl - lm;
                             lam0[k][dir] = lm + delta;
                             const float sm = delta * inv_m, si = delta * inv_i;
-                            if (dir == 0) { dvl.z += sm; dvw.x += si * r.y; dvw.y -= si * r.x; }
-                            else if (dir == 1) { dvl.y -= sm; dvw.x += si * r.z; dvw.z -= si * r.x; }
-                            else { dvl.x += sm; dvw.y += si * r.z; dvw.z -= si * r.y; }
+                            dvl = dvl + sm * u;
+                            dvw = dvw + si * a;
                             resid = fmaxf(resid, fabsf(delta * dn));
                         }
                     }
@@ -2861,16 +2900,21 @@ __device__ __forceinline__ bool substep_g(MPtr mp, const PgxDevEnv& e, float* q,
 #pragma unroll
         for (int p = 0; p < NP; p++) pmu[p] = m.friction;
 #pragma unroll
-        for (int k = 0; k < P0; k++) { /* object vertices vs the box top: object coordinates only */
+        for (int k = 0; k < P0; k++) { /* object vertices vs the table / plane: object coordinates only */
             act[k] = k < n0;
             const float4 r4 = L.g0q[k][0][es];
             const V3 r = v3(r4.x, r4.y, r4.z);
             const float id = L.g0id[k][es];
             const float warm = warm_of(cid0, cim0, IC<CG>{}, id);
+            /* the point's normal (+z on the table top and the plane; a side wall's, round 6) and
+             * btPlaneSpace1 of it */
+            V3 nk = lds3(L.g0n[k], es), t1, t2;
+            nk = act[k] ? nk : v3(0.0f, 0.0f, 1.0f);
+            plane_space(nk, t1, t2);
 #pragma unroll
             for (int dir = 0; dir < 3; dir++) {
-                const V3 lin = dir == 0 ? v3(0, 0, 1) : (dir == 1 ? v3(0, -1, 0) : v3(1, 0, 0));
-                const V3 ang = dir == 0 ? v3(r.y, -r.x, 0) : (dir == 1 ? v3(r.z, 0, -r.x) : v3(0, r.z, -r.y));
+                const V3 lin = dir == 0 ? nk : (dir == 1 ? t1 : t2);
+                const V3 ang = cross(r, lin);
                 const float den = inv_m + dot(ang, ang) * inv_i;
                 const float jinv = den > 2.220446e-16f ? fast_rcp(den) : 0.0f;
                 const float rel = dot(lin, vcu) + dot(ang, wcu);
@@ -4603,6 +4647,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
         for (int k = 0; k < (WIDE ? 0 : CG); k++) {
 #pragma unroll
             for (int qq = 0; qq < 4; qq++) L->g0q[k][qq][ln] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            L->g0n[k][0][ln] = 0.0f; L->g0n[k][1][ln] = 0.0f; L->g0n[k][2][ln] = 1.0f;
 #pragma unroll
             for (int dir = 0; dir < 3; dir++)
 #pragma unroll

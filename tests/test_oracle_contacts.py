@@ -433,3 +433,41 @@ def test_relative_breaking_thresholds(oracle):
         cfg.params.contents.flags = abi.FLAG_GLOBAL_BREAKING
         g = oracle.breaking_thresholds(cfg)
         assert np.all(g["table"][:len(caps)] == 0.02) and g["cube_table"] == 0.02
+
+
+# ---------------------------------------------------------------- the table's side walls
+def test_cube_stops_at_the_table_side_wall(oracle):
+    """Round 6: the cube's vertices meet the whole table box, its side walls included.  A cube on the
+    plane sliding into the table's +x wall (x = 0.25) stops against it instead of being thrown onto
+    the top (rounds 2-5 took each vertex against the top face of the box under it)."""
+    cfg = _cfg()
+    o = _obj((0.25 + 0.02 + 0.03, 0.0, -0.4 + 0.02), vel=(-0.6, 0.0, 0.0))
+    q = np.array(abi.NEUTRAL_Q[:7])
+    qd = np.zeros(7)
+    mot = _motors(oracle, q)
+    vmax = 0.0
+    for _ in range(400):
+        q, qd, o, st = oracle.world_substep(cfg, q, qd, o, mot)
+        vmax = max(vmax, float(np.abs(o[7:10]).max()))
+    assert vmax <= 0.6 + 1e-6, vmax                       # never thrown
+    assert 0.25 + 0.02 - 2e-3 < o[0] < 0.25 + 0.02 + 0.01, o[0]   # resting against the wall
+    assert abs(o[2] - (-0.38)) < 2e-3, o[2]               # still on the plane
+
+
+def test_cube_slides_off_the_table_edge_and_lands(oracle):
+    """A cube sliding over the table's +x edge tips and falls past it at free-fall speeds (0.4 m:
+    ~2.8 m/s), never thrown back up by the top face.  (Its fall is not a parabola: the restated
+    floating base carries btMultiBody's base bias m (w x v) in the spinning base's frame, so a cube
+    that tipped at the edge swings its velocity round as it spins.)"""
+    cfg = _cfg()
+    o = _obj((0.22, 0.0, 0.02), vel=(0.8, 0.0, 0.0))
+    q = np.array(abi.NEUTRAL_Q[:7])
+    qd = np.zeros(7)
+    mot = _motors(oracle, q)
+    vmax, zmax = 0.0, -1.0
+    for _ in range(600):
+        q, qd, o, st = oracle.world_substep(cfg, q, qd, o, mot)
+        vmax = max(vmax, float(np.linalg.norm(o[7:10])))
+        zmax = max(zmax, float(o[2]))
+    assert vmax < 3.5 and zmax < 0.03, (vmax, zmax)
+    assert o[0] > 0.27 and o[2] < -0.05, o[:3]     # over the edge and falling beside the table
