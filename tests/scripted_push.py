@@ -43,9 +43,9 @@ class ScriptedPush:
             self.d = np.stack([np.cos(th), np.sin(th), np.zeros_like(th)], axis=1)
             self.side = np.stack([-np.sin(th), np.cos(th), np.zeros_like(th)], axis=1)
             self.pre = cube - STAND_OFF * self.d + self.offset[:, None] * self.side
-            # the end of the push, fixed at the start (chasing the cube would shove it off the table,
-            # where the restated cube -- vertices against the top face under them -- meets the
-            # table's side wall only as a bifurcation)
+            # the end of the push, fixed at the start (chasing the cube would shove it off the table:
+            # a cube falling past the edge is test_cube_at_the_table_side_wall_and_edge's case, with
+            # its own bar -- here the manifold branches of a cube pushed across the table top)
             self.end = cube + 0.12 * self.d + self.offset[:, None] * self.side
             # and the cube kept on the table's interior (table x in [-0.85, 0.25], |y| <= 0.35, less the
             # cube and a margin): where the push would cross an edge it goes the other way
@@ -67,7 +67,6 @@ class ScriptedPush:
         tgt = np.where(push, through, tgt)
         a = (tgt - ee) / 0.05 + self.rng.normal(0.0, 0.15, ee.shape)
         # at most 0.6 of the action range while low: the arm pushes the cube instead of kicking it
-        # (a kicked cube can fly off the table's edge, where the restated cube -- its vertices against
-        # the top face under them -- meets the side wall only as a bifurcation)
+        # off the table (see above)
         lim = np.where(down & (not self.rough), 0.6, 1.0)
         return np.clip(a, -lim, lim).astype(np.float32)

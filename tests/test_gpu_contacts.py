@@ -72,14 +72,12 @@ OUTLIER = 1e-3   # per-step errors above this must be explained by the oracle's 
 
 
 def _one_step_errors(pg, oracle, env_id, n, steps, seed, actions=None, lanes=0, outliers=None, full=False,
-                     over=None, envelope=None, pools=None, keep=None, **kw):
+                     over=None, envelope=None, pools=None, **kw):
     """Per step, from the device state copied into the oracle: |device - oracle| of the EE
     position (obs 0:3) and the achieved goal (EE or object position).  With ``outliers`` (a
     list), every sample above OUTLIER is recorded with its oracle input for _self_sensitivity.
     With ``envelope`` (a dict), the fp32 build of the oracle steps from the same state too and
     its deviation from the fp64 oracle lands in envelope["ee"], envelope["ag"].
-    ``keep``: a mask of the env-steps to compare from the oracle's input object rows [n, OBJ_N]
-    (the others count as error 0, no pool comparison, no outlier record; keep.excluded counts them).
     ``kw``: more PandaVecEnv arguments (sim_params, lib_path)."""
     venv = pg.PandaVecEnv(env_id, num_envs=n, device="cuda:0", seed=seed, lanes_per_env=lanes, full_manifold=full,
                           **kw)
@@ -117,22 +115,18 @@ def _one_step_errors(pg, oracle, env_id, n, steps, seed, actions=None, lanes=0, 
             continue
         e_ee = np.abs(obs[:, :3] - out["obs"][:, :3]).max(axis=1)
         e_ag = np.abs(ag - out["ag"]).max(axis=1)
-        kept = np.ones(n, bool) if keep is None else keep(saved[3])
-        if keep is not None:
-            keep.excluded = getattr(keep, "excluded", 0) + int((~kept).sum())
-            e_ee, e_ag = np.where(kept, e_ee, 0.0), np.where(kept, e_ag, 0.0)
         ee_err.append(e_ee)
         ag_err.append(e_ag)
         if o32 is not None:
-            envelope["ee"].append(np.where(kept, np.abs(o32["obs"][:, :3] - out["obs"][:, :3]).max(axis=1), 0.0))
-            envelope["ag"].append(np.where(kept, np.abs(o32["ag"] - out["ag"]).max(axis=1), 0.0))
+            envelope["ee"].append(np.abs(o32["obs"][:, :3] - out["obs"][:, :3]).max(axis=1))
+            envelope["ag"].append(np.abs(o32["ag"] - out["ag"]).max(axis=1))
         if pools is not None and "manifolds" in venv.state():
             # Bullet's persistent manifolds after the step from the same state: the device's and the
             # oracle's pools hold the same points (count and row ids, in pool order)
             from oracle import oracle as orc
 
             dm = venv.state()["manifolds"].cpu().numpy()
-            for i in np.flatnonzero(kept):
+            for i in range(n):
                 cnt = int(dm[0, i])
                 dk = dm[1:1 + cnt * orc.MAN_PT:orc.MAN_PT, i]
                 rk = orc.pool(ref.obj[i])[:, orc.MP_KID]
@@ -299,18 +293,9 @@ def test_persistent_manifold_branches_under_a_scripted_push(pg, oracle, env_id):
         (lambda obs, t: np.concatenate([pol(obs, t), np.zeros((n, 1), np.float32)], axis=1))
     diag = np.zeros(128, np.int64)
     oracle.lib().pgxo_diag_read(diag.ctypes.data_as(C.c_void_p), 1)
-    def on_the_table(obj):
-        """the cube resting on or pushed across the table's top, 3 cm clear of its edges: the restated
-        cube meets the table as its vertices against the top face under them,
-        so a cube at or over the edge -- knocked there by the arm -- meets the side wall only as a
-        bifurcation, which both the oracle and the device then follow chaotically"""
-        return (np.abs(obj[:, 0] + 0.3) < 0.52) & (np.abs(obj[:, 1]) < 0.32) & (obj[:, 2] > 0.015) & (obj[:, 2] < 0.03)
-
     outl, env, pools = [], {}, {}
     ee, ag, final = _one_step_errors(pg, oracle, env_id, n, steps, 3, actions=act, lanes=16, outliers=outl,
-                                     full=True, envelope=env, pools=pools, keep=on_the_table)
-    print(f"\n{env_id}: {on_the_table.excluded} of {n * steps} env-steps off the table's interior (not compared)")
-    assert on_the_table.excluded <= 0.1 * n * steps
+                                     full=True, envelope=env, pools=pools)
     cfg, _keep = outl.pop()
     oracle.lib().pgxo_diag_read(diag.ctypes.data_as(C.c_void_p), 1)
     branches = {"merge": int(diag[121]), "append": int(diag[122]), "replace": int(diag[123]),
