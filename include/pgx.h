@@ -335,6 +335,9 @@ const char* pgx_last_error(void);
 int pgx_obs_dim(const pgx_config* cfg);
 int pgx_action_dim(const pgx_config* cfg);
 
+/* libpgx.so compiles the device constant block in (the robot, pgx_sim_params, the scene's table
+ * box and plane): a cfg that folds to another block fails with PGX_E_UNSUPPORTED, and
+ * libpgx_rtmodel.so (the same kernels reading the handle's block) takes any. */
 int pgx_create(const pgx_config* cfg, int device, pgx_handle* out);
 /* Host only: the device constant block (PgxDevModel, nbytes = its size) pgx_create folds from cfg;
  * the build's generator of the kernels' compile-time defaults uses it. */

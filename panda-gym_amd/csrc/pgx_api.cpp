@@ -324,6 +324,14 @@ static int build_dev_model(const pgx_config* cfg, PgxDevModel* dm) {
         dm->tau_obj_table = (float)std::fmin(t_obj, t_table);
         dm->tau_obj_plane = (float)std::fmin(t_obj, t_plane);
     }
+    dm->table_cx = (float)cfg->table_center[0];   /* (the same values as PgxDevEnv's, pgx_create) */
+    dm->table_cy = (float)cfg->table_center[1];
+    dm->table_hx = (float)cfg->table_half[0];
+    dm->table_hy = (float)cfg->table_half[1];
+    dm->table_top = (float)(cfg->table_center[2] + cfg->table_half[2]);
+    dm->plane_z = (float)cfg->plane_z;
+    dm->table_hz = (float)cfg->table_half[2];
+    dm->scene_pad = 0.0f;
     if (p->flags != 0) return fail(PGX_E_UNSUPPORTED, "modelling flags are oracle-only");
     int rc = check_compiled_tables(*dm);
     if (!rc) rc = check_capsules(m, R, O);

@@ -49,6 +49,10 @@ struct PgxDevModel {
      * and the plane -- the distance within which a point is reported, merged and kept */
     float tau_table[16], tau_plane[16], tau_obj[16], tau_obst[16];
     float tau_obj_table, tau_obj_plane;
+    /* the scene's table box and plane top (pgx_config table_center / table_half / plane_z, as
+     * PgxDevEnv's fields): in the block, the step kernels' table tests fold to constants in the
+     * default build instead of holding kernel-argument values in registers */
+    float table_cx, table_cy, table_hx, table_hy, table_top, plane_z, table_hz, scene_pad;
 };
 
 struct PgxDevEnv {
@@ -132,6 +136,10 @@ int pgx_launch_step_arm(const PgxDevModel* m_device, const PgxDevEnv& e, const P
                         const PgxDevOut& o, void* stream, const char** name);
 int pgx_launch_step(const PgxDevModel* m_device, const PgxDevEnv& e, const PgxDevState& s, const float* action,
                     const PgxDevOut& o, void* stream, const char** name);
+/* the ReachAO step kernels: their own translation unit too (PGX_TU 4, scheduler flags of its own);
+ * e as pgx_launch_step hands it on (perm set), two: the two-wave build, wide: the 16-lane layout */
+int pgx_launch_step_ao(const PgxDevModel* m_device, const PgxDevEnv& e, const PgxDevState& s, const float* action,
+                       const PgxDevOut& o, void* stream, const char** name, bool two, bool wide);
 int pgx_launch_reset(const PgxDevModel* m_device, const PgxDevEnv& e, const PgxDevState& s, const uint8_t* mask,
                      const double* inject_goal, const double* inject_object, const PgxDevOut& o, void* stream);
 int pgx_launch_sample_actions(const PgxDevEnv& e, float* action, uint64_t step, void* stream);

@@ -264,6 +264,14 @@ __device__ __forceinline__ V3 pick_v3(const V3* a) {
 }
 
 /* the 16-lane row's mask of a predicate (bit c = lane c of this env's row) */
+/* the first lane of this lane's row (lane & ~15), recomputed at every use (an opaque mbcnt pair):
+ * threadIdx.x or the row's ballot mask held through the substep loop cost registers there, and
+ * ReachAO's two-wave kernel spilled them to scratch */
+__device__ __forceinline__ int row_base() {
+    unsigned l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return (int)(l & ~(unsigned)(GW - 1));
+}
 __device__ __forceinline__ unsigned row_ballot(bool v) {
     return (unsigned)((__ballot(v) >> (threadIdx.x & ~(unsigned)(GW - 1))) & 0xFFFFull);
 }
@@ -4344,7 +4352,14 @@ __device__ __forceinline__ void ao_write_obs(float* dst, V3 pos, V3 vel, const f
  * neutral pose (pgx_config.ao_capsules_neutral, PgxDevEnv.ao_geo), so a device-drawn reset takes
  * the host restatement's branch at every test and consumes numpy's stream draw for draw.  Round 5
  * ran these tests on the kernel's fp32 capsules, and a seed whose test sat within fp32 rounding of
- * its threshold took the other branch.  Only resets run this code (__noinline__ callers). */
+ * its threshold took the other branch.  Only resets run this code. */
+/* The reset code is inlined (round 6): as __noinline__ calls its frames -- the by-reference
+ * arguments, the callees' stacks -- put 164 B per lane of scratch under ReachAO's step kernels.
+ * Inlined at the end of the step, where little else is live, it costs the substep loop nothing.
+ * -DPGX_AO_CALL=__noinline__ builds the calls for an A/B. */
+#ifndef PGX_AO_CALL
+#define PGX_AO_CALL __forceinline__
+#endif
 constexpr double kAo64Size = 0.05, kAo64Margin = 0.001, kAo64DummyR = 0.05;   /* reach_ao.py AO_SIZE, MARGIN, DUMMY_R */
 constexpr double kAo64GoalMargin = 0.1, kAo64ObstMargin = 0.03;                 /* GOAL_MARGIN, OBST_MARGIN */
 /* decisions the early exits below take only with this much room: the host's value of a capsule-box
@@ -4388,7 +4403,7 @@ __device__ __forceinline__ double ao64_capsule_sphere(D3 A, D3 B, double r, D3 C
  * value is at most the best sample + 1e-7, the projections only lower it) is a hit, and the best
  * sample minus |AB| times the bracket (the exact minimum of the convex box distance is no lower)
  * beyond thr + kAo64Slack is clear; otherwise the full computation decides, as the host's. */
-__device__ __noinline__ bool ao64_capsule_box_within(D3 A, D3 B, double r, D3 c, double s, double thr) {
+__device__ PGX_AO_CALL bool ao64_capsule_box_within(D3 A, D3 B, double r, D3 c, double s, double thr) {
 #pragma clang fp contract(off)
     const D3 hb = d3(s - kAo64Margin, s - kAo64Margin, s - kAo64Margin);
     const D3 ab = d3(B.x - A.x, B.y - A.y, B.z - A.z);
@@ -4429,7 +4444,7 @@ __device__ __noinline__ bool ao64_capsule_box_within(D3 A, D3 B, double r, D3 c,
  * cube's centre is clear without the search.  geo: [PGX_NCAP][7] (A, B, r) at the neutral pose.
  * PAR (wide layout): lane c tests capsule c, the row ballot ORs them. */
 template <bool PAR>
-__device__ __noinline__ bool ao_robot_hit64(const double* __restrict__ geo, int lane, int kind, D3 C, double s,
+__device__ PGX_AO_CALL bool ao_robot_hit64(const double* __restrict__ geo, int lane, int kind, D3 C, double s,
                                             double thr) {
     auto test = [&](int cp) __attribute__((always_inline)) {
         const double* g = geo + 7 * cp;
@@ -4455,16 +4470,17 @@ struct AoDraw {
     uint64_t env;
     uint32_t episode;
     int k;
-    Pcg64* g;
+    bool pcg;   /* draw from g (held here by value: no pointer, so it stays in registers) */
+    Pcg64 g;
 };
 __device__ __forceinline__ double ao_draw(AoDraw& d) {
-    return d.g ? pcg64_next_double(*d.g) : reset_uniform_s(d.seed, d.env, d.episode, d.k++);
+    return d.pcg ? pcg64_next_double(d.g) : reset_uniform_s(d.seed, d.env, d.episode, d.k++);
 }
 __device__ __forceinline__ double ao_uniform(AoDraw& d, double lo, double hi) {
     return uniform_draw(lo, hi, ao_draw(d));
 }
 /* sample_within_hollow_sphere (reach_ao.py:1188-1211) */
-__device__ __noinline__ void ao_hollow_sphere(AoDraw& d, double rmin, double rmax, bool upper, double* out) {
+__device__ PGX_AO_CALL void ao_hollow_sphere(AoDraw& d, double rmin, double rmax, bool upper, double* out) {
     const double pi = 3.14159265358979323846;
     const double phi = ao_uniform(d, 0.0, 2.0 * pi);
     const double theta = upper ? ao_uniform(d, 0.0, 0.5 * pi) : ao_uniform(d, 0.0, pi);
@@ -4493,15 +4509,14 @@ __device__ __forceinline__ AoResetIn ao_reset_in(const PgxDevEnv& e, V3 ee) {
                      e.ao_ee_set ? e.ao_ee[1] : (double)ee.y, e.ao_ee_set ? e.ao_ee[2] : (double)ee.z};
 }
 template <bool PAR, class LT>
-__device__ __noinline__ bool ao_reset(const AoResetIn& in, LT& L, int ln, int lane, uint64_t env, uint32_t episode,
+__device__ PGX_AO_CALL bool ao_reset(const AoResetIn& in, LT& L, int ln, int lane, uint64_t env, uint32_t episode,
                                       const double* inject_goal, const double* inject_obst, double* goal,
                                       uint64_t* rec, bool lead) {
 #pragma clang fp contract(off)
     bool failed = false;   /* set_coll_free_obs gave up: the reference raises StopIteration */
     const double ex = in.ex, ey = in.ey, ez = in.ez;
-    Pcg64 g{0, 0, 0, 0, 0, 0};
-    if (rec) g = pcg64_load(rec);
-    AoDraw d{in.seed, env, episode, 0, rec ? &g : nullptr};
+    AoDraw d{in.seed, env, episode, 0, rec != nullptr, Pcg64{0, 0, 0, 0, 0, 0}};
+    if (rec) d.g = pcg64_load(rec);
     const double* geo = in.geo;
     const D3 tc = d3(geo[7 * PGX_NCAP], geo[7 * PGX_NCAP + 1], geo[7 * PGX_NCAP + 2]);
     const D3 th = d3(geo[7 * PGX_NCAP + 3], geo[7 * PGX_NCAP + 4], geo[7 * PGX_NCAP + 5]);
@@ -4547,10 +4562,10 @@ __device__ __noinline__ bool ao_reset(const AoResetIn& in, LT& L, int ln, int la
         failed = failed || !placed;
         L.aoC[o][0][ln] = (float)P[0]; L.aoC[o][1][ln] = (float)P[1]; L.aoC[o][2][ln] = (float)P[2];
     }
-    const int n_active = 4 + (rec ? (int)pcg64_bounded(g, 1u) : (int)(ao_draw(d) * 2.0));
+    const int n_active = 4 + (rec ? (int)pcg64_bounded(d.g, 1u) : (int)(ao_draw(d) * 2.0));
     int perm[AO_N] = {0, 1, 2, 3, 4, 5};
     for (int j = AO_N - 1; j > 0; j--) {   /* Fisher-Yates, unrolled so perm stays in VGPRs */
-        int r = rec ? (int)pcg64_interval(g, (uint32_t)j) : (int)(ao_draw(d) * (double)(j + 1));
+        int r = rec ? (int)pcg64_interval(d.g, (uint32_t)j) : (int)(ao_draw(d) * (double)(j + 1));
         r = r > j ? j : r;
         int pj = 0, pr = 0;
 #pragma unroll
@@ -4567,7 +4582,7 @@ __device__ __noinline__ bool ao_reset(const AoResetIn& in, LT& L, int ln, int la
     if (inject_obst)
         for (int o = 0; o < AO_N; o++)
             for (int k = 0; k < 3; k++) L.aoC[o][k][ln] = (float)inject_obst[3 * o + k];
-    if (rec && lead && !inject_goal && !inject_obst) pcg64_store(g, rec);
+    if (rec && lead && !inject_goal && !inject_obst) pcg64_store(d.g, rec);
     return failed && !inject_obst;
 }
 
@@ -4801,9 +4816,20 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
 #pragma unroll
         for (int j = 0; j < NJ; j++) qprev[j] = lds_ld(&L->lqs[qslot][j][ln]);
     }
+    /* the env's row again after the substep loop, from the block and the lane (laundered) and the
+     * heavy-first permutation (an atomic load, never merged with the prologue's): neither i nor
+     * the prologue's row addresses stay live through the loop (ReachAO's two-wave kernel spilled
+     * them to scratch, a dirty line per wave written back at every launch) */
+    int ie;
+    {
+        int lnx = ln;
+        asm volatile("" : "+v"(lnx));
+        const int sl = ((e.perm && e.perm_segs == 1) ? (int)blockIdx.x : xcd_block()) * (WIDE ? EPW : 64) + lnx;
+        ie = e.perm ? __hip_atomic_load(&e.perm[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : sl;
+    }
     double goal[3];   /* read after the substep loop: not live across it */
 #pragma unroll
-    for (int c = 0; c < 3; c++) goal[c] = s.goal[c * N + ii];
+    for (int c = 0; c < 3; c++) goal[c] = s.goal[c * N + ie];
     V3 pos, vel;
     ee_state_cached(*fresh(mp), qprev, q, qd, pos, vel);
 #ifdef PGX_NAN_TRAP
@@ -4823,17 +4849,17 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     } else {
         rew = e.reward == 0 ? -((d > e.distance_threshold) ? 1.0f : 0.0f) : -(float)d;
     }
-    int el = s.elapsed[i] + 1;
-    uint32_t episode = s.episode[i];
+    int el = s.elapsed[ie] + 1;
+    uint32_t episode = s.episode[ie];
     /* TimeLimit, ReachAO.is_truncated (collision); terminate_on_success (core.py:359-361) */
     const bool trunc = (e.max_episode_steps > 0 && el >= e.max_episode_steps) || collided;
     const bool term = e.terminate_on_success && succ;
     if (lead) {
-        if (o.reward) o.reward[i] = rew;
-        if (o.success) o.success[i] = succ;
-        if (o.terminated) o.terminated[i] = term;
-        if (o.truncated) o.truncated[i] = trunc;
-        if (o.task_truncated) o.task_truncated[i] = collided;
+        if (o.reward) o.reward[ie] = rew;
+        if (o.success) o.success[ie] = succ;
+        if (o.terminated) o.terminated[ie] = term;
+        if (o.truncated) o.truncated[ie] = trunc;
+        if (o.task_truncated) o.task_truncated[ie] = collided;
     }
     if constexpr (AO) {
         if constexpr (WIDE) ao_link_obs_g(*L, ln, c);
@@ -4841,16 +4867,16 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     }
     if (trunc || term) {
         if (o.terminal_obs && lead) {
-            if constexpr (AO) ao_write_obs(o.terminal_obs + (size_t)i * od, pos, vel, q, qd, *L, ln);
-            else write_obs<OBJ>(e, o.terminal_obs + (size_t)i * od, pos, vel, ob);
+            if constexpr (AO) ao_write_obs(o.terminal_obs + (size_t)ie * od, pos, vel, q, qd, *L, ln);
+            else write_obs<OBJ>(e, o.terminal_obs + (size_t)ie * od, pos, vel, ob);
         }
         if (o.terminal_ag && lead) {
-            o.terminal_ag[3 * (size_t)i] = ag.x; o.terminal_ag[3 * (size_t)i + 1] = ag.y;
-            o.terminal_ag[3 * (size_t)i + 2] = ag.z;
+            o.terminal_ag[3 * (size_t)ie] = ag.x; o.terminal_ag[3 * (size_t)ie + 1] = ag.y;
+            o.terminal_ag[3 * (size_t)ie + 2] = ag.z;
         }
         if (o.terminal_dg && lead) {
-            o.terminal_dg[3 * (size_t)i] = (float)goal[0]; o.terminal_dg[3 * (size_t)i + 1] = (float)goal[1];
-            o.terminal_dg[3 * (size_t)i + 2] = (float)goal[2];
+            o.terminal_dg[3 * (size_t)ie] = (float)goal[0]; o.terminal_dg[3 * (size_t)ie + 1] = (float)goal[1];
+            o.terminal_dg[3 * (size_t)ie + 2] = (float)goal[2];
         }
     }
     /* SB3 VecEnv auto-reset of a finished env (off for a single gymnasium env: no_auto_reset) */
@@ -4861,9 +4887,9 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
             for (int j = 0; j < NJ; j++) { q[j] = mr.neutral_q[j]; qd[j] = 0.0f; qprev[j] = q[j]; }
             ee_state(mr, q, qd, pos, vel);
             ao_caps(mr, q, *L, ln);
-            uint64_t* rec = (e.pcg_on != nullptr && *e.pcg_on != 0) ? e.pcg + PGX_PCG64_WORDS * (size_t)i : nullptr;
+            uint64_t* rec = (e.pcg_on != nullptr && *e.pcg_on != 0) ? e.pcg + PGX_PCG64_WORDS * (size_t)ie : nullptr;
             const AoResetIn rin = ao_reset_in(e, pos);
-            if (ao_reset<WIDE != 0>(rin, *L, ln, c, e.env_id_offset + (uint64_t)i, episode, nullptr, nullptr, goal, rec,
+            if (ao_reset<WIDE != 0>(rin, *L, ln, c, e.env_id_offset + (uint64_t)ie, episode, nullptr, nullptr, goal, rec,
                                     lead) &&
                 lead)
                 atomicOr(s.errors, PGX_ERR_AO_OBSTACLE);
@@ -4871,7 +4897,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
             if constexpr (WIDE) ao_link_obs_g(*L, ln, c);
             else ao_link_obs(*L, ln);
         } else {
-            reset_env<OBJ>(m, e, i, episode, nullptr, nullptr, q, qd, goal, ob, lead);
+            reset_env<OBJ>(m, e, ie, episode, nullptr, nullptr, q, qd, goal, ob, lead);
             ee_state(m, q, qd, pos, vel);
 #pragma unroll
             for (int j = 0; j < NJ; j++) qprev[j] = q[j];   /* resetJointState refreshes the link cache */
@@ -4888,9 +4914,9 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     if constexpr (PERS) {   /* the pool back, point p by lane p */
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         const int mc = L->mcnt[ln];
-        if (lead) s.man[i] = (float)mc;
+        if (lead) s.man[ie] = (float)mc;
         if (c < mc) {
-            float* b = s.man + (size_t)(1 + PGX_MANIFOLD_POINT * c) * N + i;
+            float* b = s.man + (size_t)(1 + PGX_MANIFOLD_POINT * c) * N + ie;
             b[0] = L->mkid[c][ln];
 #pragma unroll
             for (int t = 0; t < 3; t++) {
@@ -4905,30 +4931,30 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     const V3 ag2 = OBJ ? ob.p : pos;
     if (!lead) return;
     if (o.obs) {
-        if constexpr (AO) ao_write_obs(o.obs + (size_t)i * od, pos, vel, q, qd, *L, ln);
-        else write_obs<OBJ>(e, o.obs + (size_t)i * od, pos, vel, ob);
+        if constexpr (AO) ao_write_obs(o.obs + (size_t)ie * od, pos, vel, q, qd, *L, ln);
+        else write_obs<OBJ>(e, o.obs + (size_t)ie * od, pos, vel, ob);
     }
-    if (o.ag) { o.ag[3 * (size_t)i] = ag2.x; o.ag[3 * (size_t)i + 1] = ag2.y; o.ag[3 * (size_t)i + 2] = ag2.z; }
+    if (o.ag) { o.ag[3 * (size_t)ie] = ag2.x; o.ag[3 * (size_t)ie + 1] = ag2.y; o.ag[3 * (size_t)ie + 2] = ag2.z; }
     if (o.dg) {
-        o.dg[3 * (size_t)i] = (float)goal[0]; o.dg[3 * (size_t)i + 1] = (float)goal[1];
-        o.dg[3 * (size_t)i + 2] = (float)goal[2];
+        o.dg[3 * (size_t)ie] = (float)goal[0]; o.dg[3 * (size_t)ie + 1] = (float)goal[1];
+        o.dg[3 * (size_t)ie + 2] = (float)goal[2];
     }
 #pragma unroll
     for (int j = 0; j < NJ; j++) {
-        s.q[j * N + i] = q[j];
-        s.qd[j * N + i] = qd[j];
-        s.qc[j * N + i] = qprev[j];
+        s.q[j * N + ie] = q[j];
+        s.qd[j * N + ie] = qd[j];
+        s.qc[j * N + ie] = qprev[j];
     }
 #pragma unroll
-    for (int c = 0; c < 3; c++) s.goal[c * N + i] = goal[c];
-    if (OBJ) store_obj(s, N, i, ob);
-    if constexpr (AO) ao_store(s, N, i, *L, ln);
+    for (int c = 0; c < 3; c++) s.goal[c * N + ie] = goal[c];
+    if (OBJ) store_obj(s, N, ie, ob);
+    if constexpr (AO) ao_store(s, N, ie, *L, ln);
     if (CONT) {
 #pragma unroll
-        for (int k = 0; k < CACHE_K; k++) s.contacts[k * N + i] = L->cache[k][ln];
+        for (int k = 0; k < CACHE_K; k++) s.contacts[k * N + ie] = L->cache[k][ln];
     }
-    s.elapsed[i] = el;
-    s.episode[i] = episode;
+    s.elapsed[ie] = el;
+    s.episode[ie] = episode;
 #ifdef PGX_PROF
     PGX_PROF_MARK(6);
     if (threadIdx.x == 0) {
@@ -4942,6 +4968,16 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
 #endif
 }
 
+/* the step kernels take the table / plane geometry from the constant block (equal to the env's,
+ * pgx_create): compile-time constants in the default build rather than kernel arguments the
+ * register allocator holds in VGPRs through the substep loop (ReachAO's two-wave kernel spilled
+ * three of them) */
+template <int AO>
+__device__ __forceinline__ void scene_from_model(PgxDevEnv& e, const PgxDevModel* mdev) {
+    MRef m = *model_ptr<AO>(mdev);
+    e.table_cx = m.table_cx; e.table_cy = m.table_cy; e.table_hx = m.table_hx; e.table_hy = m.table_hy;
+    e.table_top = m.table_top; e.plane_z = m.plane_z; e.table_hz = m.table_hz;
+}
 /* The step kernel at one wave per SIMD (all of the register file: no spills; the batch
  * fills the chip only to one wave per SIMD, 4096 envs in the wide layout) and at two
  * (register budget 256, some spilled to scratch): beyond 1024 waves a second wave per
@@ -4951,11 +4987,13 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
 template <int CONTROL, int OBJ, int CONT, int AO, int WIDE>
 __global__ __launch_bounds__(64) void step_kernel(const PgxDevModel* __restrict__ mdev, PgxDevEnv e, PgxDevState s,
                                                   const float* __restrict__ action, PgxDevOut o) {
+    scene_from_model<AO>(e, mdev);
     step_body<CONTROL, OBJ, CONT, AO, WIDE>(mdev, e, s, action, o);
 }
 template <int CONTROL, int OBJ, int CONT, int AO, int WIDE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void step_kernel_o2(
     const PgxDevModel* __restrict__ mdev, PgxDevEnv e, PgxDevState s, const float* __restrict__ action, PgxDevOut o) {
+    scene_from_model<AO>(e, mdev);
     step_body<CONTROL, OBJ, CONT, AO, WIDE, AO ? 0 : 2>(mdev, e, s, action, o);
 }
 
@@ -5143,11 +5181,14 @@ __global__ __launch_bounds__(SORT_BLOCK) void env_sort_scatter_kernel(int N, con
 
 }  // namespace
 
-/* PGX_TU splits the library into two translation units (Makefile): 1 holds the arm-only
+/* PGX_TU splits the library into translation units (Makefile): 1 holds the arm-only
  * step kernels (Reach, both control modes), compiled with SLP vectorisation -- packed
  * fp32 (v_pk_fma/add/mul_f32) in the redundant per-lane kinematics and dynamics, -2 % on the
- * headline kernel; 2 holds everything else, compiled without it (the object tasks' register
- * pressure turns the packed pairs into scratch spills).  0 = one unit (the profiling build). */
+ * headline kernel; 4 the ReachAO step kernels, with the scheduler's alternative register
+ * pressure trackers (its two-wave build spills less: DESIGN.md section 4); 2 everything else,
+ * compiled without SLP (the object tasks' register pressure turns the packed pairs into scratch
+ * spills).  0 = one unit (the profiling build); 3 = no launcher (tools/ru_one.sh instantiates one
+ * kernel for a register / scratch report). */
 #ifndef PGX_TU
 #define PGX_TU 0
 #endif
@@ -5167,7 +5208,19 @@ __global__ __launch_bounds__(SORT_BLOCK) void env_sort_scatter_kernel(int N, con
             PGX_STEP(C, O, K, A, W);                                                                  \
         }                                                                                             \
     } while (0)
-#if PGX_TU != 2
+#if PGX_TU == 4 || PGX_TU == 0
+int pgx_launch_step_ao(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState& s, const float* action,
+                       const PgxDevOut& o, void* stream, const char** name, bool two, bool wide) {
+    hipStream_t st = (hipStream_t)stream;
+    const int per_block = wide ? EPW : 64;
+    dim3 block(64), grid((e.n_envs + per_block - 1) / per_block);
+    if (wide && e.full_manifold) PGX_STEP2(1, 0, 1, 1, 2);
+    else if (wide) PGX_STEP2(1, 0, 1, 1, 1);
+    else PGX_STEP(1, 0, 1, 1, 0);
+    return (int)hipGetLastError();
+}
+#endif
+#if PGX_TU != 2 && PGX_TU != 3 && PGX_TU != 4
 int pgx_launch_step_arm(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState& s, const float* action,
                         const PgxDevOut& o, void* stream, const char** name) {
     hipStream_t st = (hipStream_t)stream;
@@ -5194,7 +5247,7 @@ int pgx_launch_step_arm(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevSt
     return (int)hipGetLastError();
 }
 #endif
-#if PGX_TU != 1
+#if PGX_TU != 1 && PGX_TU != 3 && PGX_TU != 4
 int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState& s, const float* action,
                     const PgxDevOut& o, void* stream, const char** name) {
     if (!e.ao && !e.has_object) return pgx_launch_step_arm(m, e, s, action, o, stream, name);
@@ -5203,7 +5256,7 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
     const int per_block = wide ? EPW : 64;
     dim3 block(64), grid((e.n_envs + per_block - 1) / per_block);
     const bool two = e.wave_mode == 2 || (e.wave_mode == 0 && wide && grid.x > 1024);   /* more waves than SIMDs */
-    const int variant = e.ao ? 13 : e.control * 4 + (e.has_object ? 2 : 0) + (e.contacts ? 1 : 0);
+    const int variant = e.control * 4 + (e.has_object ? 2 : 0) + (e.contacts ? 1 : 0);
     if (wide && e.full_manifold) {
         /* heavy-first order when the waves do not all fit at once (one per SIMD in the object
          * kernels, two in ReachAO's) */
@@ -5230,21 +5283,20 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
          * 32 KB of LDS per wave lets only 5 of the two-wave build's 8 waves per CU in, and at 256
          * registers it spills 676 B per lane (PickAndPlace 16384: 8.54 ms two-wave, 4.51 ms one
          * wave, profiles/r04/ab_full_waves_start.log) */
+        if (e.ao) return pgx_launch_step_ao(m, e, s, action, o, stream, name, two, true);
         switch (variant) {
             case 3: PGX_STEP(0, 1, 1, 0, 2); break;
             case 7: PGX_STEP(1, 1, 1, 0, 2); break;
-            case 13: PGX_STEP2(1, 0, 1, 1, 2); break;
             default: return (int)hipErrorInvalidValue;
         }
         return (int)hipGetLastError();
     }
+    if (e.ao) return pgx_launch_step_ao(m, e, s, action, o, stream, name, two, wide);
     switch (variant * 2 + wide) {
         case 6: PGX_STEP(0, 1, 1, 0, 0); break;
         case 7: PGX_STEP2(0, 1, 1, 0, 1); break;
         case 14: PGX_STEP(1, 1, 1, 0, 0); break;
         case 15: PGX_STEP2(1, 1, 1, 0, 1); break;
-        case 26: PGX_STEP(1, 0, 1, 1, 0); break;
-        case 27: PGX_STEP2(1, 0, 1, 1, 1); break;
         default: return (int)hipErrorInvalidValue;   /* object without contacts: rejected at create */
     }
     return (int)hipGetLastError();
@@ -5285,7 +5337,7 @@ int pgx_launch_set_word(int32_t* p, int32_t v, void* stream) {
     hipLaunchKernelGGL(set_word_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, p, v);
     return (int)hipGetLastError();
 }
-#endif  /* PGX_TU != 1 */
+#endif  /* PGX_TU 0 or 2 */
 #undef PGX_STEP
 #undef PGX_STEP2
 #undef PGX_KNAME

@@ -376,7 +376,13 @@ def test_obstacle_sampling_failure_raises(pg, monkeypatch):
     """The device reset of set_coll_free_obs gives up after 10000 draws like the reference, which
     raises StopIteration there (reach_ao.py:1143-1145): the kernel sets PGX_ERR_AO_OBSTACLE in the
     handle's errors word, the SB3 path (reset / step_wait) raises PgxError on it, the device path
-    leaves it for raise_device_errors().  A table swallowing the workspace makes every draw fail."""
+    leaves it for raise_device_errors().  A table swallowing the workspace makes every draw fail --
+    through the runtime-model library, since the default one compiles the scene's table in."""
+    import os
+
+    from panda_gym_amd import _native
+
+    rt = os.path.join(os.path.dirname(_native.LIB_PATH), "libpgx_rtmodel.so")
     make_config = pg.abi.make_config
 
     def huge_table(*a, **k):
@@ -386,7 +392,7 @@ def test_obstacle_sampling_failure_raises(pg, monkeypatch):
         return c
 
     monkeypatch.setattr(pg.abi, "make_config", huge_table)
-    venv = pg.PandaVecEnv(ENV, num_envs=2, device="cuda:0", seed=1)
+    venv = pg.PandaVecEnv(ENV, num_envs=2, device="cuda:0", seed=1, lib_path=rt)
     monkeypatch.undo()
     venv.state()["errors"].zero_()        # the construction reset already failed
     venv.reset_tensors()                  # device path: flagged, not raised

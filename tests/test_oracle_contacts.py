@@ -424,12 +424,15 @@ def test_relative_breaking_thresholds(oracle):
         lib = load()
         import ctypes as C
         lib.pgx_dev_model_bytes.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
-        buf = np.zeros(312, dtype=np.float32)
+        buf = np.zeros(320, dtype=np.float32)
         assert lib.pgx_dev_model_bytes(C.byref(cfg), buf.ctypes.data_as(C.c_void_p), buf.nbytes) == 0
         for k, name in enumerate(("table", "plane", "cube", "obstacle")):
             dev = buf[246 + 16 * k: 246 + 16 * k + len(caps)]
             assert np.array_equal(dev, thr[name][:len(caps)].astype(np.float32)), name
         assert buf[310] == np.float32(thr["cube_table"]) and buf[311] == np.float32(thr["cube_plane"])
+        # then the scene's table box and plane top (round 6: compile-time in the default build)
+        tc, th = np.array(cfg.table_center[:]), np.array(cfg.table_half[:])
+        assert np.array_equal(buf[312:319], np.float32([tc[0], tc[1], th[0], th[1], tc[2] + th[2], cfg.plane_z, th[2]]))
         cfg.params.contents.flags = abi.FLAG_GLOBAL_BREAKING
         g = oracle.breaking_thresholds(cfg)
         assert np.all(g["table"][:len(caps)] == 0.02) and g["cube_table"] == 0.02
