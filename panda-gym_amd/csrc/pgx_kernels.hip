@@ -4820,8 +4820,8 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
      * heavy-first permutation (an atomic load, never merged with the prologue's): neither i nor
      * the prologue's row addresses stay live through the loop (ReachAO's two-wave kernel spilled
      * them to scratch, a dirty line per wave written back at every launch) */
-    int ie;
-    {
+    int ie = i;
+    if constexpr (AO) {   /* (ReachAO only: the headline kernel measured +0.9 % with it, profiles/r06/ab_v19.log) */
         int lnx = ln;
         asm volatile("" : "+v"(lnx));
         const int sl = ((e.perm && e.perm_segs == 1) ? (int)blockIdx.x : xcd_block()) * (WIDE ? EPW : 64) + lnx;
@@ -4829,7 +4829,7 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
     }
     double goal[3];   /* read after the substep loop: not live across it */
 #pragma unroll
-    for (int c = 0; c < 3; c++) goal[c] = s.goal[c * N + ie];
+    for (int c = 0; c < 3; c++) goal[c] = s.goal[c * N + (AO ? ie : ii)];
     V3 pos, vel;
     ee_state_cached(*fresh(mp), qprev, q, qd, pos, vel);
 #ifdef PGX_NAN_TRAP
@@ -4968,12 +4968,12 @@ __device__ __forceinline__ void step_body(const PgxDevModel* __restrict__ mdev, 
 #endif
 }
 
-/* the step kernels take the table / plane geometry from the constant block (equal to the env's,
- * pgx_create): compile-time constants in the default build rather than kernel arguments the
- * register allocator holds in VGPRs through the substep loop (ReachAO's two-wave kernel spilled
- * three of them) */
+/* the ReachAO step kernels take the table / plane geometry from the constant block (equal to the
+ * env's, pgx_create): compile-time constants in the default build rather than kernel arguments the
+ * register allocator holds in VGPRs through the substep loop (its two-wave kernel spilled three) */
 template <int AO>
 __device__ __forceinline__ void scene_from_model(PgxDevEnv& e, const PgxDevModel* mdev) {
+    if constexpr (!AO) return;   /* (the arm / object kernels: +0.4 % on the headline, profiles/r06/ab_v19.log) */
     MRef m = *model_ptr<AO>(mdev);
     e.table_cx = m.table_cx; e.table_cy = m.table_cy; e.table_hx = m.table_hx; e.table_hy = m.table_hy;
     e.table_top = m.table_top; e.plane_z = m.plane_z; e.table_hz = m.table_hz;
