@@ -107,6 +107,15 @@ def test_compiled_default_model_is_current():
     h = C.c_void_p()
     assert lib.pgx_create(C.byref(cfg), 0, C.byref(h)) == -3   # PGX_E_UNSUPPORTED
     assert b"compiled for" in lib.pgx_last_error()
+    # the scene's table box is part of the block too (round 6): another table, centre or plane top
+    for field, k, v in (("table_center", 2, -0.25), ("table_half", 0, 0.6), ("plane_z", None, -0.5)):
+        cfg = abi.make_config(abi.EnvSpec(), 8, abi.make_model(load_model("panda_custom0")), abi.default_sim_params())
+        if k is None:
+            setattr(cfg, field, v)
+        else:
+            getattr(cfg, field)[k] = v
+        assert lib.pgx_create(C.byref(cfg), 0, C.byref(h)) == -3, field
+        assert b"compiled for" in lib.pgx_last_error()
     # the substep count is a runtime loop bound, not part of the block
     params = abi.default_sim_params(n_substeps=1)
     cfg = abi.make_config(abi.EnvSpec(), 8, abi.make_model(load_model("panda_custom0")), params)
