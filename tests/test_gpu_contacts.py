@@ -6,9 +6,11 @@ rounding: the fp64 oracle itself moves the EE by up to 7e-5 in one step when its
 perturbed by 1e-7 relative (tools/diag_contacts.py, DESIGN.md "Contacts"), so an fp32 step cannot
 be held to 1e-4 at every contact event and a free-running contact trajectory diverges
 chaotically.  The bar is therefore set per step, from the same state: 99th percentile <= 1e-5 of
-the EE and object positions, and every deviation above 1e-4 must sit where the oracle is itself
-that sensitive to a rounding-level (1e-7 relative) change of its input (test below); plus the
-physical invariants the oracle tests pin (test_oracle_contacts.py) checked on the device.
+the EE and object positions, the 99.9th inside the restated algorithm's own fp32 evaluation, and
+every sample <= 1e-3 under the default physics (round 6; rounds 4-5 let one sample in 2000 reach
+1e-2 where the oracle itself moved as far under a rounding-level, 1e-7 relative, change of its
+input); plus the physical invariants the oracle tests pin (test_oracle_contacts.py) checked on
+the device.
 
 Where the tool bar slides on the table (test_reach_with_table_contacts, the runtime-model friction
 test) the step is worse conditioned since round 4 gave the tool bar its own lateral friction
@@ -223,18 +225,19 @@ def test_reach_with_table_contacts(pg, oracle, lanes):
 def test_random_policy_one_step_parity(pg, oracle, env_id, lanes):
     """p99 <= 1e-5 in both layouts, p99.9 inside the fp32 envelope (round 3: <= 1e-4; with the tool
     bar's friction of round 4 the one-lane Push EE p99.9 measured 1.1e-4 against the fp32 oracle's
-    2.8e-4).  Either layout may exceed 1e-3 (up to 1e-2) only at a contact bifurcation, and only
-    where the oracle itself, from its input perturbed by 1e-7 relative (the fp32 rounding scale),
-    moves by at least the device's deviation (max over 32 trials); at most one such sample per
-    2000.  (Round 3 held the one-lane layout to max <= 1e-3; with the tool bar's friction one
-    one-lane Push sample of 12544 reached 1.7e-3.)"""
+    2.8e-4), and every sample <= 1e-3.  Rounds 4-5 allowed one sample per 2000 up to 1e-2 at a
+    contact bifurcation the oracle itself shows under a 1e-7 relative perturbation of its input
+    (one one-lane Push sample of 12544 reached 1.7e-3); since the cube meets the table's side walls
+    (round 6) the largest is 7.6e-4 (profiles/r06/pytest_gpu_v26.log), and the bar is 1e-3."""
     outl, env = [], {}
     ee, ag, final = _one_step_errors(pg, oracle, env_id, 256, 50, 21, lanes=lanes, outliers=outl, envelope=env)
     cfg, _keep = outl.pop()
     for name, e, f in (("ee", ee, env["ee"]), ("object", ag, env["ag"])):
+        print(f"\n{env_id} {name}: p99 {np.percentile(e, 99):.2e} p99.9 {np.percentile(e, 99.9):.2e} max {e.max():.2e}, "
+              f"{int((e > OUTLIER).sum())} of {e.size} above {OUTLIER:g}")
         assert np.percentile(e, 99) <= 1e-5, (name, np.percentile(e, 99))
         _inside_envelope(name, e, f, pcts=(99.9,))
-        assert e.max() <= 1e-2, (name, e.max())
+        assert e.max() <= OUTLIER, (name, e.max())   # (round 6: 1e-3, was 1e-2)
     assert len(outl) <= ee.size // 2000, len(outl)
     for rec in outl:
         s_ee, s_ag = _self_sensitivity(oracle, cfg, rec, trials=32)
@@ -247,17 +250,20 @@ def test_random_policy_one_step_parity(pg, oracle, env_id, lanes):
 @pytest.mark.parametrize("env_id", ["PandaPush-v3", "PandaPickAndPlace-v3"])
 def test_full_manifold_random_policy_one_step_parity(pg, oracle, env_id):
     """PGX_CONTACTS_FULL (16 lanes, robot budget 12): the same per-step bars as the default
-    budget over a random-policy run in which envs hold more than 4 robot points (the extra
-    rows in LDS), against the oracle at the same budget."""
+    budget (p99 <= 1e-5, p99.9 inside the fp32 envelope, every sample <= 1e-3) over a random-policy
+    run in which envs hold more than 4 robot points (the extra rows in LDS), against the oracle at
+    the same budget."""
     outl, over, env, pools = [], [0], {}, {}
     ee, ag, final = _one_step_errors(pg, oracle, env_id, 256, 50, 21, lanes=16, outliers=outl, full=True, over=over,
                                      envelope=env, pools=pools)
     cfg, _keep = outl.pop()
     assert over[0] > 0, "no env held more than 4 robot points"
     for name, e, f in (("ee", ee, env["ee"]), ("object", ag, env["ag"])):
+        print(f"\n{env_id} {name}: p99 {np.percentile(e, 99):.2e} p99.9 {np.percentile(e, 99.9):.2e} max {e.max():.2e}, "
+              f"{int((e > OUTLIER).sum())} of {e.size} above {OUTLIER:g}")
         assert np.percentile(e, 99) <= 1e-5, (name, np.percentile(e, 99))
         _inside_envelope(name, e, f, pcts=(99.9,))
-        assert e.max() <= 1e-2, (name, e.max())
+        assert e.max() <= OUTLIER, (name, e.max())   # (round 6: 1e-3, was 1e-2)
     assert len(outl) <= ee.size // 2000, len(outl)
     # Bullet's persistent manifolds: device and oracle pools agree point for point after (almost)
     # every step from the same state; a merge / break decision taken at the fp32 rounding edge may
@@ -310,7 +316,7 @@ def test_persistent_manifold_branches_under_a_scripted_push(pg, oracle, env_id):
         print(f"{name}: p99 {np.percentile(e, 99):.2e} p99.9 {np.percentile(e, 99.9):.2e} max {e.max():.2e}")
         _inside_envelope(name, e, f, pcts=(99, 99.9))
         assert np.percentile(e, 99) <= 1e-5, (name, np.percentile(e, 99))
-        assert e.max() <= 1e-2, (name, e.max())
+        assert e.max() <= OUTLIER, (name, e.max())   # (round 6: 1e-3, was 1e-2)
     assert len(outl) <= ee.size // 2000, len(outl)
     for rec in outl:
         s_ee, s_ag = _self_sensitivity(oracle, cfg, rec, trials=64)
