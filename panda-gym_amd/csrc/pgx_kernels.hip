@@ -264,14 +264,6 @@ __device__ __forceinline__ V3 pick_v3(const V3* a) {
 }
 
 /* the 16-lane row's mask of a predicate (bit c = lane c of this env's row) */
-/* the first lane of this lane's row (lane & ~15), recomputed at every use (an opaque mbcnt pair):
- * threadIdx.x or the row's ballot mask held through the substep loop cost registers there, and
- * ReachAO's two-wave kernel spilled them to scratch */
-__device__ __forceinline__ int row_base() {
-    unsigned l;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-    return (int)(l & ~(unsigned)(GW - 1));
-}
 __device__ __forceinline__ unsigned row_ballot(bool v) {
     return (unsigned)((__ballot(v) >> (threadIdx.x & ~(unsigned)(GW - 1))) & 0xFFFFull);
 }
@@ -516,19 +508,47 @@ __device__ __forceinline__ void ik(MPtr mp, const float* q0, V3 target, const fl
         V3 axis = vn > 1e-30f ? (1.0f / vn) * v3(dq[0], dq[1], dq[2]) : v3(1.0f, 0.0f, 0.0f);
         V3 ep = target - x;
         V3 er = angle * axis;
-        V3 jv[NJ], jw[NJ];
-#pragma unroll
-        for (int j = 0; j < NJ; j++) {
-            jw[j] = col(k.R[j], 2);
-            jv[j] = cross(jw[j], x - k.o[j]);
-        }
         float A[NJ][NJ], g[NJ], dth[NJ];
+        if constexpr (PAR) {
+            /* the normal equations across the env's row: lane c < 7 holds Jacobian column c, forms
+             * row c of J^T J (column b broadcast from lane b) and g_c, and the row broadcasts the
+             * lower triangle back to every lane for the (redundant) Cholesky.  The same products
+             * in the same order as the per-lane form below, so the same bits. */
+            V3 zs[NJ], os[NJ];
 #pragma unroll
-        for (int a = 0; a < NJ; a++) {
-            g[a] = dot(jv[a], ep) + dot(jw[a], er);
+            for (int j = 0; j < NJ; j++) { zs[j] = col(k.R[j], 2); os[j] = k.o[j]; }
+            const V3 jwc = pick_v3(zs), jvc = cross(jwc, x - pick_v3(os));
+            const float gc = dot(jvc, ep) + dot(jwc, er);
+            float Ac[NJ];
+            sfor<0, NJ>([&](auto bc) __attribute__((always_inline)) {
+                constexpr int b = decltype(bc)::value;
+                const V3 jvb = v3(bcast16<b>(jvc.x), bcast16<b>(jvc.y), bcast16<b>(jvc.z));
+                const V3 jwb = v3(bcast16<b>(jwc.x), bcast16<b>(jwc.y), bcast16<b>(jwc.z));
+                Ac[b] = dot(jvc, jvb) + dot(jwc, jwb);
+            });
+            sfor<0, NJ>([&](auto ac) __attribute__((always_inline)) {
+                constexpr int a = decltype(ac)::value;
+                g[a] = bcast16<a>(gc);
+                sfor<0, a + 1>([&](auto bc) __attribute__((always_inline)) {
+                    constexpr int b = decltype(bc)::value;
+                    A[a][b] = bcast16<a>(Ac[b]);
+                });
+                A[a][a] += m.ik_damping;
+            });
+        } else {
+            V3 jv[NJ], jw[NJ];
 #pragma unroll
-            for (int b = 0; b <= a; b++) A[a][b] = dot(jv[a], jv[b]) + dot(jw[a], jw[b]);
-            A[a][a] += m.ik_damping;
+            for (int j = 0; j < NJ; j++) {
+                jw[j] = col(k.R[j], 2);
+                jv[j] = cross(jw[j], x - k.o[j]);
+            }
+#pragma unroll
+            for (int a = 0; a < NJ; a++) {
+                g[a] = dot(jv[a], ep) + dot(jw[a], er);
+#pragma unroll
+                for (int b = 0; b <= a; b++) A[a][b] = dot(jv[a], jv[b]) + dot(jw[a], jw[b]);
+                A[a][a] += m.ik_damping;
+            }
         }
         chol7(A);
         chol7_solve(A, g, dth);
