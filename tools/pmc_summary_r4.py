@@ -54,6 +54,10 @@ ROBOT_POINTS = {"pmc_step_kernel": 8, "pmc_object_kernel_push": 12, "pmc_object_
                 "pmc_reach_ao_kernel": 8}   # the per-pair manifold budgets (include/pgx.h)
 
 
+# the pass script of each round's profiles (round 6 reran round 5's, tools/gpu_r6.sh PMC=1)
+PASS_SCRIPT = "pmc_r5.sh"
+
+
 def main(src=os.path.join(ROOT, "gpurun_out", "pmc_r4"), round_tag="r04"):
     rows = []
     for p in sorted(glob.glob(os.path.join(src, "p*", "run_counter_collection.csv"))):
@@ -92,7 +96,7 @@ def main(src=os.path.join(ROOT, "gpurun_out", "pmc_r4"), round_tag="r04"):
             "hbm_bytes_per_launch": hbm, "read_bytes_per_launch": 2.0 * mean.get("FETCH_SIZE", 0.0) * 1024.0,
             "write_bytes_per_launch": mean.get("WRITE_SIZE", 0.0) * 1024.0, "alg_bytes_per_launch": alg,
             "traffic_over_alg": hbm / alg if alg else None,
-            "source": f"tools/pmc_{round_tag[0]}{round_tag[2:]}.sh + tools/pmc_summary_r4.py (rocprofv3 --pmc, one group "
+            "source": f"tools/{PASS_SCRIPT} + tools/pmc_summary_r4.py (rocprofv3 --pmc, one group "
                       f"per run), profiles/{round_tag}/pmc",
         }
         if "SQ_INSTS_VALU" in mean:
