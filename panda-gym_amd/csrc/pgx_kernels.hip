@@ -5278,9 +5278,11 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
     const bool two = e.wave_mode == 2 || (e.wave_mode == 0 && wide && grid.x > 1024);   /* more waves than SIMDs */
     const int variant = e.control * 4 + (e.has_object ? 2 : 0) + (e.contacts ? 1 : 0);
     if (wide && e.full_manifold) {
-        /* heavy-first order when the waves do not all fit at once (one per SIMD in the object
-         * kernels, two in ReachAO's) */
-        const unsigned resident = e.ao ? 2048u : 1024u;
+        /* heavy-first order beyond one wave per SIMD: the object kernels' waves then do not all
+         * fit at once; ReachAO's two-wave kernel shares each SIMD between two waves, and the order
+         * measured faster there too (8192 envs 0.514 -> 0.501 ms, profiles/r06/ab_sort*.log; round 5
+         * had measured it slower, 0.768 -> 0.813, before the kernel shed its scratch) */
+        const unsigned resident = 1024u;
         const bool sort = e.perm_buf && (e.sort_mode == 1 || (e.sort_mode == 0 && grid.x > resident));
         PgxDevEnv es = e;
         es.perm = nullptr;
