@@ -5228,6 +5228,33 @@ __global__ __launch_bounds__(SORT_BLOCK) void env_sort_scatter_kernel(int N, con
             PGX_STEP(C, O, K, A, W);                                                                  \
         }                                                                                             \
     } while (0)
+#if PGX_TU != 3 && PGX_TU != 4
+/* The heavy-first env order of the per-pair manifold launches (wide layout), from 256 waves (1024
+ * envs) on.  Rounds 4-5 sorted only beyond the waves the chip holds at once (longest-first
+ * scheduling); round 6 measured it faster at every batch from 1024 envs, the two sort kernels
+ * (≈ 10 µs) included: Reach 4096 0.380 -> 0.369 ms, Reach 2048 0.376 -> 0.366, Reach 8192 0.587 ->
+ * 0.566, Push 4096 0.935 -> 0.924, PickAndPlace 4096 0.933 -> 0.930, ReachAO 8192 0.514 -> 0.501
+ * (profiles/r06/ab_*sort*.log).  A wave costs its heaviest env's rows times the most sweeps any of
+ * its envs needs; envs of one weight sharing waves leave fewer waves that pay for both. */
+constexpr unsigned kSortMinWaves = 256u;
+/* the heavy-first env order (env_sort_keys_kernel / env_sort_scatter_kernel) into e.perm_buf;
+ * returns the env the step launch reads (perm set) */
+static PgxDevEnv sort_envs(const PgxDevEnv& e, const PgxDevState& s, hipStream_t st) {
+    PgxDevEnv es = e;
+    const int rb = e.has_object ? PGX_ROBOT_POINTS : PGX_ROBOT_POINTS_ARM;
+    const int nb = (e.n_envs + SORT_BLOCK - 1) / SORT_BLOCK;
+    uint8_t* keys = reinterpret_cast<uint8_t*>(e.perm_buf + e.n_envs);
+    int32_t* blk = e.perm_buf + e.n_envs + (e.n_envs + 3) / 4;
+    hipLaunchKernelGGL(env_sort_keys_kernel, dim3(nb), dim3(SORT_BLOCK), 0, st, s, e.n_envs, rb, e.sort_key, keys, blk);
+    /* per-XCD segments when the batch divides: a wave's env rows then stay in one L2's range */
+    const int segs = (e.sort_segs != 1 && e.n_envs % (8 * SORT_BLOCK) == 0) ? 8 : 1;
+    hipLaunchKernelGGL(env_sort_scatter_kernel, dim3(nb), dim3(SORT_BLOCK), 0, st, e.n_envs, (const uint8_t*)keys,
+                       (const int32_t*)blk, e.perm_buf, segs);
+    es.perm = e.perm_buf;
+    es.perm_segs = segs;
+    return es;
+}
+#endif
 #if PGX_TU == 4 || PGX_TU == 0
 int pgx_launch_step_ao(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState& s, const float* action,
                        const PgxDevOut& o, void* stream, const char** name, bool two, bool wide) {
@@ -5249,6 +5276,11 @@ int pgx_launch_step_arm(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevSt
     dim3 block(64), grid((e.n_envs + per_block - 1) / per_block);
     const bool two = e.wave_mode == 2 || (e.wave_mode == 0 && wide && grid.x > 1024);   /* more waves than SIMDs */
     if (wide && e.contacts && e.full_manifold) {   /* Bullet's per-pair manifolds (the default budget) */
+        /* the heavy-first order from 1024 envs (kSortMinWaves), as the object / ReachAO launches */
+        PgxDevEnv es = e;
+        es.perm = nullptr;
+        if (e.perm_buf && (e.sort_mode == 1 || (e.sort_mode == 0 && grid.x >= kSortMinWaves))) es = sort_envs(e, s, st);
+        const PgxDevEnv& e = es;
         if (e.control) PGX_STEP(1, 0, 1, 0, 2);
         else PGX_STEP2(0, 0, 1, 0, 2);
         return (int)hipGetLastError();
@@ -5278,28 +5310,10 @@ int pgx_launch_step(const PgxDevModel* m, const PgxDevEnv& e, const PgxDevState&
     const bool two = e.wave_mode == 2 || (e.wave_mode == 0 && wide && grid.x > 1024);   /* more waves than SIMDs */
     const int variant = e.control * 4 + (e.has_object ? 2 : 0) + (e.contacts ? 1 : 0);
     if (wide && e.full_manifold) {
-        /* heavy-first order beyond one wave per SIMD: the object kernels' waves then do not all
-         * fit at once; ReachAO's two-wave kernel shares each SIMD between two waves, and the order
-         * measured faster there too (8192 envs 0.514 -> 0.501 ms, profiles/r06/ab_sort*.log; round 5
-         * had measured it slower, 0.768 -> 0.813, before the kernel shed its scratch) */
-        const unsigned resident = 1024u;
-        const bool sort = e.perm_buf && (e.sort_mode == 1 || (e.sort_mode == 0 && grid.x > resident));
+        const bool sort = e.perm_buf && (e.sort_mode == 1 || (e.sort_mode == 0 && grid.x >= kSortMinWaves));
         PgxDevEnv es = e;
         es.perm = nullptr;
-        if (sort) {
-            const int rb = e.has_object ? PGX_ROBOT_POINTS : PGX_ROBOT_POINTS_ARM;
-            const int nb = (e.n_envs + SORT_BLOCK - 1) / SORT_BLOCK;
-            uint8_t* keys = reinterpret_cast<uint8_t*>(e.perm_buf + e.n_envs);
-            int32_t* blk = e.perm_buf + e.n_envs + (e.n_envs + 3) / 4;
-            hipLaunchKernelGGL(env_sort_keys_kernel, dim3(nb), dim3(SORT_BLOCK), 0, st, s, e.n_envs, rb, e.sort_key, keys,
-                               blk);
-            /* per-XCD segments when the batch divides: a wave's env rows then stay in one L2's range */
-            const int segs = (e.sort_segs != 1 && e.n_envs % (8 * SORT_BLOCK) == 0) ? 8 : 1;
-            hipLaunchKernelGGL(env_sort_scatter_kernel, dim3(nb), dim3(SORT_BLOCK), 0, st, e.n_envs,
-                               (const uint8_t*)keys, (const int32_t*)blk, e.perm_buf, segs);
-            es.perm = e.perm_buf;
-            es.perm_segs = segs;
-        }
+        if (sort) es = sort_envs(e, s, st);
         const PgxDevEnv& e = es;
         /* the object tasks' per-pair manifold kernels run one wave per SIMD at every batch: their
          * 32 KB of LDS per wave lets only 5 of the two-wave build's 8 waves per CU in, and at 256

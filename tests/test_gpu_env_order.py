@@ -70,7 +70,8 @@ def _run(env_id, n, steps, mode):
 
 
 @pytest.mark.parametrize("env_id,n", [("PandaPush-v3", 67), ("PandaPickAndPlace-v3", 256), ("PandaReachAO-v3", 130),
-                                     ("PandaPickAndPlace-v3", 2048)])   # 2048: eight per-XCD segments
+                                     ("PandaPickAndPlace-v3", 2048),    # 2048: eight per-XCD segments
+                                     ("PandaReach-v3", 130), ("PandaReach-v3", 2048)])   # (round 6: Reach sorts too)
 def test_heavy_first_order_leaves_every_env_bit_identical(env_id, n):
     d_on, heavy, moved = _run(env_id, n, 40, "1")
     d_off, _, _ = _run(env_id, n, 40, "0")
